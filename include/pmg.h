@@ -1,0 +1,195 @@
+/*
+ * pmg.h -- C ABI of libpmg_hip.so, the MI355X (gfx950) engine behind the
+ * PoissonGPLVMJump1D EM hot path of poor-man-GPLVM.
+ *
+ * Conventions
+ *   - every array argument is a DEVICE pointer allocated and owned by the
+ *     caller (PyTorch in the Python host layer), row-major, no padding unless
+ *     the parameter list says so;
+ *   - `stream` is a hipStream_t passed as void* (0 = null stream); all work of
+ *     one call is enqueued on that stream in order and nothing synchronises
+ *     the host unless stated;
+ *   - every entry point returns 0 (PMG_OK) or a negative PMG_E* code; the
+ *     message of the last error on the calling thread is pmg_last_error();
+ *   - no global device state: scratch space is a caller workspace whose size
+ *     comes from the matching *_workspace_size query.
+ *
+ * Each entry point names the reference function it replaces
+ * (/root/reference/poor_man_gplvm/..., file:line).
+ *
+ * Shapes: T time bins, N neurons, L latent bins, D = 2 dynamics
+ * (0 continuous, 1 jump), NB basis columns (incl. bias).
+ */
+#ifndef PMG_H
+#define PMG_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PMG_ABI_VERSION 1
+
+#define PMG_OK 0
+#define PMG_EINVAL (-1)       /* bad shape / argument */
+#define PMG_EHIP (-2)         /* HIP runtime error */
+#define PMG_EUNSUPPORTED (-3) /* configuration outside what the kernels implement */
+#define PMG_ETIMEOUT (-4)     /* a bounded in-kernel spin gave up */
+
+/* spike-preparation flags (written to *flags_out on the device) */
+#define PMG_YFLAG_NONINT 1    /* some y is non-integer, negative or > 127: use the f64 emission */
+#define PMG_YFLAG_MASK 2      /* ma_neuron is not 0/1 */
+
+int pmg_abi_version(void);
+const char* pmg_last_error(void);
+
+/* ------------------------------------------------------------------ */
+/* Spike preparation (once per fit).  Feeds the emission and the       */
+/* sufficient statistics.  Replaces the per-call y handling of          */
+/* decoder.get_loglikelihood_ma_all (decoder.py:60-71) and the y of     */
+/* fit_tuning_helper.get_statistics (fit_tuning_helper.py:28-42).       */
+/*   y        (T,N) f32 spike counts                                     */
+/*   ma_neuron (N) f32 or (T,N) f32 (ma_is_2d) or NULL (all ones)        */
+/*   yq_out   (Tp,Kp) int8, Tp = roundup(T,64), Kp = roundup(N,32):       */
+/*            y*ma (zero padded), the integer emission operand           */
+/*   gconst_out (T) f64: sum_n ma[t,n]*gammaln(y[t,n]+1)                 */
+/*   yext_out (T,Np) f32, Np = roundup(N+1,64): y, then a ones column    */
+/*            (t_w = sum_t P falls out of the same GEMM), zero padded    */
+/*   flags_out (1) int32 device word, OR of PMG_YFLAG_*; zeroed here     */
+int pmg_spikes_prepare(const float* y, int64_t T, int32_t N, const float* ma_neuron,
+                       int32_t ma_is_2d, int8_t* yq_out, int32_t Kp, double* gconst_out,
+                       float* yext_out, int32_t Np, int32_t* flags_out, void* stream);
+
+/* ------------------------------------------------------------------ */
+/* tuning = softplus(basis @ W)   -- fit_tuning_helper.py:19-25,        */
+/* core.py:772-774.  basis (L,NB) f32, W (NB,N) f64;                     */
+/* tuning64 (L,N) f64 and tuning32 (L,N) f32 (either may be NULL).       */
+int pmg_tuning_softplus(const float* basis, const double* W, int32_t L, int32_t NB, int32_t N,
+                        double* tuning64, float* tuning32, void* stream);
+
+/* ------------------------------------------------------------------ */
+/* Poisson emission  -- decoder.get_loglikelihood_ma_poisson            */
+/* (decoder.py:30-48) vmapped by get_loglikelihood_ma_all (:60-71):      */
+/*   ll[t,l] = sum_n m[t,n]*(xlogy(y,lam) - lam - gammaln(y+1)),         */
+/*   lam = tuning*dt + 1e-20, ll = -1e20 where ma_latent == 0.           */
+/* Output is split for an fp32 consumer without losing precision:       */
+/*   delta (T,L) f32 = ll - r[t, l/32],  rblk (T, Lp/32) f64 = max over   */
+/*   the 32-latent block (Lp = roundup(L,32)).                           */
+/* Integer path (flags == 0, 1-D or no mask): exact int8 MFMA            */
+/* (v_mfma_i32_32x32x32_i8) on y and log(lam) in 4 balanced base-256     */
+/* digits of a 2^-24 fixed point.  Generic path: f64.                    */
+size_t pmg_emission_workspace_size(int64_t T, int32_t L, int32_t N);
+int pmg_emission_poisson(const int8_t* yq, const double* gconst, const double* tuning64,
+                         const float* ma_neuron_1d, const uint8_t* ma_latent, double dt,
+                         int64_t T, int32_t L, int32_t N, int32_t Kp, float* delta,
+                         double* rblk, void* workspace, size_t workspace_bytes, void* stream);
+/* Generic f64 emission (non-integer y, weighted or 2-D masks). y (T,N) f32. */
+int pmg_emission_poisson_f64(const float* y, const double* gconst, const double* tuning64,
+                             const float* ma_neuron, int32_t ma_is_2d, const uint8_t* ma_latent,
+                             double dt, int64_t T, int32_t L, int32_t N, float* delta,
+                             double* rblk, void* workspace, size_t workspace_bytes, void* stream);
+/* Per-time reference: m[t] = max_b rblk[t,b], phi[t,b] = f32(s*(rblk[t,b]-m[t])) so that  */
+/* exp(s*ll[t,l] - s*m[t]) = exp(s*delta[t,l] + phi[t,l/32]).                              */
+int pmg_emission_rowref(const double* rblk, int64_t T, int32_t nblk, double likelihood_scale,
+                        float* phi, double* m, void* stream);
+/* ll (T,L) f32 = delta + rblk  (the log_likelihood_all output, decoder.py:307). */
+int pmg_loglik_materialize(const float* delta, const double* rblk, int64_t T, int32_t L,
+                           float* ll, void* stream);
+
+/* ------------------------------------------------------------------ */
+/* Transition description (gp_kernel.create_transition_prob_1d,         */
+/* gp_kernel.py:42-89): continuous kernel K0[i,j] = g[|i-j|]*invz[i]     */
+/* (row-normalised RBF, exactly zero beyond |i-j| > band in the f32       */
+/* arithmetic the reference uses; band <= 32 here), jump kernel 1/L,     */
+/* dynamics A[prev,next].                                                */
+#define PMG_MAX_BAND 32
+typedef struct pmg_transition {
+  int32_t L;
+  int32_t band;                 /* half-width W of the continuous kernel, <= PMG_MAX_BAND */
+  float g[PMG_MAX_BAND + 1];    /* host values: g[k] = exp(-k^2/mv^2), k <= band */
+  const float* invz;            /* (L) DEVICE f32: 1 / sum_j exp(-(i-j)^2/mv^2) */
+  float A[4];                   /* host values A00 A01 A10 A11 */
+} pmg_transition;
+
+/* Chunked, time-parallel forward filter  -- decoder.filter_one_step    */
+/* (decoder.py:151-172) scanned by filter_all_step (:174-187) over the   */
+/* chunk loop of smooth_all_step_combined_ma_chunk (:283-304).           */
+/*   chunk C steps per wave, warm-up B steps from a uniform guess, then   */
+/*   boundary verification (Hilbert metric <= tol) and exact sequential  */
+/*   repair of any chunk whose start state disagreed.                    */
+/* outputs: alpha (T,2,L) f32 normalised filter posteriors;              */
+/*          logc (T) f64 one-step predictive marginals (decoder.py:167); */
+/*          logz (1) f64 = sum_t logc (decoder.py:169).                  */
+size_t pmg_fwdbwd_workspace_size(int64_t T, int32_t L, int32_t chunk);
+int pmg_forward_filter(const float* delta, const float* phi, const double* m, int64_t T,
+                       const pmg_transition* tr, double likelihood_scale, int32_t chunk,
+                       int32_t warmup, double tol, float* alpha, double* logc, double* logz,
+                       void* workspace, size_t workspace_bytes, void* stream);
+/* Chunked, time-parallel backward smoother -- decoder.smooth_one_step   */
+/* (decoder.py:200-226) / smooth_all_step (:230-256) / chunk loop        */
+/* (:313-326), in the equivalent alpha-beta form                          */
+/*   gamma_t = alpha_t * beta_t / sum,  beta_{T-1} = 1,                   */
+/*   beta_t = Trans (e_{t+1} * beta_{t+1}).                               */
+/* outputs (either may be NULL): P (T,L) f32 = sum_d gamma (the dynamics  */
+/* marginal of core.py:668, exponentiated); gamma (T,2,L) f32.            */
+/* rho (T,2,L) f32 (NULL = skip): rho_t = e_t*beta_t/N_{t-1} with         */
+/* N_{t-1} = sum prior_t e_t beta_t, so that the pairwise joint is        */
+/* sum_t alpha_t (x) (Trans .* rho_{t+1}) (decoder.py:215-221).           */
+int pmg_backward_smoother(const float* delta, const float* phi, const float* alpha, int64_t T,
+                          const pmg_transition* tr, double likelihood_scale, int32_t chunk,
+                          int32_t warmup, double tol, float* P, float* gamma, float* rho,
+                          void* workspace, size_t workspace_bytes, void* stream);
+/* number of chunks repaired by the last forward / backward call on this  */
+/* workspace (device int32 pair at a fixed offset; host reads it lazily). */
+size_t pmg_fwdbwd_repair_counter_offset(int64_t T, int32_t L, int32_t chunk);
+
+/* ------------------------------------------------------------------ */
+/* Sufficient statistics -- fit_tuning_helper.get_statistics             */
+/* (fit_tuning_helper.py:28-42): y_w = P^T y (L,N), t_w = sum_t P (L).    */
+/* P (T,L) f32 probabilities; yext from pmg_spikes_prepare.  fp32 MFMA    */
+/* (v_mfma_f32_32x32x2f32) over K-slices, slices summed in f64.           */
+size_t pmg_suffstats_workspace_size(int64_t T, int32_t L, int32_t Np);
+int pmg_suffstats(const float* P, const float* yext, int64_t T, int32_t L, int32_t N, int32_t Np,
+                  double* yw, double* tw, void* workspace, size_t workspace_bytes, void* stream);
+/* P = exp(logp) elementwise (the first M-step's exp at fit_tuning_helper.py:38). */
+int pmg_exp(const float* logp, int64_t n, float* p, void* stream);
+/* out = log(x) elementwise (log-space outputs; log(0) = -inf). */
+int pmg_log(const float* x, int64_t n, float* out, void* stream);
+
+/* ------------------------------------------------------------------ */
+/* Adam M-step -- fit_tuning_helper.make_adam_runner.run                 */
+/* (fit_tuning_helper.py:133-194) on poisson_m_step_objective            */
+/* (:63-81) with optax 0.2.2 adam; one persistent launch, neurons        */
+/* partitioned over workgroups, the stop rule                             */
+/*   i < maxiter-1 and (i < 5 or |loss-loss_prev|/max(|loss|,1e-8) > tol) */
+/* decided from globally summed f64 losses (fixed summation order).      */
+/*   W, mu, nu (NB,N) f64 in/out; count (1) int64 in/out (optax count).  */
+/*   stats (4) f64 out: n_iter, final_loss, final_error, unused.          */
+/*   loss_hist, err_hist (maxiter) f64 out (zeros past n_iter).           */
+typedef struct pmg_adam_cfg {
+  double lr, b1, b2, eps, eps_root;
+  double prior_std;
+  double tol;
+  int32_t maxiter;
+} pmg_adam_cfg;
+size_t pmg_mstep_workspace_size(int32_t N, int32_t maxiter);
+int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const float* basis,
+                   const double* yw, const double* tw, int32_t L, int32_t NB, int32_t N,
+                   const pmg_adam_cfg* cfg, double* stats, double* loss_hist, double* err_hist,
+                   void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------ */
+/* Pairwise joint (decode only) -- the logaddexp accumulation of         */
+/* decoder.smooth_one_step (decoder.py:215-221) as a T-contraction:       */
+/*   S[x,x'] = sum_{t<T-1} alpha_t[x] * rho_{t+1}[x'],  x = (d,i)          */
+/* (2L x 2L f64); the caller forms joint = A[d,d'] K[d',i,j] S.            */
+size_t pmg_joint_workspace_size(int64_t T, int32_t L);
+int pmg_joint_accumulate(const float* alpha, const float* rho, int64_t T, int32_t L, double* S,
+                         void* workspace, size_t workspace_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PMG_H */

@@ -1,0 +1,127 @@
+"""ctypes binding of ``libpmg_hip.so`` (the C ABI declared in ``include/pmg.h``).
+
+PyTorch is imported first so that the library's ``libamdhip64.so.7`` dependency
+resolves to the HIP runtime torch already loaded (one runtime per process);
+device buffers are torch tensors, passed as raw pointers together with the
+current torch stream.  There is no fallback: if the library is missing or fails
+to load, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads the HIP runtime before the library)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "csrc", "libpmg_hip.so")
+
+PMG_MAX_BAND = 32
+ABI_VERSION = 1
+
+# every symbol the header declares (checked by tests/test_capi_symbols.py)
+EXPORTED_SYMBOLS = (
+    "pmg_abi_version", "pmg_last_error", "pmg_spikes_prepare", "pmg_tuning_softplus",
+    "pmg_emission_workspace_size", "pmg_emission_poisson", "pmg_emission_poisson_f64",
+    "pmg_emission_rowref", "pmg_loglik_materialize", "pmg_fwdbwd_workspace_size",
+    "pmg_forward_filter", "pmg_backward_smoother", "pmg_fwdbwd_repair_counter_offset",
+    "pmg_suffstats_workspace_size", "pmg_suffstats", "pmg_exp", "pmg_log",
+    "pmg_mstep_workspace_size", "pmg_mstep_adam", "pmg_joint_workspace_size",
+    "pmg_joint_accumulate",
+)
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+class Transition(ctypes.Structure):
+    """pmg_transition (include/pmg.h)."""
+    _fields_ = [("L", ctypes.c_int32), ("band", ctypes.c_int32),
+                ("g", ctypes.c_float * (PMG_MAX_BAND + 1)), ("invz", ctypes.c_void_p),
+                ("A", ctypes.c_float * 4)]
+
+
+class AdamCfg(ctypes.Structure):
+    """pmg_adam_cfg (include/pmg.h)."""
+    _fields_ = [("lr", ctypes.c_double), ("b1", ctypes.c_double), ("b2", ctypes.c_double),
+                ("eps", ctypes.c_double), ("eps_root", ctypes.c_double),
+                ("prior_std", ctypes.c_double), ("tol", ctypes.c_double),
+                ("maxiter", ctypes.c_int32)]
+
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int32
+_D = ctypes.c_double
+_SZ = ctypes.c_size_t
+
+_SIGS = {
+    "pmg_abi_version": ([], _I32),
+    "pmg_last_error": ([], ctypes.c_char_p),
+    "pmg_spikes_prepare": ([_P, _I64, _I32, _P, _I32, _P, _I32, _P, _P, _I32, _P, _P], _I32),
+    "pmg_tuning_softplus": ([_P, _P, _I32, _I32, _I32, _P, _P, _P], _I32),
+    "pmg_emission_workspace_size": ([_I64, _I32, _I32], _SZ),
+    "pmg_emission_poisson": ([_P, _P, _P, _P, _P, _D, _I64, _I32, _I32, _I32, _P, _P, _P, _SZ, _P], _I32),
+    "pmg_emission_poisson_f64": ([_P, _P, _P, _P, _I32, _P, _D, _I64, _I32, _I32, _P, _P, _P, _SZ, _P], _I32),
+    "pmg_emission_rowref": ([_P, _I64, _I32, _D, _P, _P, _P], _I32),
+    "pmg_loglik_materialize": ([_P, _P, _I64, _I32, _P, _P], _I32),
+    "pmg_fwdbwd_workspace_size": ([_I64, _I32, _I32], _SZ),
+    "pmg_forward_filter": ([_P, _P, _P, _I64, ctypes.POINTER(Transition), _D, _I32, _I32, _D,
+                            _P, _P, _P, _P, _SZ, _P], _I32),
+    "pmg_backward_smoother": ([_P, _P, _P, _I64, ctypes.POINTER(Transition), _D, _I32, _I32, _D,
+                               _P, _P, _P, _P, _SZ, _P], _I32),
+    "pmg_fwdbwd_repair_counter_offset": ([_I64, _I32, _I32], _SZ),
+    "pmg_suffstats_workspace_size": ([_I64, _I32, _I32], _SZ),
+    "pmg_suffstats": ([_P, _P, _I64, _I32, _I32, _I32, _P, _P, _P, _SZ, _P], _I32),
+    "pmg_exp": ([_P, _I64, _P, _P], _I32),
+    "pmg_log": ([_P, _I64, _P, _P], _I32),
+    "pmg_mstep_workspace_size": ([_I32, _I32], _SZ),
+    "pmg_mstep_adam": ([_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, ctypes.POINTER(AdamCfg),
+                        _P, _P, _P, _P, _SZ, _P], _I32),
+    "pmg_joint_workspace_size": ([_I64, _I32], _SZ),
+    "pmg_joint_accumulate": ([_P, _P, _I64, _I32, _P, _P, _SZ, _P], _I32),
+}
+
+_lib = None
+
+
+def load(path: str | None = None):
+    """Load (once) and return the library with typed entry points."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise NativeError(f"libpmg_hip.so not found at {p}; run __graft_entry__.build() "
+                          "(make -C poor_man_gplvm_amd/csrc)")
+    lib = ctypes.CDLL(p)
+    for name, (argt, rest) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argt
+        fn.restype = rest
+    if lib.pmg_abi_version() != ABI_VERSION:
+        raise NativeError(f"ABI mismatch: library {lib.pmg_abi_version()} != {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().pmg_last_error()
+        raise NativeError(f"{what} failed (rc={rc}): {msg.decode() if msg else ''}")
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a torch tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise NativeError("expected a device tensor")
+    if not t.is_contiguous():
+        raise NativeError("expected a contiguous tensor")
+    return t.data_ptr()
+
+
+def stream_handle() -> int:
+    return torch.cuda.current_stream().cuda_stream

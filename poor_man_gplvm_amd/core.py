@@ -1,0 +1,468 @@
+"""PoissonGPLVMJump1D on MI355X: the reference's public API over the native engine.
+
+Mirrors poor_man_gplvm.core (reference core.py:376-849): the constructor
+(:381-420), fit_em (:829-849 -> :592-713), decode_latent (:454-497),
+m_step (:802-827), _decode_latent (:777-786), get_tuning (:772-774),
+init_latent_posterior (:571-583), sample / sample_latent / sample_y
+(:526-569, :795-800), predict_expected_rate (:716-733) -- same argument names,
+defaults and returned dict keys.  Differences that cannot be avoided without JAX:
+  * random draws (W init, posterior init, sampling) use numpy's PCG64 instead of
+    jax threefry; ``key`` may be an int, a numpy Generator or any array (hashed);
+  * arrays come back as numpy (the reference mixes jax and numpy arrays);
+  * log-space posteriors are log of the fp32 probabilities (-inf where a state's
+    probability underflows; the reference keeps very negative finite logs there);
+  * ``n_time_per_chunk`` is accepted and ignored (the reference uses it only to
+    bound XLA memory; the math does not depend on it, decoder.py:258-332);
+  * pynapple TsdFrame inputs are accepted when pynapple is importable.
+"""
+from __future__ import annotations
+
+import math
+import zlib
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from .engine import AdamConfig, DeviceEM, ScanConfig, SpikeData, default_device, log_of
+from .gp_kernel import banded_transition, create_transition_prob_1d, generate_basis
+
+try:  # optional, as in the reference's TsdFrame handling
+    import pynapple as nap  # type: ignore
+except Exception:  # pragma: no cover - pynapple is not installed in this image
+    nap = None
+
+
+def _is_tsd(y):
+    return nap is not None and isinstance(y, nap.TsdFrame)
+
+
+def _rng(key):
+    if isinstance(key, np.random.Generator):
+        return key
+    if key is None:
+        return np.random.default_rng(0)
+    if isinstance(key, (int, np.integer)):
+        return np.random.default_rng(int(key))
+    a = np.ascontiguousarray(np.asarray(key))
+    return np.random.default_rng(zlib.crc32(a.tobytes()))
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+class PoissonGPLVMJump1D:
+    """Poisson GPLVM with a smooth 1-d latent and jump dynamics (core.py:746)."""
+
+    def __init__(self, n_neuron, n_latent_bin=100, tuning_lengthscale=1., param_prior_std=1.,
+                 movement_variance=1., explained_variance_threshold_basis=0.999, rng_init_int=123,
+                 w_init_variance=1., w_init_mean=0., p_move_to_jump=0.01, p_jump_to_move=0.01,
+                 basis_type='rbf', custom_tuning_kernel=None, custom_transition_kernel=None,
+                 smoothness_penalty=0., scan_config: ScanConfig | None = None):
+        self.n_latent_bin = int(n_latent_bin)
+        self.tuning_lengthscale = tuning_lengthscale
+        self.param_prior_std = param_prior_std
+        self.movement_variance = movement_variance
+        self.p_move_to_jump = p_move_to_jump
+        self.p_jump_to_move = p_jump_to_move
+        self.explained_variance_threshold_basis = explained_variance_threshold_basis
+        self.rng_init_int = rng_init_int
+        self.n_neuron = int(n_neuron)
+        self.possible_latent_bin = np.arange(self.n_latent_bin)
+        self.possible_dynamics = np.arange(2)
+        self.w_init_variance = w_init_variance
+        self.w_init_mean = w_init_mean
+        self.custom_transition_kernel = custom_transition_kernel
+        self.basis_type = basis_type
+        self.tuning_basis = generate_basis(tuning_lengthscale, self.n_latent_bin,
+                                           explained_variance_threshold_basis, include_bias=True,
+                                           basis_type=basis_type, custom_kernel=custom_tuning_kernel)
+        self.n_basis = self.tuning_basis.shape[1]
+        self.smoothness_penalty = smoothness_penalty
+        self.ma_neuron_default = np.ones(self.n_neuron)
+        self.ma_latent_default = np.ones(self.n_latent_bin)
+        self.scan_config = scan_config or ScanConfig()
+        self.adam_runner = None          # kept for attribute parity (core.py:841)
+        self.opt_state_init_fun = None
+        self.initialize_params(_rng(rng_init_int))
+
+    # ------------------------------------------------------------------ params
+    def initialize_params(self, key):
+        """core.py:429-437 (numpy RNG)."""
+        rng = _rng(key)
+        W = rng.normal(size=(self.n_basis, self.n_neuron)) * math.sqrt(self.w_init_variance) + self.w_init_mean
+        self.params = W.astype(np.float32)
+        self._tuning = None   # softplus(basis @ W), computed on the device on first use
+        return self.params, self.tuning if torch.cuda.is_available() else None
+
+    @property
+    def tuning(self):
+        """(n_latent_bin, n_neuron) tuning curves (core.py:434, lazily on the device)."""
+        if self._tuning is None:
+            self._tuning = self.get_tuning(self.params, {}, self.tuning_basis)
+        return self._tuning
+
+    @tuning.setter
+    def tuning(self, value):
+        self._tuning = None if value is None else np.asarray(value, np.float32)
+
+    def get_tuning(self, params, hyperparam, tuning_basis):
+        """fit_tuning_helper.get_tuning_softplus (fit_tuning_helper.py:19-25), on device."""
+        B = np.asarray(tuning_basis, np.float32)
+        W = np.asarray(params, np.float64)
+        dev = default_device()
+        lib = nat.load()
+        bt = torch.as_tensor(np.ascontiguousarray(B), device=dev)
+        wt = torch.as_tensor(np.ascontiguousarray(W), device=dev)
+        out = torch.empty((B.shape[0], W.shape[1]), dtype=torch.float32, device=dev)
+        nat.check(lib.pmg_tuning_softplus(nat.ptr(bt), nat.ptr(wt), B.shape[0], B.shape[1], W.shape[1],
+                                          None, nat.ptr(out), nat.stream_handle()), "pmg_tuning_softplus")
+        return _np(out)
+
+    def init_latent_posterior(self, T, key, random_scale=0.1):
+        """core.py:571-583: U(0,1)*scale, row-normalised, log (numpy RNG)."""
+        u = _rng(key).random((T, self.n_latent_bin))
+        post = u * random_scale
+        post = post / post.sum(axis=1, keepdims=True)
+        with np.errstate(divide='ignore'):
+            lp = np.log(post)
+        lp = np.where(lp == -np.inf, -1e40, lp)
+        return lp.astype(np.float32), post.astype(np.float32)
+
+    # ------------------------------------------------------------------ transitions
+    def _transition(self, movement_variance, p_move_to_jump, p_jump_to_move):
+        return banded_transition(self.n_latent_bin, movement_variance, p_move_to_jump, p_jump_to_move,
+                                 custom_kernel=self.custom_transition_kernel)
+
+    # ------------------------------------------------------------------ M-step
+    def m_step(self, param_curr, y, log_posterior_curr, tuning_basis, hyperparam, opt_state_curr=None):
+        """core.py:802-827: sufficient statistics + Adam (one device launch each).
+        opt_state_curr: dict(mu, nu, count) as returned in the result (None = fresh)."""
+        hp = dict(hyperparam)
+        y = np.asarray(y)
+        sp = SpikeData(y, None)
+        B = np.asarray(tuning_basis, np.float32)
+        eng = DeviceEM(sp, B.shape[0], basis=B, scan=self.scan_config)
+        eng.set_log_posterior(log_posterior_curr)
+        cfg = AdamConfig(lr=getattr(self, '_m_step_step_size', 0.01),
+                         maxiter=getattr(self, '_m_step_maxiter', 1000),
+                         tol=getattr(self, '_m_step_tol', 1e-6),
+                         prior_std=hp.get('param_prior_std', self.param_prior_std))
+        dev = eng.dev
+        W = torch.as_tensor(np.asarray(param_curr, np.float64), device=dev).contiguous()
+        st = opt_state_curr or {'mu': np.zeros(W.shape), 'nu': np.zeros(W.shape), 'count': 0}
+        mu = torch.as_tensor(np.asarray(st['mu'], np.float64), device=dev).contiguous()
+        nu = torch.as_tensor(np.asarray(st['nu'], np.float64), device=dev).contiguous()
+        cnt = torch.tensor([int(st['count'])], dtype=torch.int64, device=dev)
+        stats = torch.zeros(4, dtype=torch.float64, device=dev)
+        lh = torch.zeros(max(cfg.maxiter, 1), dtype=torch.float64, device=dev)
+        eh = torch.zeros_like(lh)
+        eng.m_step(W, mu, nu, cnt, cfg, stats, lh, eh)
+        s = _np(stats)
+        n = int(s[0])
+        return {'params': _np(W).astype(np.float32),
+                'opt_state': {'mu': _np(mu), 'nu': _np(nu), 'count': int(_np(cnt)[0])},
+                'n_iter': n, 'final_loss': float(s[1]), 'final_error': float(s[2]),
+                'loss_history': _np(lh)[:n], 'error_history': _np(eh)[:n]}
+
+    # ------------------------------------------------------------------ E-step
+    def _decode_latent(self, y, tuning, hyperparam, log_latent_transition_kernel_l,
+                       log_dynamics_transition_kernel, ma_neuron, ma_latent=None, likelihood_scale=1.,
+                       n_time_per_chunk=10000):
+        """core.py:777-786 -> decoder.smooth_all_step_combined_ma_chunk (decoder.py:258-332).
+        The transition is rebuilt in banded form from this model's hyper-parameters
+        (hyperparam overrides); the passed log kernels are used only for the joint's
+        log-space outputs.  Returns the reference's 6-tuple (numpy)."""
+        res = self._run_decode(y, tuning, hyperparam, ma_neuron, ma_latent, likelihood_scale, joint=True,
+                               logK=log_latent_transition_kernel_l, logA=log_dynamics_transition_kernel)
+        return (res['log_posterior_all'], res['log_marginal_final'], res['log_causal_posterior_all'],
+                res['log_one_step_predictive_marginals_all'], res['log_accumulated_joint'],
+                res['log_likelihood_all'])
+
+    def _run_decode(self, y, tuning, hyperparam, ma_neuron, ma_latent, likelihood_scale, joint=True,
+                    logK=None, logA=None):
+        mv = hyperparam.get('movement_variance', self.movement_variance)
+        pmj = hyperparam.get('p_move_to_jump', self.p_move_to_jump)
+        pjm = hyperparam.get('p_jump_to_move', self.p_jump_to_move)
+        y = np.asarray(y)
+        ma = None if ma_neuron is None else np.asarray(ma_neuron, np.float32)
+        sp = SpikeData(y, ma)
+        eng = DeviceEM(sp, self.n_latent_bin, scan=self.scan_config)
+        eng.set_transition(self._transition(mv, pmj, pjm))
+        eng.set_ma_latent(ma_latent)
+        eng.set_tuning(np.asarray(tuning))
+        dev = eng.dev
+        T, L = sp.T, self.n_latent_bin
+        logz = torch.zeros(1, dtype=torch.float64, device=dev)
+        gamma = torch.empty((T, 2, L), dtype=torch.float32, device=dev)
+        rho = torch.zeros((T, 2, L), dtype=torch.float32, device=dev) if joint else None
+        eng.e_step(likelihood_scale, logz, gamma=gamma, rho=rho)
+        out = {
+            'log_posterior_all': _np(log_of(gamma)),
+            'log_marginal_final': float(_np(logz)[0]),
+            'posterior_all': _np(gamma),
+            'log_causal_posterior_all': _np(log_of(eng.alpha)),
+            'log_one_step_predictive_marginals_all': _np(eng.logc).astype(np.float32),
+            'log_likelihood_all': _np(eng.loglik()),
+        }
+        if joint:
+            S = _np(eng.joint(rho))  # (2L, 2L) f64
+            if logK is None or logA is None:
+                _, logK, _, logA = create_transition_prob_1d(L, mv, pmj, pjm, self.custom_transition_kernel)
+            logK = np.asarray(logK, np.float64)
+            logA = np.asarray(logA, np.float64)
+            S4 = S.reshape(2, L, 2, L).transpose(0, 2, 1, 3)          # [d, d', i, j]
+            with np.errstate(divide='ignore'):
+                lj = logA[:, :, None, None] + logK[None, :, :, :] + np.log(np.maximum(S4, 0.0))
+            out['log_accumulated_joint'] = lj
+        return out
+
+    # ------------------------------------------------------------------ decode
+    def decode_latent(self, y, tuning=None, hyperparam={}, ma_neuron=None, ma_latent=None,
+                      likelihood_scale=1., n_time_per_chunk=10000, t_l=None):
+        """core.py:454-497 (+ decoder.compute_transition_posterior_prob, decoder.py:334-375)."""
+        if _is_tsd(y):
+            t_l = y.t
+            y = y.d
+        if tuning is None:
+            tuning = self.tuning
+        if ma_neuron is None:
+            ma_neuron = self.ma_neuron_default
+        if ma_latent is None:
+            ma_latent = self.ma_latent_default
+        r = self._run_decode(y, tuning, hyperparam, ma_neuron, ma_latent, likelihood_scale, joint=True)
+        posterior_all = r['posterior_all']
+        plm = posterior_all.sum(axis=1)
+        pdm = posterior_all.sum(axis=2)
+        if t_l is not None and nap is not None:
+            plm = nap.TsdFrame(d=plm, t=t_l)
+            pdm = nap.TsdFrame(d=pdm, t=t_l)
+        res = {'log_posterior_all': r['log_posterior_all'],
+               'log_marginal_final': r['log_marginal_final'],
+               'posterior_all': posterior_all,
+               'posterior_latent_marg': plm,
+               'posterior_dynamics_marg': pdm,
+               'log_one_step_predictive_marginals_all': r['log_one_step_predictive_marginals_all'],
+               'log_likelihood_all': r['log_likelihood_all']}
+        res.update(compute_transition_posterior_prob(r['log_accumulated_joint']))
+        return res
+
+    # ------------------------------------------------------------------ EM
+    def fit_em(self, y, hyperparam={}, key=0, n_iter=20, log_posterior_init=None, ma_neuron=None,
+               ma_latent=None, n_time_per_chunk=10000, dt=1., likelihood_scale=1., save_every=None,
+               m_step_step_size=0.01, m_step_maxiter=1000, m_step_tol=1e-6,
+               posterior_init_kwargs={'random_scale': 0.1}, verboase=True, **kwargs):
+        """core.py:829-849 + core.py:592-713: n_iter x (M-step, E-step) on the GPU."""
+        hp = dict(hyperparam)
+        hp['param_prior_std'] = hp.get('param_prior_std', self.param_prior_std)
+        hp['smoothness_penalty'] = hp.get('smoothness_penalty', self.smoothness_penalty)
+        y_in = y
+        if _is_tsd(y):
+            y = y.d
+        y = np.asarray(y)
+        T = y.shape[0]
+        tuning_lengthscale = hp.get('tuning_lengthscale', self.tuning_lengthscale)
+        movement_variance = hp.get('movement_variance', self.movement_variance)
+        p_move_to_jump = hp.get('p_move_to_jump', self.p_move_to_jump)
+        p_jump_to_move = hp.get('p_jump_to_move', self.p_jump_to_move)
+        self.tuning_lengthscale = tuning_lengthscale
+        self.movement_variance = movement_variance
+        self.p_move_to_jump = p_move_to_jump
+        self.p_jump_to_move = p_jump_to_move
+        self._m_step_step_size, self._m_step_maxiter, self._m_step_tol = m_step_step_size, m_step_maxiter, m_step_tol
+        if save_every is None:
+            save_every = n_iter
+        _, log_latent_transition_kernel_l, _, log_dynamics_transition_kernel = create_transition_prob_1d(
+            self.n_latent_bin, movement_variance, p_move_to_jump, p_jump_to_move, self.custom_transition_kernel)
+        if ma_neuron is None:
+            ma_neuron = self.ma_neuron_default
+        if ma_latent is None:
+            ma_latent = self.ma_latent_default
+        if 'tuning_lengthscale' in hyperparam:                            # core.py:635-638
+            tuning_basis = generate_basis(tuning_lengthscale, self.n_latent_bin,
+                                          self.explained_variance_threshold_basis, include_bias=True)
+        else:
+            tuning_basis = self.tuning_basis
+        if log_posterior_init is None:
+            log_posterior_init, _ = self.init_latent_posterior(T, key, **posterior_init_kwargs)
+
+        res, info = run_em(y, self.params, tuning_basis, log_posterior_init, n_iter=n_iter,
+                     transition=self._transition(movement_variance, p_move_to_jump, p_jump_to_move),
+                     ma_neuron=ma_neuron, ma_latent=ma_latent, likelihood_scale=likelihood_scale,
+                     save_every=save_every,
+                     adam=AdamConfig(lr=m_step_step_size, maxiter=m_step_maxiter, tol=m_step_tol,
+                                     prior_std=hp['param_prior_std']),
+                     scan=self.scan_config)
+        self.params = res['params']
+        self.tuning = res['tuning']
+        self.fit_info = info
+        self.log_marginal_final = res['log_marginal']
+        self.log_latent_transition_kernel_l = log_latent_transition_kernel_l
+        self.log_dynamics_transition_kernel = log_dynamics_transition_kernel
+        self.tuning_basis = tuning_basis
+        if _is_tsd(y_in):
+            res['posterior_latent_marg'] = nap.TsdFrame(d=res['posterior_latent_marg'], t=y_in.t)
+            res['posterior_dynamics_marg'] = nap.TsdFrame(d=res['posterior_dynamics_marg'], t=y_in.t)
+        res['log_posterior_init'] = log_posterior_init
+        return res
+
+    # ------------------------------------------------------------------ misc API
+    def predict_expected_rate(self, post_latent_marg, tuning=None):
+        """core.py:716-733: rate[t,n] = sum_p tuning[p,n] post[t,p]."""
+        if tuning is None:
+            tuning = self.tuning
+        pv = post_latent_marg.d if _is_tsd(post_latent_marg) else post_latent_marg
+        rate = np.einsum('pn,tp->tn', np.asarray(tuning), np.asarray(pv))
+        if _is_tsd(post_latent_marg):
+            rate = nap.TsdFrame(d=rate, t=post_latent_marg.t)
+        return rate
+
+    def sample_latent(self, T, key=0, movement_variance=1, p_move_to_jump=0.01, p_jump_to_move=0.01,
+                      init_dynamics=None, init_latent=None):
+        """core.py:526-555 with a numpy RNG: dynamics from A[prev], then latent from K[dyn][prev]."""
+        rng = _rng(key)
+        K, _, A, _ = create_transition_prob_1d(self.n_latent_bin, movement_variance, p_move_to_jump, p_jump_to_move)
+        d = int(rng.integers(2)) if init_dynamics is None else int(init_dynamics)
+        l = int(rng.integers(self.n_latent_bin)) if init_latent is None else int(init_latent)
+        out = np.empty((T, 2), np.int32)
+        cA = np.cumsum(A, 1)
+        cK = np.cumsum(K, 2)
+        u = rng.random((T, 2))
+        for t in range(T):
+            d = int(min(np.searchsorted(cA[d], u[t, 0] * cA[d, -1], side='right'), 1))
+            l = int(min(np.searchsorted(cK[d, l], u[t, 1] * cK[d, l, -1], side='right'), self.n_latent_bin - 1))
+            out[t] = (d, l)
+        return out
+
+    def sample_y(self, latent_l, hyperparam={}, tuning=None, dt=1., key=10):
+        """core.py:795-800: Poisson(tuning[latent] * dt)."""
+        if tuning is None:
+            tuning = self.tuning
+        return _rng(key).poisson(np.asarray(tuning, np.float64)[np.asarray(latent_l)] * dt)
+
+    def sample(self, T, hyperparam={}, key=0, init_dynamics=None, init_latent=None, dt=1., tuning=None):
+        """core.py:558-569."""
+        rng = _rng(key)
+        k1, k2 = int(rng.integers(2 ** 31)), int(rng.integers(2 ** 31))
+        mv = hyperparam.get('movement_variance', self.movement_variance)
+        pmj = hyperparam.get('p_move_to_jump', self.p_move_to_jump)
+        pjm = hyperparam.get('p_jump_to_move', self.p_jump_to_move)
+        latent_l = self.sample_latent(T, k1, mv, pmj, pjm, init_dynamics, init_latent)
+        y_l = self.sample_y(latent_l[:, 1], hyperparam, tuning, dt, k2)
+        return latent_l, y_l
+
+    def __getstate__(self):
+        """core.py:757-767: picklable (no device state is held between calls)."""
+        state = self.__dict__.copy()
+        state['adam_runner'] = None
+        state['opt_state_init_fun'] = None
+        return state
+
+    def __setstate__(self, state):
+        self.__dict__.update(state)
+
+
+def compute_transition_posterior_prob(log_accumulated_joint_total):
+    """decoder.py:334-375 on the host (f64), keys in jax's sorted pytree order."""
+    from scipy.special import logsumexp
+    lj = np.asarray(log_accumulated_joint_total, np.float64)
+    ljf = lj - logsumexp(lj)
+    ljl = logsumexp(ljf, axis=(0, 1))
+    ljd = logsumexp(ljf, axis=(2, 3))
+    ltl = ljl - logsumexp(ljl, axis=1, keepdims=True)
+    ltd = ljd - logsumexp(ljd, axis=1, keepdims=True)
+    ltf = ljf - logsumexp(ljf, axis=(1, 3), keepdims=True)
+    r = {'p_joint_full': np.exp(ljf), 'p_joint_latent': np.exp(ljl), 'p_joint_dynamics': np.exp(ljd),
+         'p_transition_full': np.exp(ltf), 'p_transition_latent': np.exp(ltl),
+         'p_transition_dynamics': np.exp(ltd), 'log_joint_full': ljf, 'log_joint_latent': ljl,
+         'log_joint_dynamics': ljd, 'log_transition_full': ltf, 'log_transition_latent': ltl,
+         'log_transition_dynamics': ltd}
+    return {k: r[k].astype(np.float32) for k in sorted(r)}
+
+
+def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=None, ma_latent=None,
+           likelihood_scale=1.0, save_every=None, adam: AdamConfig | None = None,
+           scan: ScanConfig | None = None, opt_state=None, timing=None):
+    """The EM loop of core.py:650-676 on one GPU; returns the fit_em dict (core.py:696-712).
+    `timing`, if a list, receives per-iteration wall-clock seconds (bench)."""
+    adam = adam or AdamConfig()
+    y = np.asarray(y)
+    T = y.shape[0]
+    B = np.asarray(basis, np.float32)
+    L = B.shape[0]
+    if save_every is None:
+        save_every = n_iter
+    ma = None if ma_neuron is None else np.asarray(ma_neuron, np.float32)
+    sp = SpikeData(y, ma)
+    eng = DeviceEM(sp, L, basis=B, scan=scan)
+    eng.set_transition(transition)
+    eng.set_ma_latent(ma_latent)
+    eng.set_log_posterior(log_posterior_init)
+    dev = eng.dev
+    W = torch.as_tensor(np.asarray(params, np.float64), device=dev).contiguous()
+    if opt_state is None:
+        mu = torch.zeros_like(W)
+        nu = torch.zeros_like(W)
+        cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    else:
+        mu = torch.as_tensor(np.asarray(opt_state['mu'], np.float64), device=dev).contiguous()
+        nu = torch.as_tensor(np.asarray(opt_state['nu'], np.float64), device=dev).contiguous()
+        cnt = torch.tensor([int(opt_state['count'])], dtype=torch.int64, device=dev)
+    mi = max(int(adam.maxiter), 1)
+    stats = torch.zeros((n_iter, 4), dtype=torch.float64, device=dev)
+    lh = torch.zeros((n_iter, mi), dtype=torch.float64, device=dev)
+    eh = torch.zeros((n_iter, mi), dtype=torch.float64, device=dev)
+    logz = torch.zeros(max(n_iter, 1), dtype=torch.float64, device=dev)
+    gamma = torch.empty((T, 2, L), dtype=torch.float32, device=dev)
+    saved = {'log_posterior_all_saved': [], 'params_saved': [], 'tuning_saved': [], 'iter_saved': [],
+             'log_marginal_saved': []}
+    saved_idx = []
+    import time
+    for i in range(n_iter):
+        t0 = time.perf_counter() if timing is not None else 0.0
+        eng.m_step(W, mu, nu, cnt, adam, stats[i], lh[i], eh[i])
+        eng.compute_tuning(W)
+        want_gamma = (i == n_iter - 1) or (i % save_every == 0)
+        eng.e_step(likelihood_scale, logz[i:i + 1], gamma=gamma if want_gamma else None)
+        if i % save_every == 0:
+            saved['log_posterior_all_saved'].append(_np(log_of(gamma)))
+            saved['params_saved'].append(_np(W).astype(np.float32))
+            saved['tuning_saved'].append(_np(eng.tuning32))
+            saved['iter_saved'].append(i)
+            saved_idx.append(i)
+        if timing is not None:
+            torch.cuda.synchronize()
+            timing.append(time.perf_counter() - t0)
+    s = _np(stats)
+    lhn, ehn = _np(lh), _np(eh)
+    lz = _np(logz)
+    saved['log_marginal_saved'] = [float(lz[i]) for i in saved_idx]
+    m_step_res_l = {'params': [], 'opt_state': [], 'n_iter': [], 'final_loss': [], 'final_error': [],
+                    'loss_history': [], 'error_history': []}
+    for i in range(n_iter):
+        n = int(s[i, 0])
+        m_step_res_l['n_iter'].append(n)
+        m_step_res_l['final_loss'].append(float(s[i, 1]))
+        m_step_res_l['final_error'].append(float(s[i, 2]))
+        m_step_res_l['loss_history'].append(lhn[i, :n].copy())
+        m_step_res_l['error_history'].append(ehn[i, :n].copy())
+    posterior = _np(gamma)
+    res = {'log_posterior_all_saved': saved['log_posterior_all_saved'],
+           'log_posterior_init': log_posterior_init,
+           'params_saved': saved['params_saved'],
+           'tuning_saved': saved['tuning_saved'],
+           'iter_saved': saved['iter_saved'],
+           'params': _np(W).astype(np.float32),
+           'tuning': _np(eng.tuning32),
+           'log_posterior_final': _np(log_of(gamma)),
+           'log_marginal': float(lz[n_iter - 1]) if n_iter else float('nan'),
+           'log_marginal_l': [float(v) for v in lz[:n_iter]],
+           'log_marginal_saved': saved['log_marginal_saved'],
+           'posterior': posterior,
+           'posterior_latent_marg': posterior.sum(axis=1),
+           'posterior_dynamics_marg': posterior.sum(axis=2),
+           'm_step_res_l': m_step_res_l}
+    info = {'opt_state': {'mu': _np(mu), 'nu': _np(nu), 'count': int(_np(cnt)[0])},
+            'params64': _np(W), 'repairs': eng.repairs(), 'chunk': eng.C}
+    return res, info

@@ -1,0 +1,867 @@
+// Time-parallel forward filter / backward smoother over the joint
+// (dynamics x latent) state of the jump GPLVM, gfx950.
+//
+// Reference (log-domain, strictly sequential lax.scan):
+//   filter_one_step   decoder.py:151-172   prior = LSE_i(LSE_d(post+logA)+logK); post = prior+s*ll - c
+//   smooth_one_step   decoder.py:200-226   acausal_t = LSE_{d',j}(logK+logA+(acausal_{t+1}-prior_{t+1})+post_t)
+//   chunk driver      decoder.py:258-332   carries (post[-1], logZ) forward, (acausal[0], joint) backward
+//
+// MI355X design:
+//   * linear space with per-step normalisation (exact up to fp32 rounding; states
+//     below ~1e-38 of the total flush to 0 -- probability-space outputs unchanged);
+//   * the continuous kernel is a row-normalised Toeplitz band K0[i,j] = g[|i-j|]/Z_i
+//     (exactly zero beyond |i-j| = band in the reference's f32), applied
+//     as a 1-D convolution through a per-wave LDS line; the jump kernel is rank-1
+//     (a wave reduction); the 2x2 dynamics mix is elementwise;
+//   * one wave per time chunk; each chunk starts from a uniform guess `warmup`
+//     steps early (HMM forgetting), then every chunk boundary is verified in the
+//     Hilbert projective metric (max-min of log ratios, a contraction of positive
+//     linear maps, so a boundary error <= tol bounds every later output's relative
+//     error by tol) and chunks that fail are recomputed exactly from their
+//     predecessor's state by a single-wave repair pass (rare; sequential only over
+//     consecutive failures);
+//   * the smoother uses the equivalent alpha-beta form gamma_t ~ alpha_t * beta_t
+//     with beta_{T-1} = 1 (the reference's RTS seed acausal_{T-1} = post_{T-1}), so
+//     the backward pass needs only alpha_t and the emission -- no stored priors.
+//
+// Emission input: e[t,l] = exp(s*delta[t,l] + phi[t,l/32]) = exp(s*(ll[t,l] - m[t])).
+#include "pmg_common.h"
+
+namespace pmg {
+
+constexpr int kMaxBand = 32;
+
+struct FBParams {
+  const float* delta;
+  const float* phi;
+  const double* m;
+  int64_t T;
+  int L;
+  int nblk;
+  const float* invz;
+  float g[kMaxBand + 1];
+  float A00, A01, A10, A11;
+  float invL;
+  float s;
+  double s_d;
+  int C, B, M;
+  float tol;
+  // forward
+  float* alpha;
+  double* logc;
+  double* chunk_logz;
+  float* s_in;
+  float* s_out;
+  // backward
+  const float* alpha_in;
+  float* P;
+  float* gamma;
+  float* rho;
+  float* b_in;
+  float* b_out;
+  float* b_first;
+  int* flags;
+  int* repairs;
+  int Lpad;  // 64*J
+};
+
+// ---------------------------------------------------------------------------
+// per-lane helpers (lane owns latents j0 .. j0+J-1, j0 = lane*J)
+// ---------------------------------------------------------------------------
+template <int J>
+__device__ __forceinline__ void load_row(const float* __restrict__ row, int L, int j0, float v[J]) {
+  if ((L & 3) == 0 && (J & 3) == 0 && j0 + J <= L) {
+#pragma unroll
+    for (int j = 0; j < J; j += 4) {
+      float4 q = *reinterpret_cast<const float4*>(row + j0 + j);
+      v[j] = q.x; v[j + 1] = q.y; v[j + 2] = q.z; v[j + 3] = q.w;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < J; ++j) v[j] = (j0 + j < L) ? row[j0 + j] : 0.f;
+  }
+}
+
+template <int J>
+__device__ __forceinline__ void store_row(float* __restrict__ row, int L, int j0, const float v[J]) {
+  if ((L & 3) == 0 && (J & 3) == 0 && j0 + J <= L) {
+#pragma unroll
+    for (int j = 0; j < J; j += 4)
+      *reinterpret_cast<float4*>(row + j0 + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+      if (j0 + j < L) row[j0 + j] = v[j];
+  }
+}
+
+// raw emission operands for one time step
+template <int J>
+struct EmRaw {
+  float d[J];
+  float ph;
+};
+
+template <int J>
+__device__ __forceinline__ void em_load(const FBParams& p, int64_t t, int j0, EmRaw<J>& r) {
+  load_row<J>(p.delta + t * p.L, p.L, j0, r.d);
+  const int b = j0 >> 5;
+  r.ph = (b < p.nblk) ? p.phi[t * p.nblk + b] : 0.f;
+}
+
+template <int J>
+__device__ __forceinline__ void em_exp(const FBParams& p, int j0, const EmRaw<J>& r, float e[J]) {
+#pragma unroll
+  for (int j = 0; j < J; ++j) e[j] = (j0 + j < p.L) ? __expf(fmaf(p.s, r.d[j], r.ph)) : 0.f;
+}
+
+// out[j] = sum_{k=-WP..WP} g[|k|] * in[j+k]  over the whole latent line (zero halo)
+template <int J, int WP>
+__device__ __forceinline__ void band_conv(const FBParams& p, float* lds, int j0, const float in[J],
+                                          float out[J]) {
+#pragma unroll
+  for (int j = 0; j < J; ++j) lds[WP + j0 + j] = in[j];
+  __syncthreads();
+  float win[J + 2 * WP];
+#pragma unroll
+  for (int k = 0; k < J + 2 * WP; ++k) win[k] = lds[j0 + k];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    float acc = p.g[0] * win[j + WP];
+#pragma unroll
+    for (int k = 1; k <= WP; ++k) acc = fmaf(p.g[k], win[j + WP - k] + win[j + WP + k], acc);
+    out[j] = acc;
+  }
+  __syncthreads();
+}
+
+// Hilbert projective distance between two non-negative (2, Lpad) states held in
+// memory; components below 1e-30 of the max on both sides are ignored, a
+// component significant (> 1e-20) on one side only counts as a failure.
+__device__ float hilbert_dist(const float* __restrict__ x, const float* __restrict__ y, int n) {
+  const int lane = threadIdx.x & 63;
+  float xm = 0.f, ym = 0.f;
+  for (int i = lane; i < n; i += 64) {
+    xm = fmaxf(xm, x[i]);
+    ym = fmaxf(ym, y[i]);
+  }
+  xm = wave_max_shfl(xm);
+  ym = wave_max_shfl(ym);
+  if (!(xm > 0.f) || !(ym > 0.f)) return INFINITY;
+  const float ix = 1.f / xm, iy = 1.f / ym;
+  float lo = INFINITY, hi = -INFINITY;
+  int bad = 0;
+  for (int i = lane; i < n; i += 64) {
+    const float a = x[i] * ix, b = y[i] * iy;
+    if (a > 1e-30f && b > 1e-30f) {
+      const float r = __logf(a) - __logf(b);
+      lo = fminf(lo, r);
+      hi = fmaxf(hi, r);
+    } else if (fmaxf(a, b) > 1e-20f) {
+      bad = 1;
+    }
+  }
+  lo = wave_min_shfl(lo);
+  hi = wave_max_shfl(hi);
+  if (__ballot(bad)) return INFINITY;
+  if (hi < lo) return 0.f;
+  return hi - lo;
+}
+
+// same metric, x held in registers with the (2, Lpad) lane layout, y in memory
+template <int J>
+__device__ float hilbert_reg(const float x0[J], const float x1[J], const float* __restrict__ y,
+                             int Lpad, int j0) {
+  float xm = 0.f, ym = 0.f;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    xm = fmaxf(xm, fmaxf(x0[j], x1[j]));
+    ym = fmaxf(ym, fmaxf(y[j0 + j], y[Lpad + j0 + j]));
+  }
+  xm = wave_max_shfl(xm);
+  ym = wave_max_shfl(ym);
+  if (!(xm > 0.f) || !(ym > 0.f)) return INFINITY;
+  const float ix = 1.f / xm, iy = 1.f / ym;
+  float lo = INFINITY, hi = -INFINITY;
+  int bad = 0;
+#pragma unroll
+  for (int j = 0; j < 2 * J; ++j) {
+    const float a = (j < J ? x0[j] : x1[j - J]) * ix;
+    const float b = (j < J ? y[j0 + j] : y[Lpad + j0 + j - J]) * iy;
+    if (a > 1e-30f && b > 1e-30f) {
+      const float r = __logf(a) - __logf(b);
+      lo = fminf(lo, r);
+      hi = fmaxf(hi, r);
+    } else if (fmaxf(a, b) > 1e-20f) {
+      bad = 1;
+    }
+  }
+  lo = wave_min_shfl(lo);
+  hi = wave_max_shfl(hi);
+  if (__ballot(bad)) return INFINITY;
+  if (hi < lo) return 0.f;
+  return hi - lo;
+}
+
+// ---------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------
+template <int J, int WP>
+struct Fwd {
+  float p0[J], p1[J];
+  float P0, P1;  // sum of p0, p1 (wave-uniform)
+
+  __device__ void init_uniform(const FBParams& p, int j0) {
+    const float u = 0.5f * p.invL;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      p0[j] = (j0 + j < p.L) ? u : 0.f;
+      p1[j] = p0[j];
+    }
+    P0 = 0.5f;
+    P1 = 0.5f;
+  }
+  __device__ void load_state(const FBParams& p, const float* src, int j0) {
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      p0[j] = src[j0 + j];
+      p1[j] = src[p.Lpad + j0 + j];
+    }
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      a += p0[j];
+      b += p1[j];
+    }
+    wave_sum2(a, b);
+    const float inv = 1.f / (a + b);
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      p0[j] *= inv;
+      p1[j] *= inv;
+    }
+    P0 = a * inv;
+    P1 = b * inv;
+  }
+  __device__ void save_state(const FBParams& p, float* dst, int j0) const {
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      dst[j0 + j] = p0[j];
+      dst[p.Lpad + j0 + j] = p1[j];
+    }
+  }
+  // one filter step with emission e; returns the normaliser S
+  __device__ float step(const FBParams& p, float* lds, int j0, const float invz[J], const float e[J]) {
+    float a0[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) a0[j] = fmaf(p0[j], p.A00, p1[j] * p.A10) * invz[j];
+    const float jump = fmaf(p.A01, P0, p.A11 * P1) * p.invL;
+    float pr0[J];
+    band_conv<J, WP>(p, lds, j0, a0, pr0);
+    float U0 = 0.f, U1 = 0.f;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      p0[j] = pr0[j] * e[j];
+      p1[j] = jump * e[j];
+      U0 += p0[j];
+      U1 += p1[j];
+    }
+    wave_sum2(U0, U1);
+    const float S = U0 + U1;
+    const float inv = 1.f / S;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      p0[j] *= inv;
+      p1[j] *= inv;
+    }
+    P0 = U0 * inv;
+    P1 = U1 * inv;
+    return S;
+  }
+};
+
+// run chunk c forward from t0 (state already initialised) to t_e; writes outputs for t >= t_c
+template <int J, int WP>
+__device__ double fwd_run(const FBParams& p, Fwd<J, WP>& st, float* lds, int j0, const float invz[J],
+                          int64_t t0, int64_t t_c, int64_t t_e, float* s_in_dst) {
+  const int lane = threadIdx.x & 63;
+  double logz = 0.0;
+  if (t0 >= t_e) return 0.0;
+  EmRaw<J> nxt;
+  em_load<J>(p, t0, j0, nxt);
+  for (int64_t t = t0; t < t_e; ++t) {
+    float e[J];
+    em_exp<J>(p, j0, nxt, e);
+    if (t + 1 < t_e) em_load<J>(p, t + 1, j0, nxt);
+    const float S = st.step(p, lds, j0, invz, e);
+    if (t >= t_c) {
+      float* arow = p.alpha + t * 2 * (int64_t)p.L;
+      store_row<J>(arow, p.L, j0, st.p0);
+      store_row<J>(arow + p.L, p.L, j0, st.p1);
+      const double lc = (double)__logf(S) + p.s_d * p.m[t];
+      if (lane == 0) p.logc[t] = lc;
+      logz += lc;
+    } else if (t == t_c - 1 && s_in_dst) {
+      st.save_state(p, s_in_dst, j0);
+    }
+  }
+  return logz;
+}
+
+template <int J, int WP>
+__global__ void __launch_bounds__(64) k_forward(FBParams p) {
+  __shared__ __attribute__((aligned(16))) float lds[64 * J + 2 * WP];
+  const int lane = threadIdx.x;
+  const int j0 = lane * J;
+  for (int k = lane; k < 64 * J + 2 * WP; k += 64) lds[k] = 0.f;
+  __syncthreads();
+  const int c = blockIdx.x;
+  if (c >= p.M) return;
+  float invz[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) invz[j] = (j0 + j < p.L) ? p.invz[j0 + j] : 0.f;
+  const int64_t t_c = (int64_t)c * p.C;
+  const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
+  int64_t t0 = (c == 0) ? 0 : t_c - p.B;
+  if (t0 < 0) t0 = 0;
+  Fwd<J, WP> st;
+  st.init_uniform(p, j0);
+  float* sin = p.s_in + (size_t)c * 2 * p.Lpad;
+  if (c > 0 && t0 == t_c) st.save_state(p, sin, j0);  // no warm-up: the guess itself
+  const double lz = fwd_run<J, WP>(p, st, lds, j0, invz, t0, t_c, t_e, c > 0 ? sin : nullptr);
+  st.save_state(p, p.s_out + (size_t)c * 2 * p.Lpad, j0);
+  if (lane == 0) p.chunk_logz[c] = lz;
+}
+
+// single-wave sequential repair of chunks whose start state failed verification
+template <int J, int WP>
+__global__ void __launch_bounds__(64) k_forward_repair(FBParams p) {
+  __shared__ __attribute__((aligned(16))) float lds[64 * J + 2 * WP];
+  const int lane = threadIdx.x;
+  const int j0 = lane * J;
+  for (int k = lane; k < 64 * J + 2 * WP; k += 64) lds[k] = 0.f;
+  __syncthreads();
+  float invz[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) invz[j] = (j0 + j < p.L) ? p.invz[j0 + j] : 0.f;
+  const size_t SZ = (size_t)2 * p.Lpad;
+  int repairs = 0;
+  bool changed = false;
+  int c = 1;
+  Fwd<J, WP> st;
+  while (c < p.M) {
+    if (!changed) {  // jump to the next flagged chunk, 64 flags at a time
+      int found = -1;
+      for (int base = c; base < p.M && found < 0; base += 64) {
+        const int idx = base + lane;
+        const bool f = idx < p.M && p.flags[idx] != 0;
+        const unsigned long long bal = __ballot(f);
+        if (bal) found = base + (int)__builtin_ctzll(bal);
+      }
+      if (found < 0) break;
+      c = found;
+      st.load_state(p, p.s_out + (size_t)(c - 1) * SZ, j0);  // written by k_forward
+    }
+    // else: st already holds the repaired end state of chunk c-1
+    const int64_t t_c = (int64_t)c * p.C;
+    const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
+    st.save_state(p, p.s_in + (size_t)c * SZ, j0);
+    const double lz = fwd_run<J, WP>(p, st, lds, j0, invz, t_c, t_c, t_e, nullptr);
+    float* sout = p.s_out + (size_t)c * SZ;
+    const float d = hilbert_reg<J>(st.p0, st.p1, sout, p.Lpad, j0);
+    changed = !(d <= p.tol);
+    st.save_state(p, sout, j0);
+    if (lane == 0) p.chunk_logz[c] = lz;
+    __threadfence();
+    ++repairs;
+    ++c;
+  }
+  if (lane == 0) p.repairs[0] = repairs;
+}
+
+// boundary verification: flags[c] = hilbert(x[c], y[c + off]) > tol
+__global__ void __launch_bounds__(256) k_verify(const float* __restrict__ x, const float* __restrict__ y,
+                                                int first, int last, int off, int SZ, float tol,
+                                                int* __restrict__ flags, int M) {
+  const int w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int c = first + w;
+  if (c > last) return;
+  const float d = hilbert_dist(x + (size_t)c * SZ, y + (size_t)(c + off) * SZ, SZ);
+  if ((threadIdx.x & 63) == 0) flags[c] = (d <= tol) ? 0 : 1;
+  (void)M;
+}
+
+__global__ void k_sum_f64(const double* __restrict__ x, int n, double* __restrict__ out) {
+  __shared__ double sm[256];
+  double a = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) a += x[i];
+  sm[threadIdx.x] = a;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) sm[threadIdx.x] += sm[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = sm[0];
+}
+
+// ---------------------------------------------------------------------------
+// backward (beta recursion)
+// ---------------------------------------------------------------------------
+template <int J, int WP>
+struct Bwd {
+  float b0[J], b1[J];  // beta at the current time
+
+  __device__ void init_ones(const FBParams& p, int j0) {
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      b0[j] = (j0 + j < p.L) ? 1.f : 0.f;
+      b1[j] = b0[j];
+    }
+  }
+  __device__ void load_state(const FBParams& p, const float* src, int j0) {
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      b0[j] = src[j0 + j];
+      b1[j] = src[p.Lpad + j0 + j];
+    }
+  }
+  __device__ void save_state(const FBParams& p, float* dst, int j0) const {
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      dst[j0 + j] = b0[j];
+      dst[p.Lpad + j0 + j] = b1[j];
+    }
+  }
+  // beta_{t-1} = Trans (v), v = e_t * beta_t already scaled; V1 = sum v1
+  __device__ void transition_back(const FBParams& p, float* lds, int j0, const float invz[J],
+                                  const float v0[J], float V1) {
+    float w0[J];
+    band_conv<J, WP>(p, lds, j0, v0, w0);
+    const float w1 = V1 * p.invL;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const float c0 = w0[j] * invz[j];
+      const float real = (j0 + j < p.L) ? 1.f : 0.f;
+      b0[j] = fmaf(p.A00, c0, p.A01 * w1) * real;
+      b1[j] = fmaf(p.A10, c0, p.A11 * w1) * real;
+    }
+  }
+};
+
+// warm-up / plain backward steps from time t_hi down to t_lo (beta ends at t_lo)
+template <int J, int WP>
+__device__ void bwd_warm(const FBParams& p, Bwd<J, WP>& st, float* lds, int j0, const float invz[J],
+                         int64_t t_hi, int64_t t_lo) {
+  for (int64_t t = t_hi; t > t_lo; --t) {
+    EmRaw<J> r;
+    em_load<J>(p, t, j0, r);
+    float e[J];
+    em_exp<J>(p, j0, r, e);
+    float v0[J], v1[J];
+    float VS = 0.f, V1 = 0.f;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      v0[j] = e[j] * st.b0[j];
+      v1[j] = e[j] * st.b1[j];
+      VS += v0[j] + v1[j];
+      V1 += v1[j];
+    }
+    wave_sum2(VS, V1);
+    const float sc = 1.f / VS;
+#pragma unroll
+    for (int j = 0; j < J; ++j) v0[j] *= sc;
+    st.transition_back(p, lds, j0, invz, v0, V1 * sc);
+  }
+}
+
+// output steps t = t_e-1 .. t_c (beta at t_e-1 in st, v_prev = the v that produced it,
+// or has_prev = false at the sequence end).  Leaves beta_{t_c-1} in st if t_c > 0.
+template <int J, int WP>
+__device__ void bwd_out(const FBParams& p, Bwd<J, WP>& st, float* lds, int j0, const float invz[J],
+                        int64_t t_c, int64_t t_e, float vprev0[J], float vprev1[J], bool has_prev) {
+  const int64_t L = p.L;
+  for (int64_t t = t_e - 1; t >= t_c; --t) {
+    EmRaw<J> r;
+    em_load<J>(p, t, j0, r);
+    float a0[J], a1[J];
+    const float* arow = p.alpha_in + t * 2 * L;
+    load_row<J>(arow, p.L, j0, a0);
+    load_row<J>(arow + L, p.L, j0, a1);
+    float e[J];
+    em_exp<J>(p, j0, r, e);
+    float G = 0.f, V1 = 0.f;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      a0[j] *= st.b0[j];
+      a1[j] *= st.b1[j];
+      G += a0[j] + a1[j];
+      V1 += e[j] * st.b1[j];
+    }
+    wave_sum2(G, V1);
+    const float iG = 1.f / G;
+    float pp[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      a0[j] *= iG;
+      a1[j] *= iG;
+      pp[j] = a0[j] + a1[j];
+    }
+    if (t == t_c && p.b_first) {
+      float* bf = p.b_first + (size_t)(t_c / p.C) * 2 * p.Lpad;
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        bf[j0 + j] = st.b0[j];
+        bf[p.Lpad + j0 + j] = st.b1[j];
+      }
+    }
+    if (p.P) store_row<J>(p.P + t * L, p.L, j0, pp);
+    if (p.gamma) {
+      store_row<J>(p.gamma + t * 2 * L, p.L, j0, a0);
+      store_row<J>(p.gamma + t * 2 * L + L, p.L, j0, a1);
+    }
+    if (p.rho && has_prev && t + 1 < p.T) {
+      float r0[J], r1[J];
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        r0[j] = vprev0[j] * iG;
+        r1[j] = vprev1[j] * iG;
+      }
+      store_row<J>(p.rho + (t + 1) * 2 * L, p.L, j0, r0);
+      store_row<J>(p.rho + (t + 1) * 2 * L + L, p.L, j0, r1);
+    }
+    if (t == 0) break;
+    // beta scaled so that sum alpha*beta = 1, then step back
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      vprev0[j] = e[j] * st.b0[j] * iG;
+      vprev1[j] = e[j] * st.b1[j] * iG;
+    }
+    has_prev = true;
+    st.transition_back(p, lds, j0, invz, vprev0, V1 * iG);
+  }
+}
+
+// From beta_{t+1} (in st) and the emission at t+1, form v = e*beta (scaled to sum 1),
+// keep it in (vp0, vp1) and step st back to beta_t.
+template <int J, int WP>
+__device__ void bwd_boundary(const FBParams& p, Bwd<J, WP>& st, float* lds, int j0,
+                             const float invz[J], int64_t tnext, float vp0[J], float vp1[J]) {
+  EmRaw<J> r;
+  em_load<J>(p, tnext, j0, r);
+  float e[J];
+  em_exp<J>(p, j0, r, e);
+  float VS = 0.f, V1 = 0.f;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    vp0[j] = e[j] * st.b0[j];
+    vp1[j] = e[j] * st.b1[j];
+    VS += vp0[j] + vp1[j];
+    V1 += vp1[j];
+  }
+  wave_sum2(VS, V1);
+  const float sc = 1.f / VS;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    vp0[j] *= sc;
+    vp1[j] *= sc;
+  }
+  st.transition_back(p, lds, j0, invz, vp0, V1 * sc);
+}
+
+template <int J, int WP>
+__global__ void __launch_bounds__(64) k_backward(FBParams p) {
+  __shared__ __attribute__((aligned(16))) float lds[64 * J + 2 * WP];
+  const int lane = threadIdx.x;
+  const int j0 = lane * J;
+  for (int k = lane; k < 64 * J + 2 * WP; k += 64) lds[k] = 0.f;
+  __syncthreads();
+  const int c = blockIdx.x;
+  if (c >= p.M) return;
+  float invz[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) invz[j] = (j0 + j < p.L) ? p.invz[j0 + j] : 0.f;
+  const int64_t t_c = (int64_t)c * p.C;
+  const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
+  const size_t SZ = (size_t)2 * p.Lpad;
+  Bwd<J, WP> st;
+  st.init_ones(p, j0);
+  float vp0[J], vp1[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) vp0[j] = vp1[j] = 0.f;
+  bool has_prev = false;
+  if (c < p.M - 1) {
+    int64_t t_w = t_e + p.B;  // beta guess (ones) at t_w, exact when t_w is the last bin
+    if (t_w > p.T - 1) t_w = p.T - 1;
+    bwd_warm<J, WP>(p, st, lds, j0, invz, t_w, t_e);          // -> beta_{t_e}
+    bwd_boundary<J, WP>(p, st, lds, j0, invz, t_e, vp0, vp1);  // -> beta_{t_e - 1}
+    has_prev = true;
+    st.save_state(p, p.b_in + (size_t)c * SZ, j0);
+  }
+  bwd_out<J, WP>(p, st, lds, j0, invz, t_c, t_e, vp0, vp1, has_prev);
+  if (c > 0) st.save_state(p, p.b_out + (size_t)c * SZ, j0);
+}
+
+template <int J, int WP>
+__global__ void __launch_bounds__(64) k_backward_repair(FBParams p) {
+  __shared__ __attribute__((aligned(16))) float lds[64 * J + 2 * WP];
+  const int lane = threadIdx.x;
+  const int j0 = lane * J;
+  for (int k = lane; k < 64 * J + 2 * WP; k += 64) lds[k] = 0.f;
+  __syncthreads();
+  float invz[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) invz[j] = (j0 + j < p.L) ? p.invz[j0 + j] : 0.f;
+  const size_t SZ = (size_t)2 * p.Lpad;
+  int repairs = 0;
+  bool changed = false;
+  int c = p.M - 2;
+  while (c >= 0) {
+    if (!changed) {
+      int found = -1;
+      for (int top = c; top >= 0 && found < 0; top -= 64) {
+        const int idx = top - lane;
+        const bool f = idx >= 0 && p.flags[idx] != 0;
+        const unsigned long long bal = __ballot(f);
+        if (bal) found = top - (int)__builtin_ctzll(bal);
+      }
+      if (found < 0) break;
+      c = found;
+    }
+    const int64_t t_c = (int64_t)c * p.C;
+    const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
+    // restart from the successor's first smoothed beta (beta_{t_e}, b_first[c+1])
+    Bwd<J, WP> st;
+    st.load_state(p, p.b_first + (size_t)(c + 1) * SZ, j0);
+    float vp0[J], vp1[J];
+    bwd_boundary<J, WP>(p, st, lds, j0, invz, t_e, vp0, vp1);
+    st.save_state(p, p.b_in + (size_t)c * SZ, j0);
+    bwd_out<J, WP>(p, st, lds, j0, invz, t_c, t_e, vp0, vp1, true);
+    if (c > 0) {
+      const float d = hilbert_reg<J>(st.b0, st.b1, p.b_out + (size_t)c * SZ, p.Lpad, j0);
+      changed = !(d <= p.tol);
+      st.save_state(p, p.b_out + (size_t)c * SZ, j0);
+    } else {
+      changed = false;
+    }
+    __threadfence();
+    ++repairs;
+    --c;
+  }
+  if (lane == 0) p.repairs[1] = repairs;
+}
+
+// ---------------------------------------------------------------------------
+// host dispatch
+// ---------------------------------------------------------------------------
+struct FBWork {
+  float *s_in, *s_out, *b_in, *b_out, *b_first;
+  double* chunk_logz;
+  int* flags;
+  int* repairs;
+};
+
+static FBWork carve_fb(void* ws, int64_t T, int Lpad, int C) {
+  const int64_t M = (T + C - 1) / C;
+  Carver c(ws);
+  FBWork w;
+  w.repairs = c.take<int>(64);
+  w.s_in = c.take<float>((size_t)M * 2 * Lpad);
+  w.s_out = c.take<float>((size_t)M * 2 * Lpad);
+  w.b_in = c.take<float>((size_t)M * 2 * Lpad);
+  w.b_out = c.take<float>((size_t)M * 2 * Lpad);
+  w.b_first = c.take<float>((size_t)M * 2 * Lpad);
+  w.chunk_logz = c.take<double>(M);
+  w.flags = c.take<int>(M);
+  (void)w;
+  return w;
+}
+
+static int pick_J(int L) {
+  if (L <= 64) return 1;
+  if (L <= 128) return 2;
+  if (L <= 256) return 4;
+  if (L <= 512) return 8;
+  if (L <= 1024) return 16;
+  return -1;
+}
+static int pick_WP(int band) {
+  if (band <= 4) return 4;
+  if (band <= 8) return 8;
+  if (band <= 12) return 12;
+  if (band <= 16) return 16;
+  if (band <= 24) return 24;
+  if (band <= 32) return 32;
+  return -1;
+}
+
+typedef void (*fb_kernel_t)(FBParams);
+
+#define PMG_FB_TABLE(NAME)                                                                 \
+  static fb_kernel_t NAME##_table(int J, int WP) {                                         \
+    switch (J * 100 + WP) {                                                                \
+      case 104: return NAME<1, 4>;   case 108: return NAME<1, 8>;                          \
+      case 112: return NAME<1, 12>;  case 116: return NAME<1, 16>;                         \
+      case 124: return NAME<1, 24>;  case 132: return NAME<1, 32>;                         \
+      case 204: return NAME<2, 4>;   case 208: return NAME<2, 8>;                          \
+      case 212: return NAME<2, 12>;  case 216: return NAME<2, 16>;                         \
+      case 224: return NAME<2, 24>;  case 232: return NAME<2, 32>;                         \
+      case 404: return NAME<4, 4>;   case 408: return NAME<4, 8>;                          \
+      case 412: return NAME<4, 12>;  case 416: return NAME<4, 16>;                         \
+      case 424: return NAME<4, 24>;  case 432: return NAME<4, 32>;                         \
+      case 804: return NAME<8, 4>;   case 808: return NAME<8, 8>;                          \
+      case 812: return NAME<8, 12>;  case 816: return NAME<8, 16>;                         \
+      case 824: return NAME<8, 24>;  case 832: return NAME<8, 32>;                         \
+      case 1604: return NAME<16, 4>; case 1608: return NAME<16, 8>;                        \
+      case 1612: return NAME<16, 12>; case 1616: return NAME<16, 16>;                      \
+      case 1624: return NAME<16, 24>; case 1632: return NAME<16, 32>;                      \
+      default: return nullptr;                                                             \
+    }                                                                                      \
+  }
+
+PMG_FB_TABLE(k_forward)
+PMG_FB_TABLE(k_forward_repair)
+PMG_FB_TABLE(k_backward)
+PMG_FB_TABLE(k_backward_repair)
+
+static int fill_params(FBParams& p, const pmg_transition* tr, int64_t T, int C, int B,
+                       double s, double tol) {
+  PMG_REQUIRE(tr && tr->L > 0 && tr->invz, "pmg fwd/bwd: bad transition");
+  PMG_REQUIRE(tr->band >= 0 && tr->band <= kMaxBand,
+              "pmg fwd/bwd: continuous-kernel band %d > %d unsupported (dense kernels: not yet)",
+              tr->band, kMaxBand);
+  PMG_REQUIRE(T > 0 && C > 0 && B >= 0, "pmg fwd/bwd: T=%lld chunk=%d warmup=%d", (long long)T, C, B);
+  const int J = pick_J(tr->L);
+  PMG_REQUIRE(J > 0, "pmg fwd/bwd: L=%d > 1024 unsupported", tr->L);
+  memset(&p, 0, sizeof(p));
+  p.T = T;
+  p.L = tr->L;
+  p.nblk = (int)(round_up(tr->L, 32) / 32);
+  p.invz = tr->invz;
+  p.A00 = tr->A[0];
+  p.A01 = tr->A[1];
+  p.A10 = tr->A[2];
+  p.A11 = tr->A[3];
+  p.invL = 1.f / (float)tr->L;
+  p.s = (float)s;
+  p.s_d = s;
+  p.C = C;
+  p.B = B;
+  p.M = (int)((T + C - 1) / C);
+  p.tol = (float)tol;
+  p.Lpad = 64 * J;
+  for (int k = 0; k <= kMaxBand; ++k) p.g[k] = (k <= tr->band) ? tr->g[k] : 0.f;
+  return PMG_OK;
+}
+
+}  // namespace pmg
+
+using namespace pmg;
+
+extern "C" {
+
+size_t pmg_fwdbwd_workspace_size(int64_t T, int32_t L, int32_t chunk) {
+  const int J = pick_J(L);
+  if (J < 0 || chunk <= 0) return 0;
+  Carver c(nullptr);
+  FBWork w = carve_fb(nullptr, T, 64 * J, chunk);
+  (void)w;
+  const int64_t M = (T + chunk - 1) / chunk;
+  c.take<int>(64);
+  c.take<float>((size_t)M * 2 * 64 * J);
+  c.take<float>((size_t)M * 2 * 64 * J);
+  c.take<float>((size_t)M * 2 * 64 * J);
+  c.take<float>((size_t)M * 2 * 64 * J);
+  c.take<float>((size_t)M * 2 * 64 * J);
+  c.take<double>(M);
+  c.take<int>(M);
+  return c.off + 256;
+}
+
+size_t pmg_fwdbwd_repair_counter_offset(int64_t T, int32_t L, int32_t chunk) {
+  (void)T; (void)L; (void)chunk;
+  return 0;  // repairs[0] (forward), repairs[1] (backward) at the workspace start
+}
+
+int pmg_forward_filter(const float* delta, const float* phi, const double* m, int64_t T,
+                       const pmg_transition* tr, double likelihood_scale, int32_t chunk,
+                       int32_t warmup, double tol, float* alpha, double* logc, double* logz,
+                       void* workspace, size_t workspace_bytes, void* stream) {
+  FBParams p;
+  int rc = fill_params(p, tr, T, chunk, warmup, likelihood_scale, tol);
+  if (rc) return rc;
+  PMG_REQUIRE(delta && phi && m && alpha && logc && logz && workspace, "pmg_forward_filter: null");
+  PMG_REQUIRE(workspace_bytes >= pmg_fwdbwd_workspace_size(T, tr->L, chunk),
+              "pmg_forward_filter: workspace too small");
+  hipStream_t st = as_stream(stream);
+  FBWork w = carve_fb(workspace, T, p.Lpad, chunk);
+  p.delta = delta;
+  p.phi = phi;
+  p.m = m;
+  p.alpha = alpha;
+  p.logc = logc;
+  p.chunk_logz = w.chunk_logz;
+  p.s_in = w.s_in;
+  p.s_out = w.s_out;
+  p.flags = w.flags;
+  p.repairs = w.repairs;
+  const int J = p.Lpad / 64, WP = pick_WP(tr->band);
+  fb_kernel_t kf = k_forward_table(J, WP), kr = k_forward_repair_table(J, WP);
+  PMG_REQUIRE(kf && kr, "pmg_forward_filter: no kernel for J=%d WP=%d", J, WP);
+  PMG_HIP(hipMemsetAsync(w.repairs, 0, 2 * sizeof(int), st));
+  hipLaunchKernelGGL(kf, dim3(p.M), dim3(64), 0, st, p);
+  PMG_LAUNCH_CHECK();
+  if (p.M > 1) {
+    PMG_HIP(hipMemsetAsync(w.flags, 0, sizeof(int) * p.M, st));
+    const int nver = p.M - 1;
+    hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4), dim3(256), 0, st, (const float*)w.s_in,
+                       (const float*)w.s_out, 1, p.M - 1, -1, 2 * p.Lpad, p.tol, w.flags, p.M);
+    PMG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(kr, dim3(1), dim3(64), 0, st, p);
+    PMG_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(k_sum_f64, dim3(1), dim3(256), 0, st, (const double*)w.chunk_logz, p.M, logz);
+  PMG_LAUNCH_CHECK();
+  return PMG_OK;
+}
+
+int pmg_backward_smoother(const float* delta, const float* phi, const float* alpha, int64_t T,
+                          const pmg_transition* tr, double likelihood_scale, int32_t chunk,
+                          int32_t warmup, double tol, float* P, float* gamma, float* rho,
+                          void* workspace, size_t workspace_bytes, void* stream) {
+  FBParams p;
+  int rc = fill_params(p, tr, T, chunk, warmup, likelihood_scale, tol);
+  if (rc) return rc;
+  PMG_REQUIRE(delta && phi && alpha && workspace, "pmg_backward_smoother: null");
+  PMG_REQUIRE(workspace_bytes >= pmg_fwdbwd_workspace_size(T, tr->L, chunk),
+              "pmg_backward_smoother: workspace too small");
+  hipStream_t st = as_stream(stream);
+  FBWork w = carve_fb(workspace, T, p.Lpad, chunk);
+  p.delta = delta;
+  p.phi = phi;
+  p.alpha_in = alpha;
+  p.P = P;
+  p.gamma = gamma;
+  p.rho = rho;
+  p.b_in = w.b_in;
+  p.b_out = w.b_out;
+  p.b_first = w.b_first;
+  p.flags = w.flags;
+  p.repairs = w.repairs;
+  const int J = p.Lpad / 64, WP = pick_WP(tr->band);
+  fb_kernel_t kb = k_backward_table(J, WP), kr = k_backward_repair_table(J, WP);
+  PMG_REQUIRE(kb && kr, "pmg_backward_smoother: no kernel for J=%d WP=%d", J, WP);
+  hipLaunchKernelGGL(kb, dim3(p.M), dim3(64), 0, st, p);
+  PMG_LAUNCH_CHECK();
+  if (p.M > 1) {
+    PMG_HIP(hipMemsetAsync(w.flags, 0, sizeof(int) * p.M, st));
+    const int nver = p.M - 1;
+    hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4), dim3(256), 0, st, (const float*)w.b_in,
+                       (const float*)w.b_out, 0, p.M - 2, 1, 2 * p.Lpad, p.tol, w.flags, p.M);
+    PMG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(kr, dim3(1), dim3(64), 0, st, p);
+    PMG_LAUNCH_CHECK();
+  }
+  return PMG_OK;
+}
+
+}  // extern "C"

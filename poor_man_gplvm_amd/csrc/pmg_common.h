@@ -1,0 +1,144 @@
+// Shared helpers for the gfx950 kernels of libpmg_hip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/pmg.h"
+
+namespace pmg {
+
+// thread-local last error message (pmg_last_error)
+void set_error(const char* fmt, ...);
+
+#define PMG_HIP(call)                                                            \
+  do {                                                                           \
+    hipError_t e_ = (call);                                                      \
+    if (e_ != hipSuccess) {                                                      \
+      ::pmg::set_error("%s:%d %s: %s", __FILE__, __LINE__, #call,                \
+                       hipGetErrorString(e_));                                   \
+      return PMG_EHIP;                                                           \
+    }                                                                            \
+  } while (0)
+
+#define PMG_LAUNCH_CHECK()                                                       \
+  do {                                                                           \
+    hipError_t e_ = hipGetLastError();                                           \
+    if (e_ != hipSuccess) {                                                      \
+      ::pmg::set_error("%s:%d launch: %s", __FILE__, __LINE__,                   \
+                       hipGetErrorString(e_));                                   \
+      return PMG_EHIP;                                                           \
+    }                                                                            \
+  } while (0)
+
+#define PMG_REQUIRE(cond, ...)                                                   \
+  do {                                                                           \
+    if (!(cond)) {                                                               \
+      ::pmg::set_error(__VA_ARGS__);                                             \
+      return PMG_EINVAL;                                                         \
+    }                                                                            \
+  } while (0)
+
+static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+static inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+// workspace carving: 256-byte aligned slices
+struct Carver {
+  char* base;
+  size_t off;
+  explicit Carver(void* b) : base(static_cast<char*>(b)), off(0) {}
+  template <class T>
+  T* take(size_t count) {
+    off = (off + 255) & ~size_t(255);
+    T* p = reinterpret_cast<T*>(base ? base + off : nullptr);
+    off += count * sizeof(T);
+    return p;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// wave64 reductions through DPP (row ops) + row_bcast, result broadcast from
+// lane 63 with readlane (wave-uniform SGPR value).
+// dpp_ctrl: quad_perm[1,0,3,2]=0xB1, quad_perm[2,3,0,1]=0x4E,
+// row_half_mirror=0x141, row_mirror=0x140, row_bcast15=0x142, row_bcast31=0x143
+// ---------------------------------------------------------------------------
+template <int CTRL, int ROWMASK = 0xf, int BANKMASK = 0xf, bool BC = false>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(
+      __builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWMASK, BANKMASK, BC));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+  v += dppf<0xB1>(v);
+  v += dppf<0x4E>(v);
+  v += dppf<0x141>(v);
+  v += dppf<0x140>(v);
+  v += dppf<0x142, 0xa>(v);
+  v += dppf<0x143, 0xc>(v);
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+// two independent sums (interleaved for ILP)
+__device__ __forceinline__ void wave_sum2(float& a, float& b) {
+  a += dppf<0xB1>(a);
+  b += dppf<0xB1>(b);
+  a += dppf<0x4E>(a);
+  b += dppf<0x4E>(b);
+  a += dppf<0x141>(a);
+  b += dppf<0x141>(b);
+  a += dppf<0x140>(a);
+  b += dppf<0x140>(b);
+  a += dppf<0x142, 0xa>(a);
+  b += dppf<0x142, 0xa>(b);
+  a += dppf<0x143, 0xc>(a);
+  b += dppf<0x143, 0xc>(b);
+  a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a), 63));
+  b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(b), 63));
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+  v = fmaxf(v, dppf<0xB1>(v));
+  v = fmaxf(v, dppf<0x4E>(v));
+  v = fmaxf(v, dppf<0x141>(v));
+  v = fmaxf(v, dppf<0x140>(v));
+  v = fmaxf(v, dppf<0x142, 0xa>(v));
+  v = fmaxf(v, dppf<0x143, 0xc>(v));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+// f64 reductions via shuffles (used off the critical path)
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_max_f64(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float wave_min_shfl(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float wave_max_shfl(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// jax.nn.softplus == logaddexp(x, 0)
+__device__ __forceinline__ double softplus_d(double x) {
+  return fmax(x, 0.0) + log1p(exp(-fabs(x)));
+}
+__device__ __forceinline__ float softplus_f(float x) {
+  return fmaxf(x, 0.f) + log1pf(__expf(-fabsf(x)));
+}
+__device__ __forceinline__ float sigmoid_f(float x) {
+  return 1.f / (1.f + __expf(-x));
+}
+
+}  // namespace pmg

@@ -1,0 +1,185 @@
+// Small elementwise / per-row kernels of the EM hot path and the ABI plumbing.
+//   spikes preparation  (y handling of decoder.py:30-71, fit_tuning_helper.py:28-42)
+//   tuning softplus     (fit_tuning_helper.py:19-25)
+//   emission row reference, log-likelihood materialisation, exp / log maps
+#include <stdarg.h>
+
+#include "pmg_common.h"
+
+namespace pmg {
+
+static thread_local char g_err[512];
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+// One wave per time row: y*ma -> int8 operand, gammaln constant, f32 copy with a
+// ones column, integrality / mask flags.
+__global__ void __launch_bounds__(256) k_spikes_prepare(
+    const float* __restrict__ y, int64_t T, int N, const float* __restrict__ ma, int ma_2d,
+    int8_t* __restrict__ yq, int Kp, double* __restrict__ gconst, float* __restrict__ yext,
+    int Np, int* __restrict__ flags, int64_t Tp) {
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (t >= Tp) return;
+  if (t >= T) {  // zero padding rows of the int8 operand
+    for (int n = lane; n < Kp; n += 64) yq[t * Kp + n] = 0;
+    return;
+  }
+  const float* yr = y + t * (int64_t)N;
+  const float* mr = ma ? (ma_2d ? ma + t * (int64_t)N : ma) : nullptr;
+  double g = 0.0;
+  int bad = 0;
+  for (int n = lane; n < Kp; n += 64) {
+    float v = 0.f, m = 1.f;
+    if (n < N) {
+      v = yr[n];
+      if (mr) m = mr[n];
+      if (!(m == 0.f || m == 1.f)) bad |= PMG_YFLAG_MASK;
+      if (!(v >= 0.f && v <= 127.f && v == rintf(v))) bad |= PMG_YFLAG_NONINT;
+      if (m != 0.f) g += (double)m * lgamma((double)v + 1.0);
+    }
+    float ym = (n < N) ? v * m : 0.f;
+    yq[t * Kp + n] = (int8_t)(int)fminf(fmaxf(ym, -128.f), 127.f);
+  }
+  for (int n = lane; n < Np; n += 64) {
+    float v = (n < N) ? yr[n] : (n == N ? 1.f : 0.f);
+    yext[t * (int64_t)Np + n] = v;
+  }
+  g = wave_sum_f64(g);
+  if (lane == 0) gconst[t] = g;
+  unsigned long long anybad = __ballot(bad != 0);
+  if (anybad) {
+    int b = bad;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) b |= __shfl_xor(b, o, 64);
+    if (lane == 0) atomicOr(flags, b);
+  }
+}
+
+__global__ void k_tuning_softplus(const float* __restrict__ basis, const double* __restrict__ W,
+                                  int L, int NB, int N, double* __restrict__ t64,
+                                  float* __restrict__ t32) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int l = blockIdx.y;
+  if (n >= N) return;
+  const float* br = basis + (int64_t)l * NB;
+  double acc = 0.0;
+  for (int k = 0; k < NB; ++k) acc = fma((double)br[k], W[(int64_t)k * N + n], acc);
+  double f = softplus_d(acc);
+  if (t64) t64[(int64_t)l * N + n] = f;
+  if (t32) t32[(int64_t)l * N + n] = (float)f;
+}
+
+__global__ void k_rowref(const double* __restrict__ rblk, int64_t T, int nblk, double s,
+                         float* __restrict__ phi, double* __restrict__ m) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= T) return;
+  const double* r = rblk + t * nblk;
+  double mx = -INFINITY;
+  for (int b = 0; b < nblk; ++b) mx = fmax(mx, r[b]);
+  if (mx == -INFINITY) mx = 0.0;  // cannot happen for L >= 1 (masked latents are -1e20)
+  m[t] = mx;
+  for (int b = 0; b < nblk; ++b) phi[t * nblk + b] = (float)(s * (r[b] - mx));
+}
+
+__global__ void k_loglik(const float* __restrict__ delta, const double* __restrict__ rblk,
+                         int64_t T, int L, int nblk, float* __restrict__ ll) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= T * (int64_t)L) return;
+  const int64_t t = i / L;
+  const int l = (int)(i - t * L);
+  ll[i] = (float)((double)delta[i] + rblk[t * nblk + (l >> 5)]);
+}
+
+__global__ void k_exp(const float* __restrict__ x, int64_t n, float* __restrict__ y) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) y[i] = expf(x[i]);
+}
+__global__ void k_log(const float* __restrict__ x, int64_t n, float* __restrict__ y) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) y[i] = logf(x[i]);
+}
+
+}  // namespace pmg
+
+using namespace pmg;
+
+extern "C" {
+
+int pmg_abi_version(void) { return PMG_ABI_VERSION; }
+const char* pmg_last_error(void) { return g_err; }
+
+int pmg_spikes_prepare(const float* y, int64_t T, int32_t N, const float* ma_neuron,
+                       int32_t ma_is_2d, int8_t* yq_out, int32_t Kp, double* gconst_out,
+                       float* yext_out, int32_t Np, int32_t* flags_out, void* stream) {
+  PMG_REQUIRE(T > 0 && N > 0, "pmg_spikes_prepare: T=%lld N=%d", (long long)T, N);
+  PMG_REQUIRE(Kp >= N && Kp % 32 == 0, "pmg_spikes_prepare: Kp=%d must be >= N and a multiple of 32", Kp);
+  PMG_REQUIRE(Np >= N + 1 && Np % 64 == 0, "pmg_spikes_prepare: Np=%d must be >= N+1 and a multiple of 64", Np);
+  PMG_REQUIRE(y && yq_out && gconst_out && yext_out && flags_out, "pmg_spikes_prepare: null pointer");
+  hipStream_t st = as_stream(stream);
+  PMG_HIP(hipMemsetAsync(flags_out, 0, sizeof(int32_t), st));
+  const int64_t Tp = round_up(T, 64);
+  const int waves = 4;
+  dim3 grid((unsigned)((Tp + waves - 1) / waves));
+  hipLaunchKernelGGL(k_spikes_prepare, grid, dim3(64 * waves), 0, st, y, T, N, ma_neuron,
+                     ma_is_2d, yq_out, Kp, gconst_out, yext_out, Np, flags_out, Tp);
+  PMG_LAUNCH_CHECK();
+  return PMG_OK;
+}
+
+int pmg_tuning_softplus(const float* basis, const double* W, int32_t L, int32_t NB, int32_t N,
+                        double* tuning64, float* tuning32, void* stream) {
+  PMG_REQUIRE(L > 0 && NB > 0 && N > 0 && basis && W, "pmg_tuning_softplus: bad args");
+  dim3 grid((N + 127) / 128, L);
+  hipLaunchKernelGGL(k_tuning_softplus, grid, dim3(128), 0, as_stream(stream), basis, W, L, NB,
+                     N, tuning64, tuning32);
+  PMG_LAUNCH_CHECK();
+  return PMG_OK;
+}
+
+int pmg_emission_rowref(const double* rblk, int64_t T, int32_t nblk, double likelihood_scale,
+                        float* phi, double* m, void* stream) {
+  PMG_REQUIRE(T > 0 && nblk > 0 && rblk && phi && m, "pmg_emission_rowref: bad args");
+  hipLaunchKernelGGL(k_rowref, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), rblk, T, nblk, likelihood_scale, phi, m);
+  PMG_LAUNCH_CHECK();
+  return PMG_OK;
+}
+
+int pmg_loglik_materialize(const float* delta, const double* rblk, int64_t T, int32_t L,
+                           float* ll, void* stream) {
+  PMG_REQUIRE(T > 0 && L > 0 && delta && rblk && ll, "pmg_loglik_materialize: bad args");
+  const int64_t n = T * (int64_t)L;
+  const int nblk = (int)(round_up(L, 32) / 32);
+  hipLaunchKernelGGL(k_loglik, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), delta, rblk, T, L, nblk, ll);
+  PMG_LAUNCH_CHECK();
+  return PMG_OK;
+}
+
+int pmg_exp(const float* logp, int64_t n, float* p, void* stream) {
+  PMG_REQUIRE(n >= 0 && logp && p, "pmg_exp: bad args");
+  if (n == 0) return PMG_OK;
+  unsigned blocks = (unsigned)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
+  hipLaunchKernelGGL(k_exp, dim3(blocks), dim3(256), 0, as_stream(stream), logp, n, p);
+  PMG_LAUNCH_CHECK();
+  return PMG_OK;
+}
+
+int pmg_log(const float* x, int64_t n, float* out, void* stream) {
+  PMG_REQUIRE(n >= 0 && x && out, "pmg_log: bad args");
+  if (n == 0) return PMG_OK;
+  unsigned blocks = (unsigned)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
+  hipLaunchKernelGGL(k_log, dim3(blocks), dim3(256), 0, as_stream(stream), x, n, out);
+  PMG_LAUNCH_CHECK();
+  return PMG_OK;
+}
+
+}  // extern "C"

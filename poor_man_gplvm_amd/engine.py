@@ -1,0 +1,286 @@
+"""Device-resident EM engine for PoissonGPLVMJump1D on one MI355X.
+
+Orchestrates the native kernels of ``libpmg_hip.so`` for one fit:
+
+    M-step   pmg_suffstats  -> pmg_mstep_adam            (core.py:802-827)
+    tuning   pmg_tuning_softplus                          (core.py:664, :772)
+    E-step   pmg_emission_poisson -> pmg_emission_rowref
+             -> pmg_forward_filter -> pmg_backward_smoother  (core.py:666 -> decoder.py:258-332)
+             P = sum_d gamma feeds the next M-step          (core.py:668)
+
+All tensors live on the GPU (torch allocations, torch's current stream); the host
+only reads back per-iteration scalars at the end of a fit and the posteriors the
+caller asks for.  There is no CPU fallback: a missing library or an unsupported
+configuration raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from .gp_kernel import BandedTransition, banded_transition
+
+
+def _ru(x, m):
+    return (int(x) + m - 1) // m * m
+
+
+@dataclass
+class AdamConfig:
+    lr: float = 0.01
+    maxiter: int = 1000
+    tol: float = 1e-6
+    prior_std: float = 1.0
+    b1: float = 0.9
+    b2: float = 0.999
+    eps: float = 1e-8
+    eps_root: float = 0.0
+
+    def to_c(self):
+        return nat.AdamCfg(self.lr, self.b1, self.b2, self.eps, self.eps_root, self.prior_std,
+                           self.tol, int(self.maxiter))
+
+
+@dataclass
+class ScanConfig:
+    """Time-parallel scan parameters (see fwdbwd.hip)."""
+    chunk: int | None = None     # time steps per chunk (None: ~2048 chunks)
+    warmup: int = 48             # forgetting warm-up before each chunk
+    tol: float = 1e-6            # Hilbert-metric boundary tolerance
+
+    def chunk_for(self, T):
+        if self.chunk:
+            return int(self.chunk)
+        return max(32, int(math.ceil(T / 2048)))
+
+
+def default_device():
+    if not torch.cuda.is_available():
+        raise nat.NativeError("poor_man_gplvm_amd needs a ROCm GPU (torch.cuda.is_available() is False)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+class SpikeData:
+    """Spike counts prepared once per fit (pmg_spikes_prepare)."""
+
+    def __init__(self, y, ma_neuron=None, device=None):
+        lib = nat.load()
+        dev = device or default_device()
+        y = np.asarray(y)
+        if y.ndim != 2:
+            raise ValueError(f"y must be (n_time, n_neuron), got {y.shape}")
+        self.T, self.N = int(y.shape[0]), int(y.shape[1])
+        self.device = dev
+        self.y = torch.as_tensor(np.ascontiguousarray(y, dtype=np.float32), device=dev)
+        self.Kp = _ru(self.N, 32)
+        self.Np = _ru(self.N + 1, 64)
+        self.Tp = _ru(self.T, 64)
+        self.ma_2d = False
+        self.ma = None
+        if ma_neuron is not None:
+            ma = np.asarray(ma_neuron, dtype=np.float32)
+            if ma.ndim == 2:
+                if ma.shape != (self.T, self.N):
+                    raise ValueError(f"2-D ma_neuron must be {(self.T, self.N)}, got {ma.shape}")
+                self.ma_2d = True
+            elif ma.shape != (self.N,):
+                raise ValueError(f"ma_neuron must be ({self.N},) or ({self.T},{self.N}), got {ma.shape}")
+            if not (ma.ndim == 1 and np.all(ma == 1.0)):
+                self.ma = torch.as_tensor(np.ascontiguousarray(ma), device=dev)
+        self.yq = torch.empty((self.Tp, self.Kp), dtype=torch.int8, device=dev)
+        self.gconst = torch.empty(self.T, dtype=torch.float64, device=dev)
+        self.yext = torch.empty((self.T, self.Np), dtype=torch.float32, device=dev)
+        flags = torch.zeros(1, dtype=torch.int32, device=dev)
+        nat.check(lib.pmg_spikes_prepare(nat.ptr(self.y), self.T, self.N, nat.ptr(self.ma),
+                                         int(self.ma_2d), nat.ptr(self.yq), self.Kp,
+                                         nat.ptr(self.gconst), nat.ptr(self.yext), self.Np,
+                                         nat.ptr(flags), nat.stream_handle()),
+                  "pmg_spikes_prepare")
+        self.flags = int(flags.item())
+        # exact int8 path: integer counts in [0,127], 0/1 mask, no per-time mask
+        self.int_path = self.flags == 0 and not self.ma_2d
+
+
+class DeviceEM:
+    """One fit's device state: spikes, basis, transition, workspaces, buffers."""
+
+    def __init__(self, spikes: SpikeData, L: int, basis=None, scan: ScanConfig | None = None):
+        self.lib = nat.load()
+        self.sp = spikes
+        self.dev = spikes.device
+        self.T, self.N, self.L = spikes.T, spikes.N, int(L)
+        self.scan = scan or ScanConfig()
+        self.C = self.scan.chunk_for(self.T)
+        self.nblk = _ru(self.L, 32) // 32
+        T, L, N, dev = self.T, self.L, self.N, self.dev
+        f32, f64 = torch.float32, torch.float64
+        self.basis = None
+        if basis is not None:
+            b = np.ascontiguousarray(basis, dtype=np.float32)
+            if b.shape[0] != L:
+                raise ValueError("basis must have n_latent_bin rows")
+            self.NB = int(b.shape[1])
+            self.basis = torch.as_tensor(b, device=dev)
+        self.delta = torch.empty((T, L), dtype=f32, device=dev)
+        self.rblk = torch.empty((T, self.nblk), dtype=f64, device=dev)
+        self.phi = torch.empty((T, self.nblk), dtype=f32, device=dev)
+        self.mref = torch.empty(T, dtype=f64, device=dev)
+        self.alpha = torch.empty((T, 2, L), dtype=f32, device=dev)
+        self.logc = torch.empty(T, dtype=f64, device=dev)
+        self.P = torch.empty((T, L), dtype=f32, device=dev)
+        self.tuning64 = torch.empty((L, N), dtype=f64, device=dev)
+        self.tuning32 = torch.empty((L, N), dtype=f32, device=dev)
+        self.yw = torch.empty((L, N), dtype=f64, device=dev)
+        self.tw = torch.empty(L, dtype=f64, device=dev)
+        self.ws_em = torch.empty(int(self.lib.pmg_emission_workspace_size(T, L, N)), dtype=torch.uint8, device=dev)
+        self.ws_fb = torch.empty(int(self.lib.pmg_fwdbwd_workspace_size(T, L, self.C)), dtype=torch.uint8, device=dev)
+        self.ws_ss = torch.empty(int(self.lib.pmg_suffstats_workspace_size(T, L, spikes.Np)), dtype=torch.uint8, device=dev)
+        if self.ws_fb.numel() == 0:
+            raise nat.NativeError(f"n_latent_bin={L} unsupported by the scan kernels (max 1024)")
+        self.ws_ad = None
+        self._tr = None
+        self._tr_c = None
+        self._invz = None
+        self.ma_latent = None
+
+    # ------------------------------------------------------------------ setup
+    def set_transition(self, tr: BandedTransition):
+        if tr.L != self.L:
+            raise ValueError("transition size mismatch")
+        self._tr = tr
+        self._invz = torch.as_tensor(tr.invz, device=self.dev)
+        c = nat.Transition()
+        c.L = tr.L
+        c.band = tr.band
+        for k in range(tr.band + 1):
+            c.g[k] = float(tr.g[k])
+        c.invz = nat.ptr(self._invz)
+        A = tr.A.astype(np.float32)
+        c.A[0], c.A[1], c.A[2], c.A[3] = float(A[0, 0]), float(A[0, 1]), float(A[1, 0]), float(A[1, 1])
+        self._tr_c = c
+
+    def set_ma_latent(self, ma_latent):
+        if ma_latent is None:
+            self.ma_latent = None
+            return
+        m = np.asarray(ma_latent)
+        if m.shape != (self.L,):
+            raise ValueError(f"ma_latent must have shape ({self.L},)")
+        if np.all(m != 0):
+            self.ma_latent = None
+        else:
+            self.ma_latent = torch.as_tensor((m != 0).astype(np.uint8), device=self.dev)
+
+    def set_log_posterior(self, log_post):
+        """P = exp(log_posterior) (T, L) for the first M-step (fit_tuning_helper.py:38)."""
+        lp = torch.as_tensor(np.ascontiguousarray(log_post, dtype=np.float32), device=self.dev)
+        if tuple(lp.shape) != (self.T, self.L):
+            raise ValueError(f"log_posterior must be {(self.T, self.L)}")
+        nat.check(self.lib.pmg_exp(nat.ptr(lp), lp.numel(), nat.ptr(self.P), nat.stream_handle()), "pmg_exp")
+
+    # ------------------------------------------------------------------ M-step
+    def m_step(self, W, mu, nu, count, cfg: AdamConfig, stats_out, lh_out, eh_out):
+        """Sufficient statistics of self.P, then the Adam loop; W/mu/nu/count in place."""
+        sh = nat.stream_handle()
+        nat.check(self.lib.pmg_suffstats(nat.ptr(self.P), nat.ptr(self.sp.yext), self.T, self.L, self.N,
+                                         self.sp.Np, nat.ptr(self.yw), nat.ptr(self.tw),
+                                         nat.ptr(self.ws_ss), self.ws_ss.numel(), sh), "pmg_suffstats")
+        self.adam(W, mu, nu, count, cfg, stats_out, lh_out, eh_out)
+
+    def adam(self, W, mu, nu, count, cfg: AdamConfig, stats_out, lh_out, eh_out):
+        if self.basis is None:
+            raise ValueError("no basis")
+        need = int(self.lib.pmg_mstep_workspace_size(self.N, int(cfg.maxiter)))
+        if self.ws_ad is None or self.ws_ad.numel() < need:
+            self.ws_ad = torch.empty(need, dtype=torch.uint8, device=self.dev)
+        c = cfg.to_c()
+        nat.check(self.lib.pmg_mstep_adam(nat.ptr(W), nat.ptr(mu), nat.ptr(nu), nat.ptr(count),
+                                          nat.ptr(self.basis), nat.ptr(self.yw), nat.ptr(self.tw),
+                                          self.L, self.NB, self.N, ctypes.byref(c), nat.ptr(stats_out),
+                                          nat.ptr(lh_out), nat.ptr(eh_out), nat.ptr(self.ws_ad),
+                                          self.ws_ad.numel(), nat.stream_handle()), "pmg_mstep_adam")
+
+    def compute_tuning(self, W):
+        nat.check(self.lib.pmg_tuning_softplus(nat.ptr(self.basis), nat.ptr(W), self.L, self.NB, self.N,
+                                               nat.ptr(self.tuning64), nat.ptr(self.tuning32),
+                                               nat.stream_handle()), "pmg_tuning_softplus")
+
+    def set_tuning(self, tuning):
+        t = np.ascontiguousarray(tuning, dtype=np.float64)
+        if t.shape != (self.L, self.N):
+            raise ValueError(f"tuning must be {(self.L, self.N)}")
+        self.tuning64.copy_(torch.as_tensor(t, device=self.dev))
+        self.tuning32.copy_(self.tuning64.to(torch.float32))
+
+    # ------------------------------------------------------------------ E-step
+    def emission(self, likelihood_scale=1.0, dt=1.0):
+        sp, sh = self.sp, nat.stream_handle()
+        if sp.int_path:
+            ma1 = sp.ma if (sp.ma is not None and not sp.ma_2d) else None
+            nat.check(self.lib.pmg_emission_poisson(nat.ptr(sp.yq), nat.ptr(sp.gconst), nat.ptr(self.tuning64),
+                                                    nat.ptr(ma1), nat.ptr(self.ma_latent), float(dt), self.T,
+                                                    self.L, self.N, sp.Kp, nat.ptr(self.delta),
+                                                    nat.ptr(self.rblk), nat.ptr(self.ws_em),
+                                                    self.ws_em.numel(), sh), "pmg_emission_poisson")
+        else:
+            nat.check(self.lib.pmg_emission_poisson_f64(nat.ptr(sp.y), nat.ptr(sp.gconst), nat.ptr(self.tuning64),
+                                                        nat.ptr(sp.ma), int(sp.ma_2d), nat.ptr(self.ma_latent),
+                                                        float(dt), self.T, self.L, self.N, nat.ptr(self.delta),
+                                                        nat.ptr(self.rblk), nat.ptr(self.ws_em),
+                                                        self.ws_em.numel(), sh), "pmg_emission_poisson_f64")
+        nat.check(self.lib.pmg_emission_rowref(nat.ptr(self.rblk), self.T, self.nblk, float(likelihood_scale),
+                                               nat.ptr(self.phi), nat.ptr(self.mref), sh), "pmg_emission_rowref")
+
+    def forward(self, likelihood_scale, logz_out):
+        sc = self.scan
+        nat.check(self.lib.pmg_forward_filter(nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.mref), self.T,
+                                              ctypes.byref(self._tr_c), float(likelihood_scale), self.C,
+                                              int(sc.warmup), float(sc.tol), nat.ptr(self.alpha),
+                                              nat.ptr(self.logc), nat.ptr(logz_out), nat.ptr(self.ws_fb),
+                                              self.ws_fb.numel(), nat.stream_handle()), "pmg_forward_filter")
+
+    def backward(self, likelihood_scale, P=True, gamma=None, rho=None):
+        sc = self.scan
+        nat.check(self.lib.pmg_backward_smoother(nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.alpha),
+                                                 self.T, ctypes.byref(self._tr_c), float(likelihood_scale),
+                                                 self.C, int(sc.warmup), float(sc.tol),
+                                                 nat.ptr(self.P) if P else None, nat.ptr(gamma), nat.ptr(rho),
+                                                 nat.ptr(self.ws_fb), self.ws_fb.numel(), nat.stream_handle()),
+                  "pmg_backward_smoother")
+
+    def e_step(self, likelihood_scale, logz_out, gamma=None, rho=None):
+        self.emission(likelihood_scale)
+        self.forward(likelihood_scale, logz_out)
+        self.backward(likelihood_scale, True, gamma, rho)
+
+    def repairs(self):
+        """(forward, backward) chunks repaired by the last scans (device read: syncs)."""
+        r = self.ws_fb[:8].view(torch.int32).cpu().numpy()
+        return int(r[0]), int(r[1])
+
+    def loglik(self):
+        ll = torch.empty((self.T, self.L), dtype=torch.float32, device=self.dev)
+        nat.check(self.lib.pmg_loglik_materialize(nat.ptr(self.delta), nat.ptr(self.rblk), self.T, self.L,
+                                                  nat.ptr(ll), nat.stream_handle()), "pmg_loglik_materialize")
+        return ll
+
+    def joint(self, rho):
+        """S[x,x'] = sum_t alpha_t[x] rho_{t+1}[x'] (2L x 2L, f64)."""
+        ws = torch.empty(int(self.lib.pmg_joint_workspace_size(self.T, self.L)), dtype=torch.uint8, device=self.dev)
+        S = torch.empty((2 * self.L, 2 * self.L), dtype=torch.float64, device=self.dev)
+        nat.check(self.lib.pmg_joint_accumulate(nat.ptr(self.alpha), nat.ptr(rho), self.T, self.L, nat.ptr(S),
+                                                nat.ptr(ws), ws.numel(), nat.stream_handle()),
+                  "pmg_joint_accumulate")
+        return S
+
+
+def log_of(x: torch.Tensor) -> torch.Tensor:
+    """Elementwise log on the device (pmg_log); log(0) = -inf."""
+    out = torch.empty_like(x)
+    nat.check(nat.load().pmg_log(nat.ptr(x), x.numel(), nat.ptr(out), nat.stream_handle()), "pmg_log")
+    return out
