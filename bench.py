@@ -1,0 +1,220 @@
+"""Benchmark: EM iterations/s of PoissonGPLVMJump1D.fit_em at BASELINE config C3
+(N=512 neurons, T=1e5 time bins, L=512 latent bins; tuning_lengthscale=10 -> 79
+basis columns; movement_variance=1, p_move_to_jump=p_jump_to_move=0.01; Adam lr 0.01,
+maxiter 1000, tol 1e-6) on synthetic spikes drawn from the model itself.
+
+One "step" = one full EM iteration on the device: sufficient statistics + Adam M-step
++ tuning + emission + forward filter + backward smoother (core.py:650-676).
+
+N GPUs (one process per GPU, torchrun): every rank runs an independent EM restart
+(model_selection_helper.py:53-59: restarts differ only in the posterior init) on the
+same data -- no data-path collective, weak scaling; value = restarts x iterations / max
+wall time over ranks.
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (N, T, L)
+    "c1": (30, 1000, 100),
+    "c2": (128, 10000, 256),
+    "c3": (512, 100000, 512),
+    "c5": (256, 50000, 256),
+}
+PEAK_HBM_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
+PEAK_FP32_MFMA_TFLOPS = 157.3    # dense FP32 matrix (spec)
+PEAK_I8_MFMA_TOPS = 5000.0       # dense int8 MFMA (= fp8 rate, spec)
+
+
+def synth(N, T, L, ls=10.0, seed=0, rank=0):
+    """Synthetic workload (BASELINE.md section 2 seeds) with a vectorised sampler."""
+    from poor_man_gplvm_amd.gp_kernel import generate_basis, create_transition_prob_1d
+    B = generate_basis(ls, L)
+    W = np.random.default_rng(seed).normal(size=(B.shape[1], N))
+    F = B.astype(np.float64) @ W
+    tun = np.logaddexp(F, 0.0)
+    K, _, A, _ = create_transition_prob_1d(L, 1.0, 0.01, 0.01)
+    rng = np.random.default_rng(seed + 1)
+    lat = np.empty(T, np.int64)
+    d, l = 0, L // 2
+    cK = np.cumsum(K, axis=2)
+    u = rng.random((T, 2))
+    for t in range(T):
+        d = 1 if u[t, 0] < A[d, 1] else 0
+        l = int(min(np.searchsorted(cK[d, l], u[t, 1] * cK[d, l, -1], side="right"), L - 1))
+        lat[t] = l
+    y = np.random.default_rng(seed + 2).poisson(tun[lat]).astype(np.float32)
+    uu = np.random.default_rng(seed + 3 + rank).random((T, L)) * 0.1
+    p = uu / uu.sum(1, keepdims=True)
+    lp0 = np.log(p).astype(np.float32)
+    W0 = np.random.default_rng(123).normal(size=W.shape).astype(np.float32)
+    return y, B, W0, lp0
+
+
+def cpu_baseline(N, T, L, adam_iters, t_sample=128, adam_sample=10):
+    """Time the float64 CPU oracle (the reference algorithm: dense log-domain filter,
+    smoother, emission, suff-stats, Adam) on a bounded sample of the same workload
+    and scale to one full EM iteration.  Single-threaded numpy (cores=1)."""
+    try:
+        from threadpoolctl import threadpool_limits
+        lim = threadpool_limits(1)
+    except Exception:
+        lim = None
+    from oracle import gplvm_oracle as O
+    y, B, W0, lp0 = synth(N, t_sample + 1, L)
+    B64 = B.astype(np.float64)
+    _, logK, _, logA = O.create_transition_prob_1d(L, 1.0)
+    tun = O.get_tuning_softplus(W0, B64)
+    t0 = time.perf_counter()
+    O.smooth_all_step_combined_ma_chunk(y.astype(np.float64), tun, logK, logA, with_joint=True)
+    t_e = (time.perf_counter() - t0) / (t_sample + 1)          # s per time step (E-step incl. emission)
+    t0 = time.perf_counter()
+    yw, tw = O.get_statistics(lp0.astype(np.float64), y)
+    t_ss = (time.perf_counter() - t0) / (t_sample + 1)         # s per time step (suff-stats)
+    yw = yw * (T / (t_sample + 1))
+    tw = tw * (T / (t_sample + 1))
+    t0 = time.perf_counter()
+    O.adam_run(W0.astype(np.float64), O.adam_init(W0), 1.0, B64, yw, tw, maxiter=adam_sample + 1, tol=0.0)
+    t_adam = (time.perf_counter() - t0) / adam_sample           # s per Adam iteration
+    total = T * (t_e + t_ss) + adam_iters * t_adam
+    if lim is not None:
+        lim.unregister() if hasattr(lim, "unregister") else None
+    return {"value": 1.0 / total, "unit": "EM iters/s", "cores": 1, "kind": "port",
+            "sample": (f"float64 numpy oracle (reference algorithm, joint accumulated as in decoder.py:221) "
+                       f"timed on {t_sample + 1} time steps x (N={N}, L={L}) for the E-step and suff-stats "
+                       f"and {adam_sample} Adam iterations; scaled to T={T} and {adam_iters:.0f} Adam "
+                       f"iterations (the GPU run's mean): {total:.1f} s per EM iteration")}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--chunk", type=int, default=0)
+    ap.add_argument("--warm-steps", type=int, default=48)
+    ap.add_argument("--verbose", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from poor_man_gplvm_amd.engine import SpikeData, DeviceEM, AdamConfig, ScanConfig, KernelTimer
+    from poor_man_gplvm_amd.gp_kernel import banded_transition
+
+    N, T, L = CONFIGS[args.config]
+    y, B, W0, lp0 = synth(N, T, L, rank=rank)
+    dev = torch.device("cuda", local)
+    scan = ScanConfig(chunk=args.chunk or None, warmup=args.warm_steps)
+    sp = SpikeData(y)
+    eng = DeviceEM(sp, L, basis=B, scan=scan)
+    eng.set_transition(banded_transition(L, 1.0, 0.01, 0.01))
+    eng.set_log_posterior(lp0)
+    adam = AdamConfig(lr=0.01, maxiter=1000, tol=1e-6, prior_std=1.0)
+    W = torch.as_tensor(W0.astype(np.float64), device=dev).contiguous()
+    mu, nu = torch.zeros_like(W), torch.zeros_like(W)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    n_all = args.warmup + args.steps
+    stats = torch.zeros((n_all, 4), dtype=torch.float64, device=dev)
+    lh = torch.zeros((n_all, adam.maxiter), dtype=torch.float64, device=dev)
+    eh = torch.zeros_like(lh)
+    logz = torch.zeros(n_all, dtype=torch.float64, device=dev)
+
+    def em_iter(i):
+        eng.m_step(W, mu, nu, cnt, adam, stats[i], lh[i], eh[i])
+        eng.compute_tuning(W)
+        eng.e_step(1.0, logz[i:i + 1])
+
+    for i in range(args.warmup):
+        em_iter(i)
+    torch.cuda.synchronize()
+    timer = KernelTimer()
+    eng.timer = timer
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.warmup, n_all):
+        em_iter(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        te = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        elapsed = float(te.item())
+    summ = timer.summary()
+    s = stats.cpu().numpy()
+    adam_iters = float(np.mean(s[args.warmup:, 0])) if args.steps else 0.0
+    repairs = eng.repairs()
+
+    # roofline of the dominant kernel (largest mean time per EM iteration)
+    Lc = L
+    nblk = (L + 31) // 32
+    bytes_fwd = T * Lc * 4 + T * nblk * 4 + T * 8 + T * 2 * Lc * 4 + T * 8
+    bytes_bwd = T * Lc * 4 + T * nblk * 4 + T * 2 * Lc * 4 + T * Lc * 4
+    flops_ss = 2.0 * T * L * (N + 1)
+    ops_em = 2.0 * T * L * N
+    roof = {
+        "forward_filter": ("hbm", bytes_fwd / 1e9, PEAK_HBM_GBS, "GB/s"),
+        "backward_smoother": ("hbm", bytes_bwd / 1e9, PEAK_HBM_GBS, "GB/s"),
+        "suffstats": ("mfma", flops_ss / 1e12, PEAK_FP32_MFMA_TFLOPS, "TFLOP/s"),
+        "emission": ("mfma", ops_em / 1e12, PEAK_I8_MFMA_TOPS, "TFLOP/s"),
+    }
+    dom = max((k for k in summ if k in roof), key=lambda k: summ[k][1])
+    bound, units_per_launch, peak, unit = roof[dom]
+    achieved = units_per_launch / (summ[dom][1] / 1e3)
+    value = world * args.steps / elapsed
+    out = {
+        "metric": "EM iters/sec at N=512, T=1e5, B=512; fwd-bwd achieved HBM GB/s",
+        "value": value,
+        "unit": "EM iters/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 state / int8-exact emission / f64 stats",
+        "data": "synthetic (spikes sampled from the model; seeds of BASELINE.md section 2)",
+        "config": {"workload": f"{args.config}: PoissonGPLVMJump1D.fit_em N={N} T={T} L={L} "
+                               f"nb={B.shape[1]} (one EM iteration per step; ranks = independent restarts)",
+                   "n_neuron": N, "n_time": T, "n_latent_bin": L, "parallelism": f"restarts x{world}"},
+        "roofline": {"kernel": dom, "bound": bound, "achieved": achieved, "peak": peak, "unit": unit,
+                     "frac": achieved / peak, "traffic": None},
+        "kernels_ms": {k: round(v[1], 4) for k, v in summ.items()},
+        "fwd_bwd_GBps": (bytes_fwd + bytes_bwd) / 1e9 / ((summ["forward_filter"][1] + summ["backward_smoother"][1]) / 1e3),
+        "adam_iters_mean": adam_iters,
+        "chunk": eng.C,
+        "repairs_last": repairs,
+    }
+    if rank == 0 and not args.no_cpu_baseline and world == 1:
+        out["cpu_baseline"] = cpu_baseline(N, T, L, adam_iters)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

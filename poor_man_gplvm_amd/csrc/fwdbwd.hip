@@ -25,11 +25,14 @@
 //     the backward pass needs only alpha_t and the emission -- no stored priors.
 //
 // Emission input: e[t,l] = exp(s*delta[t,l] + phi[t,l/32]) = exp(s*(ll[t,l] - m[t])).
+#include <stdlib.h>
+
 #include "pmg_common.h"
 
 namespace pmg {
 
 constexpr int kMaxBand = 32;
+constexpr int kFixRounds = 2;  // parallel repair rounds before the sequential fallback
 
 struct FBParams {
   const float* delta;
@@ -58,7 +61,6 @@ struct FBParams {
   float* gamma;
   float* rho;
   float* b_in;
-  float* b_out;
   float* b_first;
   int* flags;
   int* repairs;
@@ -280,7 +282,8 @@ struct Fwd {
   }
 };
 
-// run chunk c forward from t0 (state already initialised) to t_e; writes outputs for t >= t_c
+// run forward from t0 (state initialised) to t_e; writes outputs for t >= t_c and the
+// state at t_c-1 into s_in_dst (if given)
 template <int J, int WP>
 __device__ double fwd_run(const FBParams& p, Fwd<J, WP>& st, float* lds, int j0, const float invz[J],
                           int64_t t0, int64_t t_c, int64_t t_e, float* s_in_dst) {
@@ -308,43 +311,58 @@ __device__ double fwd_run(const FBParams& p, Fwd<J, WP>& st, float* lds, int j0,
   return logz;
 }
 
+#define PMG_FB_PROLOGUE                                                 \
+  __shared__ __attribute__((aligned(16))) float lds[64 * J + 2 * WP];  \
+  const int lane = threadIdx.x & 63;                                    \
+  const int j0 = lane * J;                                              \
+  for (int k = lane; k < 64 * J + 2 * WP; k += 64) lds[k] = 0.f;        \
+  __syncthreads();                                                      \
+  float invz[J];                                                        \
+  _Pragma("unroll") for (int j = 0; j < J; ++j) invz[j] = (j0 + j < p.L) ? p.invz[j0 + j] : 0.f; \
+  const size_t SZ = (size_t)2 * p.Lpad;                                 \
+  (void)SZ;
+
+// speculative pass: chunk c starts `B` steps early from a uniform guess
 template <int J, int WP>
 __global__ void __launch_bounds__(64) k_forward(FBParams p) {
-  __shared__ __attribute__((aligned(16))) float lds[64 * J + 2 * WP];
-  const int lane = threadIdx.x;
-  const int j0 = lane * J;
-  for (int k = lane; k < 64 * J + 2 * WP; k += 64) lds[k] = 0.f;
-  __syncthreads();
   const int c = blockIdx.x;
   if (c >= p.M) return;
-  float invz[J];
-#pragma unroll
-  for (int j = 0; j < J; ++j) invz[j] = (j0 + j < p.L) ? p.invz[j0 + j] : 0.f;
+  PMG_FB_PROLOGUE
   const int64_t t_c = (int64_t)c * p.C;
   const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
   int64_t t0 = (c == 0) ? 0 : t_c - p.B;
   if (t0 < 0) t0 = 0;
   Fwd<J, WP> st;
   st.init_uniform(p, j0);
-  float* sin = p.s_in + (size_t)c * 2 * p.Lpad;
+  float* sin = p.s_in + (size_t)c * SZ;
   if (c > 0 && t0 == t_c) st.save_state(p, sin, j0);  // no warm-up: the guess itself
   const double lz = fwd_run<J, WP>(p, st, lds, j0, invz, t0, t_c, t_e, c > 0 ? sin : nullptr);
-  st.save_state(p, p.s_out + (size_t)c * 2 * p.Lpad, j0);
+  st.save_state(p, p.s_out + (size_t)c * SZ, j0);
   if (lane == 0) p.chunk_logz[c] = lz;
 }
 
-// single-wave sequential repair of chunks whose start state failed verification
+// parallel repair round: every flagged chunk restarts from its snapshot s_in[c]
+template <int J, int WP>
+__global__ void __launch_bounds__(64) k_forward_fix(FBParams p) {
+  const int c = blockIdx.x;
+  if (c >= p.M || c == 0 || p.flags[c] == 0) return;
+  PMG_FB_PROLOGUE
+  const int64_t t_c = (int64_t)c * p.C;
+  const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
+  Fwd<J, WP> st;
+  st.load_state(p, p.s_in + (size_t)c * SZ, j0);
+  const double lz = fwd_run<J, WP>(p, st, lds, j0, invz, t_c, t_c, t_e, nullptr);
+  st.save_state(p, p.s_out + (size_t)c * SZ, j0);
+  if (lane == 0) {
+    p.chunk_logz[c] = lz;
+    atomicAdd(&p.repairs[0], 1);
+  }
+}
+
+// sequential fallback for whatever is still flagged after the parallel rounds
 template <int J, int WP>
 __global__ void __launch_bounds__(64) k_forward_repair(FBParams p) {
-  __shared__ __attribute__((aligned(16))) float lds[64 * J + 2 * WP];
-  const int lane = threadIdx.x;
-  const int j0 = lane * J;
-  for (int k = lane; k < 64 * J + 2 * WP; k += 64) lds[k] = 0.f;
-  __syncthreads();
-  float invz[J];
-#pragma unroll
-  for (int j = 0; j < J; ++j) invz[j] = (j0 + j < p.L) ? p.invz[j0 + j] : 0.f;
-  const size_t SZ = (size_t)2 * p.Lpad;
+  PMG_FB_PROLOGUE
   int repairs = 0;
   bool changed = false;
   int c = 1;
@@ -360,9 +378,8 @@ __global__ void __launch_bounds__(64) k_forward_repair(FBParams p) {
       }
       if (found < 0) break;
       c = found;
-      st.load_state(p, p.s_out + (size_t)(c - 1) * SZ, j0);  // written by k_forward
+      st.load_state(p, p.s_out + (size_t)(c - 1) * SZ, j0);
     }
-    // else: st already holds the repaired end state of chunk c-1
     const int64_t t_c = (int64_t)c * p.C;
     const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
     st.save_state(p, p.s_in + (size_t)c * SZ, j0);
@@ -376,19 +393,24 @@ __global__ void __launch_bounds__(64) k_forward_repair(FBParams p) {
     ++repairs;
     ++c;
   }
-  if (lane == 0) p.repairs[0] = repairs;
+  if (lane == 0) p.repairs[0] += repairs;
 }
 
-// boundary verification: flags[c] = hilbert(x[c], y[c + off]) > tol
-__global__ void __launch_bounds__(256) k_verify(const float* __restrict__ x, const float* __restrict__ y,
+// boundary verification: flags[c] = hilbert(x[c], y[c + off]) > tol; a failing
+// boundary also snapshots y[c + off] into x[c] (the restart state of the repair)
+__global__ void __launch_bounds__(256) k_verify(float* __restrict__ x, const float* __restrict__ y,
                                                 int first, int last, int off, int SZ, float tol,
-                                                int* __restrict__ flags, int M) {
+                                                int* __restrict__ flags) {
   const int w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int c = first + w;
   if (c > last) return;
-  const float d = hilbert_dist(x + (size_t)c * SZ, y + (size_t)(c + off) * SZ, SZ);
-  if ((threadIdx.x & 63) == 0) flags[c] = (d <= tol) ? 0 : 1;
-  (void)M;
+  const float* yc = y + (size_t)(c + off) * SZ;
+  float* xc = x + (size_t)c * SZ;
+  const float d = hilbert_dist(xc, yc, SZ);
+  const bool bad = !(d <= tol);
+  if ((threadIdx.x & 63) == 0) flags[c] = bad ? 1 : 0;
+  if (bad)
+    for (int i = threadIdx.x & 63; i < SZ; i += 64) xc[i] = yc[i];
 }
 
 __global__ void k_sum_f64(const double* __restrict__ x, int n, double* __restrict__ out) {
@@ -405,7 +427,10 @@ __global__ void k_sum_f64(const double* __restrict__ x, int n, double* __restric
 }
 
 // ---------------------------------------------------------------------------
-// backward (beta recursion)
+// backward (beta recursion).  Every step back uses the same arithmetic
+//   v = e_t * beta_t / sum(e_t * beta_t),  beta_{t-1} = Trans(v)
+// on the warm-up and on the output path, so two chunks that have converged to
+// the same beta produce bit-identical continuations (as the forward does).
 // ---------------------------------------------------------------------------
 template <int J, int WP>
 struct Bwd {
@@ -432,12 +457,18 @@ struct Bwd {
       dst[p.Lpad + j0 + j] = b1[j];
     }
   }
-  // beta_{t-1} = Trans (v), v = e_t * beta_t already scaled; V1 = sum v1
-  __device__ void transition_back(const FBParams& p, float* lds, int j0, const float invz[J],
-                                  const float v0[J], float V1) {
+  // v = e*beta scaled by 1/(V0+V1) (returned in v0/v1); beta <- Trans(v)
+  __device__ void step_back(const FBParams& p, float* lds, int j0, const float invz[J],
+                            const float e[J], float V0, float V1, float v0[J], float v1[J]) {
+    const float sc = 1.f / (V0 + V1);
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      v0[j] = e[j] * b0[j] * sc;
+      v1[j] = e[j] * b1[j] * sc;
+    }
     float w0[J];
     band_conv<J, WP>(p, lds, j0, v0, w0);
-    const float w1 = V1 * p.invL;
+    const float w1 = V1 * sc * p.invL;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const float c0 = w0[j] * invz[j];
@@ -448,37 +479,30 @@ struct Bwd {
   }
 };
 
-// warm-up / plain backward steps from time t_hi down to t_lo (beta ends at t_lo)
+// one plain backward step at time t (beta_t -> beta_{t-1}); v kept in (v0, v1)
 template <int J, int WP>
-__device__ void bwd_warm(const FBParams& p, Bwd<J, WP>& st, float* lds, int j0, const float invz[J],
-                         int64_t t_hi, int64_t t_lo) {
-  for (int64_t t = t_hi; t > t_lo; --t) {
-    EmRaw<J> r;
-    em_load<J>(p, t, j0, r);
-    float e[J];
-    em_exp<J>(p, j0, r, e);
-    float v0[J], v1[J];
-    float VS = 0.f, V1 = 0.f;
+__device__ __forceinline__ void bwd_plain(const FBParams& p, Bwd<J, WP>& st, float* lds, int j0,
+                                          const float invz[J], int64_t t, float v0[J], float v1[J]) {
+  EmRaw<J> r;
+  em_load<J>(p, t, j0, r);
+  float e[J];
+  em_exp<J>(p, j0, r, e);
+  float V0 = 0.f, V1 = 0.f;
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
-      v0[j] = e[j] * st.b0[j];
-      v1[j] = e[j] * st.b1[j];
-      VS += v0[j] + v1[j];
-      V1 += v1[j];
-    }
-    wave_sum2(VS, V1);
-    const float sc = 1.f / VS;
-#pragma unroll
-    for (int j = 0; j < J; ++j) v0[j] *= sc;
-    st.transition_back(p, lds, j0, invz, v0, V1 * sc);
+  for (int j = 0; j < J; ++j) {
+    V0 += e[j] * st.b0[j];
+    V1 += e[j] * st.b1[j];
   }
+  wave_sum2(V0, V1);
+  st.step_back(p, lds, j0, invz, e, V0, V1, v0, v1);
 }
 
-// output steps t = t_e-1 .. t_c (beta at t_e-1 in st, v_prev = the v that produced it,
-// or has_prev = false at the sequence end).  Leaves beta_{t_c-1} in st if t_c > 0.
+// output steps t = t_e-1 .. t_c.  On entry st holds beta_{t_e-1} and (vp0, vp1) the v that
+// produced it (has_prev false at the sequence end).  Writes beta_{t_c} to bf (registers).
 template <int J, int WP>
 __device__ void bwd_out(const FBParams& p, Bwd<J, WP>& st, float* lds, int j0, const float invz[J],
-                        int64_t t_c, int64_t t_e, float vprev0[J], float vprev1[J], bool has_prev) {
+                        int64_t t_c, int64_t t_e, float vp0[J], float vp1[J], bool has_prev,
+                        float bf0[J], float bf1[J]) {
   const int64_t L = p.L;
   for (int64_t t = t_e - 1; t >= t_c; --t) {
     EmRaw<J> r;
@@ -489,15 +513,17 @@ __device__ void bwd_out(const FBParams& p, Bwd<J, WP>& st, float* lds, int j0, c
     load_row<J>(arow + L, p.L, j0, a1);
     float e[J];
     em_exp<J>(p, j0, r, e);
-    float G = 0.f, V1 = 0.f;
+    float G = 0.f, V0 = 0.f, V1 = 0.f;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       a0[j] *= st.b0[j];
       a1[j] *= st.b1[j];
       G += a0[j] + a1[j];
+      V0 += e[j] * st.b0[j];
       V1 += e[j] * st.b1[j];
     }
-    wave_sum2(G, V1);
+    wave_sum2(V0, V1);
+    G = wave_sum(G);
     const float iG = 1.f / G;
     float pp[J];
 #pragma unroll
@@ -506,83 +532,41 @@ __device__ void bwd_out(const FBParams& p, Bwd<J, WP>& st, float* lds, int j0, c
       a1[j] *= iG;
       pp[j] = a0[j] + a1[j];
     }
-    if (t == t_c && p.b_first) {
-      float* bf = p.b_first + (size_t)(t_c / p.C) * 2 * p.Lpad;
-#pragma unroll
-      for (int j = 0; j < J; ++j) {
-        bf[j0 + j] = st.b0[j];
-        bf[p.Lpad + j0 + j] = st.b1[j];
-      }
-    }
     if (p.P) store_row<J>(p.P + t * L, p.L, j0, pp);
     if (p.gamma) {
       store_row<J>(p.gamma + t * 2 * L, p.L, j0, a0);
       store_row<J>(p.gamma + t * 2 * L + L, p.L, j0, a1);
     }
-    if (p.rho && has_prev && t + 1 < p.T) {
+    if (p.rho && has_prev && t + 1 < p.T) {  // rho_{t+1} = v_{t+1} / sum(alpha_t * beta_t)
       float r0[J], r1[J];
 #pragma unroll
       for (int j = 0; j < J; ++j) {
-        r0[j] = vprev0[j] * iG;
-        r1[j] = vprev1[j] * iG;
+        r0[j] = vp0[j] * iG;
+        r1[j] = vp1[j] * iG;
       }
       store_row<J>(p.rho + (t + 1) * 2 * L, p.L, j0, r0);
       store_row<J>(p.rho + (t + 1) * 2 * L + L, p.L, j0, r1);
     }
-    if (t == 0) break;
-    // beta scaled so that sum alpha*beta = 1, then step back
+    if (t == t_c) {
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
-      vprev0[j] = e[j] * st.b0[j] * iG;
-      vprev1[j] = e[j] * st.b1[j] * iG;
+      for (int j = 0; j < J; ++j) {
+        bf0[j] = st.b0[j];
+        bf1[j] = st.b1[j];
+      }
+      break;
     }
+    st.step_back(p, lds, j0, invz, e, V0, V1, vp0, vp1);
     has_prev = true;
-    st.transition_back(p, lds, j0, invz, vprev0, V1 * iG);
   }
-}
-
-// From beta_{t+1} (in st) and the emission at t+1, form v = e*beta (scaled to sum 1),
-// keep it in (vp0, vp1) and step st back to beta_t.
-template <int J, int WP>
-__device__ void bwd_boundary(const FBParams& p, Bwd<J, WP>& st, float* lds, int j0,
-                             const float invz[J], int64_t tnext, float vp0[J], float vp1[J]) {
-  EmRaw<J> r;
-  em_load<J>(p, tnext, j0, r);
-  float e[J];
-  em_exp<J>(p, j0, r, e);
-  float VS = 0.f, V1 = 0.f;
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    vp0[j] = e[j] * st.b0[j];
-    vp1[j] = e[j] * st.b1[j];
-    VS += vp0[j] + vp1[j];
-    V1 += vp1[j];
-  }
-  wave_sum2(VS, V1);
-  const float sc = 1.f / VS;
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    vp0[j] *= sc;
-    vp1[j] *= sc;
-  }
-  st.transition_back(p, lds, j0, invz, vp0, V1 * sc);
 }
 
 template <int J, int WP>
 __global__ void __launch_bounds__(64) k_backward(FBParams p) {
-  __shared__ __attribute__((aligned(16))) float lds[64 * J + 2 * WP];
-  const int lane = threadIdx.x;
-  const int j0 = lane * J;
-  for (int k = lane; k < 64 * J + 2 * WP; k += 64) lds[k] = 0.f;
-  __syncthreads();
   const int c = blockIdx.x;
   if (c >= p.M) return;
-  float invz[J];
-#pragma unroll
-  for (int j = 0; j < J; ++j) invz[j] = (j0 + j < p.L) ? p.invz[j0 + j] : 0.f;
+  PMG_FB_PROLOGUE
   const int64_t t_c = (int64_t)c * p.C;
   const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
-  const size_t SZ = (size_t)2 * p.Lpad;
   Bwd<J, WP> st;
   st.init_ones(p, j0);
   float vp0[J], vp1[J];
@@ -592,26 +576,48 @@ __global__ void __launch_bounds__(64) k_backward(FBParams p) {
   if (c < p.M - 1) {
     int64_t t_w = t_e + p.B;  // beta guess (ones) at t_w, exact when t_w is the last bin
     if (t_w > p.T - 1) t_w = p.T - 1;
-    bwd_warm<J, WP>(p, st, lds, j0, invz, t_w, t_e);          // -> beta_{t_e}
-    bwd_boundary<J, WP>(p, st, lds, j0, invz, t_e, vp0, vp1);  // -> beta_{t_e - 1}
+    for (int64_t t = t_w; t > t_e; --t) bwd_plain<J, WP>(p, st, lds, j0, invz, t, vp0, vp1);
+    st.save_state(p, p.b_in + (size_t)c * SZ, j0);                 // beta_{t_e}
+    bwd_plain<J, WP>(p, st, lds, j0, invz, t_e, vp0, vp1);          // -> beta_{t_e-1}
     has_prev = true;
-    st.save_state(p, p.b_in + (size_t)c * SZ, j0);
   }
-  bwd_out<J, WP>(p, st, lds, j0, invz, t_c, t_e, vp0, vp1, has_prev);
-  if (c > 0) st.save_state(p, p.b_out + (size_t)c * SZ, j0);
+  float bf0[J], bf1[J];
+  bwd_out<J, WP>(p, st, lds, j0, invz, t_c, t_e, vp0, vp1, has_prev, bf0, bf1);
+  float* bf = p.b_first + (size_t)c * SZ;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    bf[j0 + j] = bf0[j];
+    bf[p.Lpad + j0 + j] = bf1[j];
+  }
 }
 
+// parallel repair round: flagged chunk c restarts from its snapshot b_in[c] = beta_{t_e}
+template <int J, int WP>
+__global__ void __launch_bounds__(64) k_backward_fix(FBParams p) {
+  const int c = blockIdx.x;
+  if (c >= p.M - 1 || p.flags[c] == 0) return;
+  PMG_FB_PROLOGUE
+  const int64_t t_c = (int64_t)c * p.C;
+  const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
+  Bwd<J, WP> st;
+  st.load_state(p, p.b_in + (size_t)c * SZ, j0);
+  float vp0[J], vp1[J];
+  bwd_plain<J, WP>(p, st, lds, j0, invz, t_e, vp0, vp1);
+  float bf0[J], bf1[J];
+  bwd_out<J, WP>(p, st, lds, j0, invz, t_c, t_e, vp0, vp1, true, bf0, bf1);
+  float* bf = p.b_first + (size_t)c * SZ;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    bf[j0 + j] = bf0[j];
+    bf[p.Lpad + j0 + j] = bf1[j];
+  }
+  if (lane == 0) atomicAdd(&p.repairs[1], 1);
+}
+
+// sequential fallback (descending chunks)
 template <int J, int WP>
 __global__ void __launch_bounds__(64) k_backward_repair(FBParams p) {
-  __shared__ __attribute__((aligned(16))) float lds[64 * J + 2 * WP];
-  const int lane = threadIdx.x;
-  const int j0 = lane * J;
-  for (int k = lane; k < 64 * J + 2 * WP; k += 64) lds[k] = 0.f;
-  __syncthreads();
-  float invz[J];
-#pragma unroll
-  for (int j = 0; j < J; ++j) invz[j] = (j0 + j < p.L) ? p.invz[j0 + j] : 0.f;
-  const size_t SZ = (size_t)2 * p.Lpad;
+  PMG_FB_PROLOGUE
   int repairs = 0;
   bool changed = false;
   int c = p.M - 2;
@@ -629,38 +635,41 @@ __global__ void __launch_bounds__(64) k_backward_repair(FBParams p) {
     }
     const int64_t t_c = (int64_t)c * p.C;
     const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
-    // restart from the successor's first smoothed beta (beta_{t_e}, b_first[c+1])
     Bwd<J, WP> st;
     st.load_state(p, p.b_first + (size_t)(c + 1) * SZ, j0);
-    float vp0[J], vp1[J];
-    bwd_boundary<J, WP>(p, st, lds, j0, invz, t_e, vp0, vp1);
     st.save_state(p, p.b_in + (size_t)c * SZ, j0);
-    bwd_out<J, WP>(p, st, lds, j0, invz, t_c, t_e, vp0, vp1, true);
-    if (c > 0) {
-      const float d = hilbert_reg<J>(st.b0, st.b1, p.b_out + (size_t)c * SZ, p.Lpad, j0);
-      changed = !(d <= p.tol);
-      st.save_state(p, p.b_out + (size_t)c * SZ, j0);
-    } else {
-      changed = false;
+    float vp0[J], vp1[J];
+    bwd_plain<J, WP>(p, st, lds, j0, invz, t_e, vp0, vp1);
+    float bf0[J], bf1[J];
+    bwd_out<J, WP>(p, st, lds, j0, invz, t_c, t_e, vp0, vp1, true, bf0, bf1);
+    float* bf = p.b_first + (size_t)c * SZ;
+    const float d = hilbert_reg<J>(bf0, bf1, bf, p.Lpad, j0);
+    changed = !(d <= p.tol);
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      bf[j0 + j] = bf0[j];
+      bf[p.Lpad + j0 + j] = bf1[j];
     }
     __threadfence();
     ++repairs;
     --c;
   }
-  if (lane == 0) p.repairs[1] = repairs;
+  if (lane == 0) p.repairs[1] += repairs;
 }
 
 // ---------------------------------------------------------------------------
 // host dispatch
 // ---------------------------------------------------------------------------
 struct FBWork {
-  float *s_in, *s_out, *b_in, *b_out, *b_first;
+  float *s_in, *s_out, *b_in, *b_first;
   double* chunk_logz;
   int* flags;
   int* repairs;
 };
 
-static FBWork carve_fb(void* ws, int64_t T, int Lpad, int C) {
+// workspace layout (the Python diagnostics mirror it): repairs[64] | s_in | s_out |
+// b_in | b_first (M x 2 x Lpad f32 each) | chunk_logz[M] | flags[M]
+static FBWork carve_fb(void* ws, int64_t T, int Lpad, int C, size_t* total = nullptr) {
   const int64_t M = (T + C - 1) / C;
   Carver c(ws);
   FBWork w;
@@ -668,11 +677,10 @@ static FBWork carve_fb(void* ws, int64_t T, int Lpad, int C) {
   w.s_in = c.take<float>((size_t)M * 2 * Lpad);
   w.s_out = c.take<float>((size_t)M * 2 * Lpad);
   w.b_in = c.take<float>((size_t)M * 2 * Lpad);
-  w.b_out = c.take<float>((size_t)M * 2 * Lpad);
   w.b_first = c.take<float>((size_t)M * 2 * Lpad);
   w.chunk_logz = c.take<double>(M);
   w.flags = c.take<int>(M);
-  (void)w;
+  if (total) *total = c.off + 256;
   return w;
 }
 
@@ -720,6 +728,8 @@ typedef void (*fb_kernel_t)(FBParams);
 
 PMG_FB_TABLE(k_forward)
 PMG_FB_TABLE(k_forward_repair)
+PMG_FB_TABLE(k_forward_fix)
+PMG_FB_TABLE(k_backward_fix)
 PMG_FB_TABLE(k_backward)
 PMG_FB_TABLE(k_backward_repair)
 
@@ -761,20 +771,10 @@ extern "C" {
 
 size_t pmg_fwdbwd_workspace_size(int64_t T, int32_t L, int32_t chunk) {
   const int J = pick_J(L);
-  if (J < 0 || chunk <= 0) return 0;
-  Carver c(nullptr);
-  FBWork w = carve_fb(nullptr, T, 64 * J, chunk);
-  (void)w;
-  const int64_t M = (T + chunk - 1) / chunk;
-  c.take<int>(64);
-  c.take<float>((size_t)M * 2 * 64 * J);
-  c.take<float>((size_t)M * 2 * 64 * J);
-  c.take<float>((size_t)M * 2 * 64 * J);
-  c.take<float>((size_t)M * 2 * 64 * J);
-  c.take<float>((size_t)M * 2 * 64 * J);
-  c.take<double>(M);
-  c.take<int>(M);
-  return c.off + 256;
+  if (J < 0 || chunk <= 0 || T <= 0) return 0;
+  size_t total = 0;
+  carve_fb(nullptr, T, 64 * J, chunk, &total);
+  return total;
 }
 
 size_t pmg_fwdbwd_repair_counter_offset(int64_t T, int32_t L, int32_t chunk) {
@@ -805,19 +805,27 @@ int pmg_forward_filter(const float* delta, const float* phi, const double* m, in
   p.flags = w.flags;
   p.repairs = w.repairs;
   const int J = p.Lpad / 64, WP = pick_WP(tr->band);
-  fb_kernel_t kf = k_forward_table(J, WP), kr = k_forward_repair_table(J, WP);
-  PMG_REQUIRE(kf && kr, "pmg_forward_filter: no kernel for J=%d WP=%d", J, WP);
-  PMG_HIP(hipMemsetAsync(w.repairs, 0, 2 * sizeof(int), st));
+  fb_kernel_t kf = k_forward_table(J, WP), kfix = k_forward_fix_table(J, WP),
+              kr = k_forward_repair_table(J, WP);
+  PMG_REQUIRE(kf && kfix && kr, "pmg_forward_filter: no kernel for J=%d WP=%d", J, WP);
+  PMG_HIP(hipMemsetAsync(w.repairs, 0, sizeof(int), st));
   hipLaunchKernelGGL(kf, dim3(p.M), dim3(64), 0, st, p);
   PMG_LAUNCH_CHECK();
   if (p.M > 1) {
-    PMG_HIP(hipMemsetAsync(w.flags, 0, sizeof(int) * p.M, st));
     const int nver = p.M - 1;
-    hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4), dim3(256), 0, st, (const float*)w.s_in,
-                       (const float*)w.s_out, 1, p.M - 1, -1, 2 * p.Lpad, p.tol, w.flags, p.M);
-    PMG_LAUNCH_CHECK();
-    hipLaunchKernelGGL(kr, dim3(1), dim3(64), 0, st, p);
-    PMG_LAUNCH_CHECK();
+    const bool no_repair = getenv("PMG_DEBUG_NO_REPAIR") != nullptr;
+    for (int round = 0; round <= kFixRounds; ++round) {
+      hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4), dim3(256), 0, st, w.s_in,
+                         (const float*)w.s_out, 1, p.M - 1, -1, 2 * p.Lpad, p.tol, w.flags);
+      PMG_LAUNCH_CHECK();
+      if (no_repair) break;
+      if (round < kFixRounds) {
+        hipLaunchKernelGGL(kfix, dim3(p.M), dim3(64), 0, st, p);
+      } else {
+        hipLaunchKernelGGL(kr, dim3(1), dim3(64), 0, st, p);
+      }
+      PMG_LAUNCH_CHECK();
+    }
   }
   hipLaunchKernelGGL(k_sum_f64, dim3(1), dim3(256), 0, st, (const double*)w.chunk_logz, p.M, logz);
   PMG_LAUNCH_CHECK();
@@ -843,23 +851,31 @@ int pmg_backward_smoother(const float* delta, const float* phi, const float* alp
   p.gamma = gamma;
   p.rho = rho;
   p.b_in = w.b_in;
-  p.b_out = w.b_out;
   p.b_first = w.b_first;
   p.flags = w.flags;
   p.repairs = w.repairs;
   const int J = p.Lpad / 64, WP = pick_WP(tr->band);
-  fb_kernel_t kb = k_backward_table(J, WP), kr = k_backward_repair_table(J, WP);
-  PMG_REQUIRE(kb && kr, "pmg_backward_smoother: no kernel for J=%d WP=%d", J, WP);
+  fb_kernel_t kb = k_backward_table(J, WP), kfix = k_backward_fix_table(J, WP),
+              kr = k_backward_repair_table(J, WP);
+  PMG_REQUIRE(kb && kfix && kr, "pmg_backward_smoother: no kernel for J=%d WP=%d", J, WP);
+  PMG_HIP(hipMemsetAsync(w.repairs + 1, 0, sizeof(int), st));
   hipLaunchKernelGGL(kb, dim3(p.M), dim3(64), 0, st, p);
   PMG_LAUNCH_CHECK();
   if (p.M > 1) {
-    PMG_HIP(hipMemsetAsync(w.flags, 0, sizeof(int) * p.M, st));
     const int nver = p.M - 1;
-    hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4), dim3(256), 0, st, (const float*)w.b_in,
-                       (const float*)w.b_out, 0, p.M - 2, 1, 2 * p.Lpad, p.tol, w.flags, p.M);
-    PMG_LAUNCH_CHECK();
-    hipLaunchKernelGGL(kr, dim3(1), dim3(64), 0, st, p);
-    PMG_LAUNCH_CHECK();
+    const bool no_repair = getenv("PMG_DEBUG_NO_REPAIR") != nullptr;
+    for (int round = 0; round <= kFixRounds; ++round) {
+      hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4), dim3(256), 0, st, w.b_in,
+                         (const float*)w.b_first, 0, p.M - 2, 1, 2 * p.Lpad, p.tol, w.flags);
+      PMG_LAUNCH_CHECK();
+      if (no_repair) break;
+      if (round < kFixRounds) {
+        hipLaunchKernelGGL(kfix, dim3(p.M), dim3(64), 0, st, p);
+      } else {
+        hipLaunchKernelGGL(kr, dim3(1), dim3(64), 0, st, p);
+      }
+      PMG_LAUNCH_CHECK();
+    }
   }
   return PMG_OK;
 }

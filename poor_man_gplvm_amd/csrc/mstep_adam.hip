@@ -22,10 +22,16 @@
 
 namespace pmg {
 
-constexpr int kLag = 2;
+// In-loop workgroup barrier that waits only for LDS traffic (lgkmcnt), so the
+// decision pipeline's global loads stay in flight across it (a __syncthreads()
+// would drain vmcnt, cdna_hip_programming.md "Pipelining across barriers").
+#define PMG_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+
+constexpr int kLag = 4;                 // bodies a workgroup runs ahead of the decision
 constexpr int kRing = kLag + 2;
-constexpr int kSMax = 4;        // neurons per workgroup
-constexpr int kThreads = 512;   // L <= 512
+constexpr int kSMax = 4;                // neurons per workgroup
+constexpr int kThreads = 512;           // L <= 512
+constexpr int kPartPerLane = 4;         // G <= 256 workgroups -> 4 partials per lane
 
 struct AdamParams {
   double* W;
@@ -41,30 +47,132 @@ struct AdamParams {
   double* stats;
   double* loss_hist;
   double* err_hist;
-  unsigned* cnt;            // [maxiter]
-  unsigned long long* lpart;  // [maxiter][G] f64 bits
-  unsigned long long* gpart;  // [maxiter][G]
+  unsigned long long* lpart;  // [maxiter + kLag + 2][G] f64 bits, pre-filled with kSentinel
+  unsigned long long* gpart;  // [..][G]
+  double* ring;               // [G][kRing][3][NBM*4] (W, mu, nu) after each body
   int* timeout;
 };
+
+// signalling NaN with a payload: no arithmetic result has this bit pattern
+constexpr unsigned long long kSentinel = 0x7FF4DEADBEEF0001ull;
 
 __device__ __forceinline__ void st_sc1(unsigned long long* p, double v) {
   __hip_atomic_store(p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ double ld_sc1(const unsigned long long* p) {
-  return __longlong_as_double((long long)__hip_atomic_load(const_cast<unsigned long long*>(p),
-                                                           __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT));
+__device__ __forceinline__ unsigned long long ld_bits(const unsigned long long* p) {
+  return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void load_parts(const AdamParams& p, int j, int lane,
+                                           unsigned long long* lv) {
+#pragma unroll
+  for (int q = 0; q < kPartPerLane; ++q) {
+    const int gi = lane + 64 * q;
+    lv[q] = gi < p.G ? ld_bits(&p.lpart[(size_t)j * p.G + gi]) : 0ull;
+  }
 }
 
-template <int NBM, int LGM>
+// the one summation order of a body's partials (decision, histories): lane-strided
+// sums in q order, then the f64 butterfly of wave_sum_f64
+__device__ __forceinline__ double sum_parts(const unsigned long long* lv) {
+  double a = 0.0;
+#pragma unroll
+  for (int q = 0; q < kPartPerLane; ++q) a += __longlong_as_double((long long)lv[q]);
+  return wave_sum_f64(a);
+}
+
+__global__ void k_fill_u64(unsigned long long* __restrict__ x, size_t n, unsigned long long v) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) x[i] = v;
+}
+
+// ---------------------------------------------------------------------------
+// Wave transpose-reduce: 64 per-lane values x[0..63] -> lane l returns
+// sum over the 64 lanes of x[bitrev6(l)].  Six butterfly stages (lane bit 5..0:
+// permlane32_swap, permlane16_swap, DPP row_ror:8, row_half_mirror,
+// quad_perm[2,3,0,1], quad_perm[1,0,3,2]); at every stage the lower half of each
+// lane group keeps the even register of a pair and the upper half the odd one, so
+// each stage halves the registers: ~140 instructions for 64 sums.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float f_of(unsigned u) { return __uint_as_float(u); }
+__device__ __forceinline__ unsigned u_of(float f) { return __float_as_uint(f); }
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_pair_add(float a, float b, bool upper) {
+  // lower lanes: a + partner(a); upper lanes: b + partner(b)
+  const float x = upper ? b : a;
+  const float y = upper ? a : b;
+  return x + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(y), CTRL, 0xf, 0xf, false));
+}
+
+__device__ __forceinline__ int bitrev5(int l) {
+  return ((l & 1) << 4) | ((l & 2) << 2) | (l & 4) | ((l & 8) >> 2) | ((l & 16) >> 4);
+}
+
+// 32 values x_i = a[i/S]*b[i%S] (generated on the fly, pairwise, to keep register
+// pressure at 16 + 2): stages on lane bits 4..0 inside each 32-lane half, then the
+// two halves are added (permlane32_swap of a register with itself).  Lane l returns
+// the 64-lane sum of x[bitrev5(l & 31)].
+template <int SP, int C0, int R>
+__device__ __forceinline__ float wave_products_reduce32(const float* brow, const float* gr) {
+  const int lane = threadIdx.x & 63;
+  float x[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int v0 = C0 + 2 * i, v1 = v0 + 1;
+    const float p0 = (v0 < R) ? brow[v0 / SP] * gr[v0 % SP] : 0.f;
+    const float p1 = (v1 < R) ? brow[v1 / SP] * gr[v1 % SP] : 0.f;
+    auto r = __builtin_amdgcn_permlane16_swap(u_of(p0), u_of(p1), false, false);
+    x[i] = f_of(r[0]) + f_of(r[1]);
+  }
+  const bool b3 = lane & 8, b2 = lane & 4, b1 = lane & 2, b0 = lane & 1;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x[i] = dpp_pair_add<0x128>(x[2 * i], x[2 * i + 1], b3);  // row_ror:8
+#pragma unroll
+  for (int i = 0; i < 4; ++i) x[i] = dpp_pair_add<0x141>(x[2 * i], x[2 * i + 1], b2);  // row_half_mirror
+#pragma unroll
+  for (int i = 0; i < 2; ++i) x[i] = dpp_pair_add<0x4E>(x[2 * i], x[2 * i + 1], b1);   // quad_perm 2,3,0,1
+  const float v = dpp_pair_add<0xB1>(x[0], x[1], b0);                                  // quad_perm 1,0,3,2
+  auto r = __builtin_amdgcn_permlane32_swap(u_of(v), u_of(v), false, false);
+  return f_of(r[0]) + f_of(r[1]);
+}
+
+// products brow[q]*g for q in [C0, R) (one neuron), reduced over the wave, written to
+// sred[(QOFF + q) * 4] (the caller offsets sred by the neuron slot)
+template <int C0, int R, int QOFF>
+struct ChunkLoop {
+  static __device__ __forceinline__ void run(const float* brow, float g, float* sred, int lane) {
+    const float gg[1] = {g};
+    const float red = wave_products_reduce32<1, C0, R>(brow, gg);
+    const int v = C0 + bitrev5(lane & 31);
+    if (lane < 32 && v < R) sred[(QOFF + v) * 4] = red;
+    if constexpr (C0 + 32 < R) ChunkLoop<C0 + 32, R, QOFF>::run(brow, g, sred, lane);
+  }
+};
+
+// Basis split: the first NBR columns of each row live in registers, the remaining
+// NBM-NBR in an LDS row tile with a padded stride (stride = 16m+4 words: the 16
+// lanes of a ds_read_b128 group land on distinct bank quads).
+template <int NBM>
+struct BasisSplit {
+  static constexpr int NBR = NBM < 32 ? NBM : 32;
+  static constexpr int NBL = NBM - NBR;               // multiple of 16
+  static constexpr int STRIDE = NBL > 0 ? NBL + 4 : 4;
+};
+
+template <int NBM, int LGM, int SP>
 __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
-  __shared__ float sW[NBM * kSMax];               // current W (f32) for f = B W
-  __shared__ float sGr[kThreads * kSMax];         // G[l][n]
-  __shared__ float sRed[kThreads * kSMax];        // group partials of B^T G
-  __shared__ double sRing[kRing][3][NBM * kSMax]; // (W, mu, nu) after each body
-  __shared__ double sSum[2][kThreads / 64];
-  __shared__ int sCtl[4];
+  using BS = BasisSplit<NBM>;
+  constexpr int NBR = BS::NBR, NBL = BS::NBL, STRIDE = BS::STRIDE;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sBl = smem;                                   // [kThreads][STRIDE]
+  float* sW = sBl + kThreads * STRIDE;                 // [NBM][4] current W (f32)
+  float* sRed = sW + NBM * kSMax;                      // [8 waves][NBM][4] partial B^T G
+  double* sSum = reinterpret_cast<double*>(sRed + (kThreads / 64) * NBM * kSMax);  // [2][8]
+  double* sYw = sSum + 2 * (kThreads / 64);                                         // [kThreads][4]
+  int* sCtl = reinterpret_cast<int*>(sYw + kThreads * kSMax);                       // [4]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
@@ -76,216 +184,272 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
   const double lconst = log(sd) + 0.5 * log(2.0 * M_PI);
 
   // ---- one-time loads -------------------------------------------------------
-  float brow[NBM];
   const bool is_row = tid < L;
+  float brow[NBR];
 #pragma unroll
-  for (int k = 0; k < NBM; ++k) brow[k] = (is_row && k < NB) ? p.basis[(size_t)tid * NB + k] : 0.f;
-  const int kk = tid % NB, grp = tid / NB;
-  const bool is_col = grp < p.ng;
-  const int lbeg = grp * p.LG;
-  float bcol[LGM];
-#pragma unroll
-  for (int i = 0; i < LGM; ++i) {
-    const int l = lbeg + i;
-    bcol[i] = (is_col && i < p.LG && l < L) ? p.basis[(size_t)l * NB + kk] : 0.f;
+  for (int k = 0; k < NBR; ++k) brow[k] = (is_row && k < NB) ? p.basis[(size_t)tid * NB + k] : 0.f;
+  for (int k = 0; k < STRIDE; ++k) {
+    const int q = NBR + k;
+    sBl[tid * STRIDE + k] = (is_row && k < NBL && q < NB) ? p.basis[(size_t)tid * NB + q] : 0.f;
   }
-  float ywf[kSMax];
-  double ywd[kSMax];
   double twd = 0.0;
-#pragma unroll
-  for (int s = 0; s < kSMax; ++s) {
-    ywd[s] = (is_row && s < S) ? p.yw[(size_t)tid * p.N + n0 + s] : 0.0;
-    ywf[s] = (float)ywd[s];
-  }
+  for (int s = 0; s < kSMax; ++s)
+    sYw[tid * kSMax + s] = (is_row && s < S) ? p.yw[(size_t)tid * p.N + n0 + s] : 0.0;
   if (is_row) twd = p.tw[tid];
   const float twf = (float)twd;
-  // element role: (ek, en) owns W[ek][n0+en]
   const int ek = tid % NB, en = tid / NB;
   const bool is_el = en < S;
   for (int q = tid; q < NBM * kSMax; q += blockDim.x) sW[q] = 0.f;
   if (tid < 4) sCtl[tid] = 0;
+  // element state (W, mu, nu) of this thread's weight, and its global ring
+  double w_cur = 0.0, mu_cur = 0.0, nu_cur = 0.0;
+  double* ring = p.ring + (size_t)g * kRing * 3 * NBM * kSMax;
+  const int e = ek * kSMax + en;
   __syncthreads();
   if (is_el) {
     const size_t o = (size_t)ek * p.N + n0 + en;
-    sRing[0][0][ek * kSMax + en] = p.W[o];
-    sRing[0][1][ek * kSMax + en] = p.mu[o];
-    sRing[0][2][ek * kSMax + en] = p.nu[o];
-    sW[ek * kSMax + en] = (float)p.W[o];
+    w_cur = p.W[o];
+    mu_cur = p.mu[o];
+    nu_cur = p.nu[o];
+    sW[e] = (float)w_cur;
+    ring[(0 * 3 + 0) * NBM * kSMax + e] = w_cur;
+    ring[(0 * 3 + 1) * NBM * kSMax + e] = mu_cur;
+    ring[(0 * 3 + 2) * NBM * kSMax + e] = nu_cur;
   }
   const int64_t count0 = p.count[0];
+  double b1t = pow(p.b1, (double)count0), b2t = pow(p.b2, (double)count0);
   __syncthreads();
 
   double loss_prev = 0.0, loss0 = 0.0;
-  int next_j = 0;          // next body whose global loss is undecided
-  int stop_j = -1;         // body after which the loop stops
-  double fin_loss = 0.0, fin_err = 0.0;
+  int dj = 0;                              // next body to decide (wave 0)
+  unsigned long long lv0[kPartPerLane];    // body dj loss partials (in flight)
+  unsigned long long lv1[kPartPerLane];    // body dj+1
+  bool issued0 = false, issued1 = false;
+  double fin_loss = 0.0;
   const int maxiter = p.maxiter;
   const bool eval_only = maxiter <= 1;
 
   for (int k = 0;; ++k) {
-    const int slot = k % kRing;
     // ---- body k: evaluate at W_k ---------------------------------------------
     double lpart = 0.0;
-    if (is_row) {
+    // neurons one at a time (runtime loop, not unrolled: one neuron's registers live)
+#pragma unroll 1
+    for (int s = 0; s < S; ++s) {
+      float F = 0.f;
 #pragma unroll
-      for (int s = 0; s < kSMax; ++s) {
-        if (s < S) {
-          float F = 0.f;
+      for (int q = 0; q < NBR; ++q) F = fmaf(brow[q], sW[q * kSMax + s], F);
 #pragma unroll
-          for (int q = 0; q < NBM; ++q) F = fmaf(brow[q], sW[q * kSMax + s], F);
-          const float f = softplus_f(F);
-          const float sg = sigmoid_f(F);
-          sGr[tid * kSMax + s] = (ywf[s] / (f + 1e-20f) - twf) * sg;
-          const double fd = (double)f;
-          const double xl = (ywd[s] != 0.0) ? ywd[s] * log(fd + 1e-20) : 0.0;
-          lpart -= xl - fd * twd;
+      for (int q4 = 0; q4 < NBL; q4 += 4) {
+        const float4 b4 = *reinterpret_cast<const float4*>(&sBl[tid * STRIDE + q4]);
+        F = fmaf(b4.x, sW[(NBR + q4) * kSMax + s], F);
+        F = fmaf(b4.y, sW[(NBR + q4 + 1) * kSMax + s], F);
+        F = fmaf(b4.z, sW[(NBR + q4 + 2) * kSMax + s], F);
+        F = fmaf(b4.w, sW[(NBR + q4 + 3) * kSMax + s], F);
+      }
+      const double ywd = is_row ? sYw[tid * kSMax + s] : 0.0;
+      const float f = softplus_f(F);
+      const float sg = sigmoid_f(F);
+      const float gr = is_row ? ((float)ywd / (f + 1e-20f) - twf) * sg : 0.f;
+      if (is_row) {
+        const double xl = (ywd != 0.0) ? ywd * (double)__logf(f + 1e-20f) : 0.0;
+        lpart -= xl - (double)f * twd;
+      }
+      // per-wave partial of B^T G for this neuron, 32 columns per chunk
+      float* sr = &sRed[(wid * NBM) * kSMax] + s;
+      ChunkLoop<0, NBR, 0>::run(brow, gr, sr, lane);
+#pragma unroll
+      for (int c0 = 0; c0 < NBL; c0 += 32) {
+        float bl[32];
+#pragma unroll
+        for (int q4 = 0; q4 < 32; q4 += 4) {
+          const float4 b4 = (c0 + q4 < NBL)
+                                ? *reinterpret_cast<const float4*>(&sBl[tid * STRIDE + c0 + q4])
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+          bl[q4] = b4.x;
+          bl[q4 + 1] = b4.y;
+          bl[q4 + 2] = b4.z;
+          bl[q4 + 3] = b4.w;
         }
+        const float gg[1] = {gr};
+        const float red = wave_products_reduce32<1, 0, 32>(bl, gg);
+        const int v = c0 + bitrev5(lane & 31);
+        if (lane < 32 && v < NBL) sr[(NBR + v) * kSMax] = red;
       }
     }
-    __syncthreads();
-    if (is_col) {
-#pragma unroll
-      for (int s = 0; s < kSMax; ++s) {
-        if (s < S) {
-          float acc = 0.f;
-#pragma unroll
-          for (int i = 0; i < LGM; ++i) {
-            const int l = lbeg + i;
-            if (i < p.LG && l < L) acc = fmaf(bcol[i], sGr[l * kSMax + s], acc);
-          }
-          sRed[(grp * NB + kk) * kSMax + s] = acc;
-        }
-      }
-    }
-    __syncthreads();
+    PMG_LDS_BARRIER();
     double gsq = 0.0;
+    b1t *= p.b1;
+    b2t *= p.b2;
     if (is_el) {
       float gsum = 0.f;
-      for (int q = 0; q < p.ng; ++q) gsum += sRed[(q * NB + ek) * kSMax + en];
-      const int e = ek * kSMax + en;
-      const double w = sRing[slot][0][e];
-      const double gr = -(double)gsum + w * isd2;
+      const int nw = (int)(blockDim.x >> 6);
+      for (int q = 0; q < nw; ++q) gsum += sRed[(q * NBM) * kSMax + e];
+      const double gr = -(double)gsum + w_cur * isd2;
       gsq = gr * gr;
-      lpart += 0.5 * w * w * isd2 + lconst;
-      // optax 0.2.2 scale_by_adam + scale(-lr)
-      const double cnt = (double)(count0 + k + 1);
-      const double mu = (1.0 - p.b1) * gr + p.b1 * sRing[slot][1][e];
-      const double nu = (1.0 - p.b2) * gr * gr + p.b2 * sRing[slot][2][e];
-      const double mh = mu / (1.0 - pow(p.b1, cnt));
-      const double nh = nu / (1.0 - pow(p.b2, cnt));
-      const double wn = w - p.lr * (mh / (sqrt(nh + p.eps_root) + p.eps));
+      lpart += 0.5 * w_cur * w_cur * isd2 + lconst;
+      if (!eval_only) {  // optax 0.2.2 scale_by_adam + scale(-lr)
+        const double mu = (1.0 - p.b1) * gr + p.b1 * mu_cur;
+        const double nu = (1.0 - p.b2) * gr * gr + p.b2 * nu_cur;
+        const double mh = mu / (1.0 - b1t);
+        const double nh = nu / (1.0 - b2t);
+        w_cur = w_cur - p.lr * (mh / (sqrt(nh + p.eps_root) + p.eps));
+        mu_cur = mu;
+        nu_cur = nu;
+      }
       const int ns = (k + 1) % kRing;
-      sRing[ns][0][e] = eval_only ? w : wn;
-      sRing[ns][1][e] = eval_only ? sRing[slot][1][e] : mu;
-      sRing[ns][2][e] = eval_only ? sRing[slot][2][e] : nu;
+      ring[(ns * 3 + 0) * NBM * kSMax + e] = w_cur;
+      ring[(ns * 3 + 1) * NBM * kSMax + e] = mu_cur;
+      ring[(ns * 3 + 2) * NBM * kSMax + e] = nu_cur;
+      sW[e] = (float)w_cur;
     }
-    // block sums of the partial loss and squared gradient
     lpart = wave_sum_f64(lpart);
     gsq = wave_sum_f64(gsq);
     if (lane == 0) {
-      sSum[0][wid] = lpart;
-      sSum[1][wid] = gsq;
+      sSum[wid] = lpart;
+      sSum[(kThreads / 64) + wid] = gsq;
     }
-    __syncthreads();
+    PMG_LDS_BARRIER();
     if (tid == 0) {
       double a = 0.0, b = 0.0;
       for (int q = 0; q < (int)(blockDim.x >> 6); ++q) {
-        a += sSum[0][q];
-        b += sSum[1][q];
+        a += sSum[q];
+        b += sSum[(kThreads / 64) + q];
       }
       st_sc1(&p.lpart[(size_t)k * p.G + g], a);
       st_sc1(&p.gpart[(size_t)k * p.G + g], b);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_fetch_add(&p.cnt[k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (is_el) sW[ek * kSMax + en] = (float)sRing[(k + 1) % kRing][0][ek * kSMax + en];
-    __syncthreads();
 
-    // ---- decide bodies whose partials are (or must be) complete --------------
-    const int last_decidable = eval_only ? k : k - kLag;
-    while (stop_j < 0 && next_j <= last_decidable && next_j < maxiter) {
-      const int j = next_j;
-      if (wid == 0) {
-        if (lane == 0) {
+    // ---- decision pipeline (wave 0) -------------------------------------------
+    // Partials are pre-filled with a signalling-NaN sentinel (never produced by
+    // arithmetic) and each is written once by one 8-byte atomic store, so a load
+    // returns either the sentinel (not published yet) or the final value.  Loads for
+    // bodies dj and dj+1 are issued in one body and consumed in the next, so the
+    // cross-XCD latency overlaps the following body's arithmetic; only when the
+    // pipeline is kLag bodies behind does wave 0 block (bounded spin).
+    if (wid == 0) {
+      for (int rep = 0; rep < 2; ++rep) {
+        const bool must = eval_only || (k - dj) >= kLag;
+        if (!issued0 || dj > k) break;
+        bool ok = true;
+#pragma unroll
+        for (int q = 0; q < kPartPerLane; ++q) ok &= (lv0[q] != kSentinel);
+        ok = __all(ok);
+        if (!ok && must) {  // blocking re-poll of body dj
           unsigned spins = 0;
-          while (__hip_atomic_load(&p.cnt[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                 (unsigned)p.G) {
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1u << 26)) {
-              atomicOr(p.timeout, 1);
-              sCtl[2] = 1;
+          while (!ok) {
+            __builtin_amdgcn_s_sleep(1);
+            load_parts(p, dj, lane, lv0);
+            ok = true;
+#pragma unroll
+            for (int q = 0; q < kPartPerLane; ++q) ok &= (lv0[q] != kSentinel);
+            ok = __all(ok);
+            if (++spins > (1u << 24)) {
+              if (lane == 0) {
+                atomicOr(p.timeout, 1);
+                sCtl[2] = 1;
+              }
               break;
             }
           }
+          if (!ok) break;
         }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        double a = 0.0, b = 0.0;
-        for (int q = lane; q < p.G; q += 64) {
-          a += ld_sc1(&p.lpart[(size_t)j * p.G + q]);
-          b += ld_sc1(&p.gpart[(size_t)j * p.G + q]);
+        if (!ok) {  // not published yet: re-issue, try next body
+          load_parts(p, dj, lane, lv0);
+          break;
         }
-        a = wave_sum_f64(a);
-        b = wave_sum_f64(b);
-        if (lane == 0) {
-          const double loss = a, err = sqrt(b);
-          if (j == 0) {
-            loss0 = loss;
-            loss_prev = loss;
-            if (g == 0) {
-              p.loss_hist[0] = loss;
-              p.err_hist[0] = err;
-            }
-          }
-          bool cont;
-          if (eval_only) {
-            cont = false;
-          } else {
-            if (g == 0 && j + 1 < maxiter) {
-              p.loss_hist[j + 1] = loss;
-              p.err_hist[j + 1] = err;
-            }
-            const double rel = fabs(loss - loss_prev) / fmax(fabs(loss), 1e-8);
-            cont = (j + 1 < maxiter - 1) && ((j + 1 < 5) || (rel > p.tol));
-          }
+        const double loss = sum_parts(lv0);
+        const int j = dj;
+        if (j == 0) {
+          loss0 = loss;
           loss_prev = loss;
-          sCtl[0] = cont ? 0 : 1;
-          if (!cont) {
-            fin_loss = loss;
-            fin_err = err;
-          }
+        }
+        bool cont;
+        if (eval_only) {
+          cont = false;
+        } else {
+          const double rel = fabs(loss - loss_prev) / fmax(fabs(loss), 1e-8);
+          cont = (j + 1 < maxiter - 1) && ((j + 1 < 5) || (rel > p.tol));
+        }
+        loss_prev = loss;
+        ++dj;
+        if (!cont) {
+          fin_loss = loss;
+          if (lane == 0) sCtl[0] = 1, sCtl[1] = j;
+          break;
+        }
+#pragma unroll
+        for (int q = 0; q < kPartPerLane; ++q) lv0[q] = lv1[q];
+        issued0 = issued1;
+        issued1 = false;
+      }
+      if (!sCtl[0]) {  // keep bodies dj and dj+1 in flight (both <= k)
+        if (!issued0 && dj <= k) {
+          load_parts(p, dj, lane, lv0);
+          issued0 = true;
+        }
+        if (!issued1 && dj + 1 <= k) {
+          load_parts(p, dj + 1, lane, lv1);
+          issued1 = true;
         }
       }
-      __syncthreads();
-      if (sCtl[0]) stop_j = next_j;
-      ++next_j;
-      __syncthreads();
     }
-    if (stop_j >= 0) break;
-    if (sCtl[2]) break;  // a wait timed out (reported through p.timeout)
+    PMG_LDS_BARRIER();
+    if (sCtl[0] || sCtl[2]) break;
   }
-
-  // ---- write the state after body stop_j (W_{stop_j+1}) -----------------------
+  const int stop_j = sCtl[1];
+  // ---- write the state after body stop_j (W_{stop_j+1}) from the ring ---------
   const int fs = eval_only ? (1 % kRing) : ((stop_j + 1) % kRing);
-  if (is_el && stop_j >= 0) {
+  if (is_el && !sCtl[2]) {
     const size_t o = (size_t)ek * p.N + n0 + en;
-    const int e = ek * kSMax + en;
-    p.W[o] = sRing[fs][0][e];
-    p.mu[o] = sRing[fs][1][e];
-    p.nu[o] = sRing[fs][2][e];
+    p.W[o] = ring[(fs * 3 + 0) * NBM * kSMax + e];
+    p.mu[o] = ring[(fs * 3 + 1) * NBM * kSMax + e];
+    p.nu[o] = ring[(fs * 3 + 2) * NBM * kSMax + e];
   }
-  if (g == 0 && tid == 0 && stop_j >= 0) {
+  if (g == 0 && tid == 0 && !sCtl[2]) {
     const int n_iter = eval_only ? 1 : stop_j + 2;
     p.stats[0] = (double)n_iter;
     p.stats[1] = fin_loss;
-    p.stats[2] = fin_err;
     p.stats[3] = loss0;
     p.count[0] = count0 + (eval_only ? 0 : (stop_j + 1));
   }
 }
 
+template <int NBM>
+static size_t adam_lds_bytes() {
+  using BS = BasisSplit<NBM>;
+  return sizeof(float) * ((size_t)kThreads * BS::STRIDE + NBM * kSMax +
+                          (kThreads / 64) * NBM * kSMax) +
+         sizeof(double) * (2 * (kThreads / 64) + kThreads * kSMax) + sizeof(int) * 4 + 64;
+}
+
+// Histories (fit_tuning_helper.py:147-149, :175-176) from the published partials, summed
+// in the decision's order: loss_hist[0] = loss of body 0, loss_hist[j+1] = loss of body j
+// (j + 1 < n_iter); the same for the gradient norm; final_error = norm of the last body.
+__global__ void __launch_bounds__(64) k_adam_hist(AdamParams p) {
+  const int lane = threadIdx.x;
+  const int n_iter = (int)p.stats[0];
+  if (n_iter <= 0) return;
+  for (int i = blockIdx.x; i < n_iter; i += gridDim.x) {
+    const int j = (i == 0) ? 0 : i - 1;
+    unsigned long long lv[kPartPerLane], gv[kPartPerLane];
+#pragma unroll
+    for (int q = 0; q < kPartPerLane; ++q) {
+      const int gi = lane + 64 * q;
+      lv[q] = gi < p.G ? p.lpart[(size_t)j * p.G + gi] : 0ull;
+      gv[q] = gi < p.G ? p.gpart[(size_t)j * p.G + gi] : 0ull;
+    }
+    const double loss = sum_parts(lv);
+    const double err = sqrt(sum_parts(gv));
+    if (lane == 0) {
+      p.loss_hist[i] = loss;
+      p.err_hist[i] = err;
+      if (i == n_iter - 1) p.stats[2] = err;
+    }
+  }
+}
+
 struct AdamWork {
-  unsigned* cnt;
+  double* ring;
   unsigned long long* lpart;
   unsigned long long* gpart;
   int* timeout;
@@ -295,7 +459,7 @@ static size_t adam_ws(int G, int maxiter, AdamWork* w, void* base) {
   Carver c(base);
   AdamWork ww;
   ww.timeout = c.take<int>(64);
-  ww.cnt = c.take<unsigned>((size_t)maxiter + kLag + 2);
+  ww.ring = c.take<double>((size_t)G * kRing * 3 * 128 * kSMax);
   ww.lpart = c.take<unsigned long long>(((size_t)maxiter + kLag + 2) * G);
   ww.gpart = c.take<unsigned long long>(((size_t)maxiter + kLag + 2) * G);
   if (w) *w = ww;
@@ -304,13 +468,26 @@ static size_t adam_ws(int G, int maxiter, AdamWork* w, void* base) {
 
 typedef void (*adam_kernel_t)(AdamParams);
 
-static adam_kernel_t pick_adam(int NB, int LG) {
-  const int m = NB > LG ? NB : LG;
-  if (m <= 32) return k_adam<32, 32>;
-  if (m <= 64) return k_adam<64, 64>;
-  if (m <= 96) return k_adam<96, 96>;
-  if (m <= 128) return k_adam<128, 128>;
-  return nullptr;
+struct AdamKernel {
+  adam_kernel_t fn;
+  size_t lds;
+};
+
+template <int NBM>
+static AdamKernel pick_sp(int SPn) {
+  (void)SPn;  // neurons are looped at run time inside the kernel
+  return {k_adam<NBM, NBM, 1>, adam_lds_bytes<NBM>()};
+}
+
+static AdamKernel pick_adam(int NB, int SPn) {
+  if (NB <= 32) return pick_sp<32>(SPn);
+  if (NB <= 48) return pick_sp<48>(SPn);
+  if (NB <= 64) return pick_sp<64>(SPn);
+  if (NB <= 80) return pick_sp<80>(SPn);
+  if (NB <= 96) return pick_sp<96>(SPn);
+  if (NB <= 112) return pick_sp<112>(SPn);
+  if (NB <= 128) return pick_sp<128>(SPn);
+  return {nullptr, 0};
 }
 
 static int num_cus() {
@@ -324,6 +501,7 @@ static void adam_geometry(int N, int L, int NB, int& S, int& G, int& ng, int& LG
   const int cus = num_cus();
   S = (N + cus - 1) / cus;
   if (S < 1) S = 1;
+  if (S == 3) S = 4;
   G = (N + S - 1) / S;
   ng = kThreads / NB;
   if (ng < 1) ng = 1;
@@ -355,15 +533,22 @@ int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const floa
   adam_geometry(N, L, NB, S, G, ng, LG);
   PMG_REQUIRE(S <= kSMax, "pmg_mstep_adam: N=%d needs %d neurons per workgroup (> %d)", N, S, kSMax);
   PMG_REQUIRE(NB * S <= kThreads, "pmg_mstep_adam: NB*S=%d > %d", NB * S, kThreads);
-  adam_kernel_t kern = pick_adam(NB, LG);
-  PMG_REQUIRE(kern != nullptr, "pmg_mstep_adam: NB=%d / row group %d > 128 unsupported", NB, LG);
+  AdamKernel kern = pick_adam(NB, S);
+  PMG_REQUIRE(kern.fn != nullptr && kern.lds <= 160 * 1024,
+              "pmg_mstep_adam: NB=%d unsupported (basis must fit registers + 160 KiB LDS)", NB);
   const int maxiter = cfg->maxiter > 1 ? cfg->maxiter : 1;
   PMG_REQUIRE(workspace_bytes >= adam_ws(G, maxiter, nullptr, nullptr),
               "pmg_mstep_adam: workspace too small");
   hipStream_t st = as_stream(stream);
   AdamWork w;
   adam_ws(G, maxiter, &w, workspace);
-  PMG_HIP(hipMemsetAsync(w.cnt, 0, sizeof(unsigned) * ((size_t)maxiter + kLag + 2), st));
+  {
+    const size_t n = ((size_t)maxiter + kLag + 2) * G;
+    hipLaunchKernelGGL(k_fill_u64, dim3(256), dim3(256), 0, st, w.lpart, n, kSentinel);
+    PMG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_fill_u64, dim3(256), dim3(256), 0, st, w.gpart, n, kSentinel);
+    PMG_LAUNCH_CHECK();
+  }
   PMG_HIP(hipMemsetAsync(w.timeout, 0, sizeof(int), st));
   PMG_HIP(hipMemsetAsync(loss_hist, 0, sizeof(double) * (size_t)maxiter, st));
   PMG_HIP(hipMemsetAsync(err_hist, 0, sizeof(double) * (size_t)maxiter, st));
@@ -394,11 +579,17 @@ int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const floa
   p.stats = stats;
   p.loss_hist = loss_hist;
   p.err_hist = err_hist;
-  p.cnt = w.cnt;
   p.lpart = w.lpart;
   p.gpart = w.gpart;
   p.timeout = w.timeout;
-  hipLaunchKernelGGL(kern, dim3(G), dim3(kThreads), 0, st, p);
+  p.ring = w.ring;
+  PMG_HIP(hipMemsetAsync(stats, 0, 4 * sizeof(double), st));
+  if (kern.lds > 64 * 1024)
+    PMG_HIP(hipFuncSetAttribute((const void*)kern.fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)kern.lds));
+  hipLaunchKernelGGL(kern.fn, dim3(G), dim3(kThreads), kern.lds, st, p);
+  PMG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_adam_hist, dim3(64), dim3(64), 0, st, p);
   PMG_LAUNCH_CHECK();
   return PMG_OK;
 }

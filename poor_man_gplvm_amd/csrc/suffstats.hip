@@ -7,8 +7,9 @@
 //
 // Both operands are time-major, which is exactly the per-lane layout of
 // v_mfma_f32_32x32x2f32: lane (r = lane&31, h = lane>>5) supplies A[row r][k = h] and
-// B[k = h][col r], i.e. 32 consecutive floats of one time row per half-wave --
-// coalesced 128-B loads straight from HBM, no LDS transpose.
+// B[k = h][col r], i.e. 32 consecutive floats of one time row per half-wave, so K-tiles
+// are staged row-major in LDS (float4 global loads, no transpose) and read back with
+// conflict-free ds_read_b32.
 // Products are exact fp32 (the instruction is an fma chain); each wave flushes its
 // fp32 accumulators into f64 registers every 128 time steps and writes one f64
 // partial per K-slice; slices are summed in f64 in a fixed order.
@@ -20,54 +21,111 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 
 constexpr int kFlush = 128;  // time steps per fp32 accumulation segment
 
-// wave tile 64 (m) x 64 (n); grid of waves (mt, nt, ks)
+// Workgroup tile 128 (m) x 128 (n), 4 waves as 2 x 2 of 64 x 64 (2 x 2 MFMA tiles each).
+// K (time) advances in tiles of KB rows staged through LDS: the next tile is loaded
+// into registers (float4, coalesced) while the MFMAs consume the current one.
+constexpr int KB = 32;
+constexpr int TM = 128, TN = 128;
+
 __global__ void __launch_bounds__(256) k_atb(const float* __restrict__ A, int64_t lda, int Mdim,
                                              const float* __restrict__ B, int64_t ldb, int Ndim,
                                              int shift, int64_t K, int64_t KT, int nMT, int nNT,
                                              int nKS, int Mp, int Npd, double* __restrict__ part) {
-  const int lane = threadIdx.x & 63;
-  const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (w >= (int64_t)nMT * nNT * nKS) return;
-  const int mt = (int)(w % nMT);
-  const int nt = (int)((w / nMT) % nNT);
-  const int ks = (int)(w / ((int64_t)nMT * nNT));
+  __shared__ __attribute__((aligned(16))) float sA[KB][TM];
+  __shared__ __attribute__((aligned(16))) float sB[KB][TN];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int mt = blockIdx.x % nMT;
+  const int nt = (blockIdx.x / nMT) % nNT;
+  const int ks = blockIdx.x / (nMT * nNT);
+  const int wm = wid & 1, wn = wid >> 1;
   const int r = lane & 31, h = lane >> 5;
-  const int m0 = mt * 64 + r, m1 = m0 + 32;
-  const int n0 = nt * 64 + r, n1 = n0 + 32;
-  const bool vm0 = m0 < Mdim, vm1 = m1 < Mdim, vn0 = n0 < Ndim, vn1 = n1 < Ndim;
   const int64_t kb = (int64_t)ks * KT;
   const int64_t ke = kb + KT < K ? kb + KT : K;
+
+  // staging map: each thread moves 4 float4 of A and 4 of B per K-tile
+  // element e = tid + 256*q (q < 4): row = e / 32, col4 = e % 32
+  const bool vecA = (lda & 3) == 0 && (Mdim & 3) == 0;
+  const bool vecB = (ldb & 3) == 0 && (Ndim & 3) == 0;
+  float4 ra[4], rb[4];
+  auto load_tile = [&](int64_t t0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid + 256 * q;
+      const int row = e >> 5, c4 = (e & 31) * 4;
+      const int64_t t = t0 + row;
+      const int m = mt * TM + c4, n = nt * TN + c4;
+      float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
+      if (t < ke) {
+        const float* ar = A + t * lda;
+        const float* br = B + (t + shift) * ldb;
+        if (vecA && m + 3 < Mdim) {
+          va = *reinterpret_cast<const float4*>(ar + m);
+        } else {
+          va.x = m < Mdim ? ar[m] : 0.f;
+          va.y = m + 1 < Mdim ? ar[m + 1] : 0.f;
+          va.z = m + 2 < Mdim ? ar[m + 2] : 0.f;
+          va.w = m + 3 < Mdim ? ar[m + 3] : 0.f;
+        }
+        if (vecB && n + 3 < Ndim) {
+          vb = *reinterpret_cast<const float4*>(br + n);
+        } else {
+          vb.x = n < Ndim ? br[n] : 0.f;
+          vb.y = n + 1 < Ndim ? br[n + 1] : 0.f;
+          vb.z = n + 2 < Ndim ? br[n + 2] : 0.f;
+          vb.w = n + 3 < Ndim ? br[n + 3] : 0.f;
+        }
+      }
+      ra[q] = va;
+      rb[q] = vb;
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid + 256 * q;
+      const int row = e >> 5, c4 = (e & 31) * 4;
+      *reinterpret_cast<float4*>(&sA[row][c4]) = ra[q];
+      *reinterpret_cast<float4*>(&sB[row][c4]) = rb[q];
+    }
+  };
 
   double acc64[4][16];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc64[q][i] = 0.0;
+  v16f c00 = {0}, c01 = {0}, c10 = {0}, c11 = {0};
+  int rows_in_seg = 0;
 
-  for (int64_t s0 = kb; s0 < ke; s0 += kFlush) {
-    const int64_t s1 = s0 + kFlush < ke ? s0 + kFlush : ke;
-    v16f c00 = {0}, c01 = {0}, c10 = {0}, c11 = {0};
-#pragma unroll 4
-    for (int64_t t = s0; t < s1; t += 2) {
-      const int64_t tt = t + h;
-      const bool vt = tt < s1;
-      const float* ar = A + tt * lda;
-      const float* br = B + (tt + shift) * ldb;
-      const float a0 = (vt && vm0) ? ar[m0] : 0.f;
-      const float a1 = (vt && vm1) ? ar[m1] : 0.f;
-      const float b0 = (vt && vn0) ? br[n0] : 0.f;
-      const float b1 = (vt && vn1) ? br[n1] : 0.f;
+  const int am0 = wm * 64 + r, am1 = am0 + 32;
+  const int bn0 = wn * 64 + r, bn1 = bn0 + 32;
+  if (kb < ke) load_tile(kb);
+  for (int64_t t0 = kb; t0 < ke; t0 += KB) {
+    __syncthreads();
+    store_tile();
+    __syncthreads();
+    if (t0 + KB < ke) load_tile(t0 + KB);  // in flight during the MFMAs below
+#pragma unroll
+    for (int kk = 0; kk < KB; kk += 2) {
+      const float a0 = sA[kk + h][am0], a1 = sA[kk + h][am1];
+      const float b0 = sB[kk + h][bn0], b1 = sB[kk + h][bn1];
       c00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, c00, 0, 0, 0);
       c01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, c01, 0, 0, 0);
       c10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, c10, 0, 0, 0);
       c11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, c11, 0, 0, 0);
     }
+    rows_in_seg += KB;
+    if (rows_in_seg >= kFlush || t0 + KB >= ke) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      acc64[0][i] += (double)c00[i];
-      acc64[1][i] += (double)c01[i];
-      acc64[2][i] += (double)c10[i];
-      acc64[3][i] += (double)c11[i];
+      for (int i = 0; i < 16; ++i) {
+        acc64[0][i] += (double)c00[i];
+        acc64[1][i] += (double)c01[i];
+        acc64[2][i] += (double)c10[i];
+        acc64[3][i] += (double)c11[i];
+        c00[i] = c01[i] = c10[i] = c11[i] = 0.f;
+      }
+      rows_in_seg = 0;
     }
   }
   // C/D layout: col = lane&31, row = (i&3) + 8*(i>>2) + 4*h
@@ -75,10 +133,10 @@ __global__ void __launch_bounds__(256) k_atb(const float* __restrict__ A, int64_
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int mi = q >> 1, ni = q & 1;
-    const int col = nt * 64 + ni * 32 + r;
+    const int col = nt * TN + wn * 64 + ni * 32 + r;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int row = mt * 64 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+      const int row = mt * TM + wm * 64 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
       pp[(size_t)row * Npd + col] = acc64[q][i];
     }
   }
@@ -101,13 +159,13 @@ __global__ void k_atb_reduce(const double* __restrict__ part, int nKS, int Mp, i
 
 static int atb_geometry(int64_t K, int Mdim, int Ndim, int& nMT, int& nNT, int& nKS, int64_t& KT,
                         int& Mp, int& Npd) {
-  nMT = (Mdim + 63) / 64;
-  nNT = (Ndim + 63) / 64;
-  Mp = nMT * 64;
-  Npd = nNT * 64;
-  // enough waves to fill the chip (~8 per CU), K-slices of whole flush segments
+  nMT = (Mdim + TM - 1) / TM;
+  nNT = (Ndim + TN - 1) / TN;
+  Mp = nMT * TM;
+  Npd = nNT * TN;
+  // ~2 workgroups per CU over 256 CUs, K-slices of whole flush segments
   const int64_t tiles = (int64_t)nMT * nNT;
-  int64_t want = (2048 + tiles - 1) / tiles;
+  int64_t want = (512 + tiles - 1) / tiles;
   if (want < 1) want = 1;
   KT = (K + want - 1) / want;
   KT = round_up(KT < kFlush ? kFlush : KT, kFlush);
@@ -130,8 +188,8 @@ static int atb_run(const float* A, int64_t lda, int Mdim, const float* B, int64_
   int64_t KT;
   atb_geometry(K, Mdim, Ndim, nMT, nNT, nKS, KT, Mp, Npd);
   double* part = reinterpret_cast<double*>(ws);
-  const int64_t waves = (int64_t)nMT * nNT * nKS;
-  hipLaunchKernelGGL(k_atb, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, A, lda, Mdim, B,
+  const int64_t wgs = (int64_t)nMT * nNT * nKS;
+  hipLaunchKernelGGL(k_atb, dim3((unsigned)wgs), dim3(256), 0, st, A, lda, Mdim, B,
                      ldb, Ndim, shift, K, KT, nMT, nNT, nKS, Mp, Npd, part);
   PMG_LAUNCH_CHECK();
   const int64_t total = (int64_t)Mdim * Npd;

@@ -50,8 +50,10 @@ class AdamConfig:
 class ScanConfig:
     """Time-parallel scan parameters (see fwdbwd.hip)."""
     chunk: int | None = None     # time steps per chunk (None: ~2048 chunks)
-    warmup: int = 48             # forgetting warm-up before each chunk
+    warmup: int = 64             # forgetting warm-up before each chunk (initial value)
     tol: float = 1e-6            # Hilbert-metric boundary tolerance
+    adaptive: bool = True        # double the warm-up when >1% of chunks needed repair
+    max_warmup: int = 1024
 
     def chunk_for(self, T):
         if self.chunk:
@@ -106,6 +108,55 @@ class SpikeData:
         self.int_path = self.flags == 0 and not self.ma_2d
 
 
+class KernelTimer:
+    """Per-call HIP event pairs on the current stream (torch.cuda.Event records on
+    torch's current stream, the stream every native call is enqueued on)."""
+
+    def __init__(self):
+        self.events = {}
+
+    def __call__(self, name):
+        return _TimedSection(self, name)
+
+    def summary(self):
+        """{name: (calls, mean ms)} -- synchronises."""
+        torch.cuda.synchronize()
+        out = {}
+        for k, evs in self.events.items():
+            ms = [a.elapsed_time(b) for a, b in evs]
+            out[k] = (len(ms), float(np.mean(ms)) if ms else 0.0)
+        return out
+
+    def reset(self):
+        self.events = {}
+
+
+class _TimedSection:
+    def __init__(self, timer, name):
+        self.timer, self.name = timer, name
+
+    def __enter__(self):
+        self.a = torch.cuda.Event(enable_timing=True)
+        self.a.record()
+
+    def __exit__(self, *exc):
+        b = torch.cuda.Event(enable_timing=True)
+        b.record()
+        self.timer.events.setdefault(self.name, []).append((self.a, b))
+        return False
+
+
+class _NoTimer:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NO_TIMER = _NoTimer()
+
+
 class DeviceEM:
     """One fit's device state: spikes, basis, transition, workspaces, buffers."""
 
@@ -143,10 +194,17 @@ class DeviceEM:
         if self.ws_fb.numel() == 0:
             raise nat.NativeError(f"n_latent_bin={L} unsupported by the scan kernels (max 1024)")
         self.ws_ad = None
+        self.warmup = int(self.scan.warmup)
+        self._rep_host = torch.zeros(2, dtype=torch.int32).pin_memory()
+        self._rep_evt = None
+        self.timer = None       # optional KernelTimer (bench): per-call HIP events
         self._tr = None
         self._tr_c = None
         self._invz = None
         self.ma_latent = None
+
+    def _t(self, name):
+        return self.timer(name) if self.timer is not None else _NO_TIMER
 
     # ------------------------------------------------------------------ setup
     def set_transition(self, tr: BandedTransition):
@@ -187,7 +245,8 @@ class DeviceEM:
     def m_step(self, W, mu, nu, count, cfg: AdamConfig, stats_out, lh_out, eh_out):
         """Sufficient statistics of self.P, then the Adam loop; W/mu/nu/count in place."""
         sh = nat.stream_handle()
-        nat.check(self.lib.pmg_suffstats(nat.ptr(self.P), nat.ptr(self.sp.yext), self.T, self.L, self.N,
+        with self._t('suffstats'):
+          nat.check(self.lib.pmg_suffstats(nat.ptr(self.P), nat.ptr(self.sp.yext), self.T, self.L, self.N,
                                          self.sp.Np, nat.ptr(self.yw), nat.ptr(self.tw),
                                          nat.ptr(self.ws_ss), self.ws_ss.numel(), sh), "pmg_suffstats")
         self.adam(W, mu, nu, count, cfg, stats_out, lh_out, eh_out)
@@ -199,14 +258,16 @@ class DeviceEM:
         if self.ws_ad is None or self.ws_ad.numel() < need:
             self.ws_ad = torch.empty(need, dtype=torch.uint8, device=self.dev)
         c = cfg.to_c()
-        nat.check(self.lib.pmg_mstep_adam(nat.ptr(W), nat.ptr(mu), nat.ptr(nu), nat.ptr(count),
+        with self._t('mstep_adam'):
+          nat.check(self.lib.pmg_mstep_adam(nat.ptr(W), nat.ptr(mu), nat.ptr(nu), nat.ptr(count),
                                           nat.ptr(self.basis), nat.ptr(self.yw), nat.ptr(self.tw),
                                           self.L, self.NB, self.N, ctypes.byref(c), nat.ptr(stats_out),
                                           nat.ptr(lh_out), nat.ptr(eh_out), nat.ptr(self.ws_ad),
                                           self.ws_ad.numel(), nat.stream_handle()), "pmg_mstep_adam")
 
     def compute_tuning(self, W):
-        nat.check(self.lib.pmg_tuning_softplus(nat.ptr(self.basis), nat.ptr(W), self.L, self.NB, self.N,
+        with self._t('tuning_softplus'):
+          nat.check(self.lib.pmg_tuning_softplus(nat.ptr(self.basis), nat.ptr(W), self.L, self.NB, self.N,
                                                nat.ptr(self.tuning64), nat.ptr(self.tuning32),
                                                nat.stream_handle()), "pmg_tuning_softplus")
 
@@ -220,6 +281,13 @@ class DeviceEM:
     # ------------------------------------------------------------------ E-step
     def emission(self, likelihood_scale=1.0, dt=1.0):
         sp, sh = self.sp, nat.stream_handle()
+        with self._t('emission'):
+          self._emission_call(sp, sh, dt)
+        with self._t('emission_rowref'):
+          nat.check(self.lib.pmg_emission_rowref(nat.ptr(self.rblk), self.T, self.nblk, float(likelihood_scale),
+                                                 nat.ptr(self.phi), nat.ptr(self.mref), sh), "pmg_emission_rowref")
+
+    def _emission_call(self, sp, sh, dt):
         if sp.int_path:
             ma1 = sp.ma if (sp.ma is not None and not sp.ma_2d) else None
             nat.check(self.lib.pmg_emission_poisson(nat.ptr(sp.yq), nat.ptr(sp.gconst), nat.ptr(self.tuning64),
@@ -233,22 +301,39 @@ class DeviceEM:
                                                         float(dt), self.T, self.L, self.N, nat.ptr(self.delta),
                                                         nat.ptr(self.rblk), nat.ptr(self.ws_em),
                                                         self.ws_em.numel(), sh), "pmg_emission_poisson_f64")
-        nat.check(self.lib.pmg_emission_rowref(nat.ptr(self.rblk), self.T, self.nblk, float(likelihood_scale),
-                                               nat.ptr(self.phi), nat.ptr(self.mref), sh), "pmg_emission_rowref")
+
+    def _adapt_warmup(self):
+        """Adaptive warm-up from the previous E-step's repair counters, read without a
+        host sync (pinned async copy + event query)."""
+        if not self.scan.adaptive or self._rep_evt is None or not self._rep_evt.query():
+            return
+        M = (self.T + self.C - 1) // self.C
+        f, b = (int(v) for v in self._rep_host.tolist())
+        if max(f, b) > max(1, M // 100) and self.warmup < self.scan.max_warmup:
+            self.warmup = min(self.scan.max_warmup, 2 * self.warmup)
+        self._rep_evt = None
+
+    def _snapshot_repairs(self):
+        self._rep_host.copy_(self.ws_fb[:8].view(torch.int32), non_blocking=True)
+        self._rep_evt = torch.cuda.Event()
+        self._rep_evt.record()
 
     def forward(self, likelihood_scale, logz_out):
+        self._adapt_warmup()
         sc = self.scan
-        nat.check(self.lib.pmg_forward_filter(nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.mref), self.T,
+        with self._t('forward_filter'):
+          nat.check(self.lib.pmg_forward_filter(nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.mref), self.T,
                                               ctypes.byref(self._tr_c), float(likelihood_scale), self.C,
-                                              int(sc.warmup), float(sc.tol), nat.ptr(self.alpha),
+                                              int(self.warmup), float(sc.tol), nat.ptr(self.alpha),
                                               nat.ptr(self.logc), nat.ptr(logz_out), nat.ptr(self.ws_fb),
                                               self.ws_fb.numel(), nat.stream_handle()), "pmg_forward_filter")
 
     def backward(self, likelihood_scale, P=True, gamma=None, rho=None):
         sc = self.scan
-        nat.check(self.lib.pmg_backward_smoother(nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.alpha),
+        with self._t('backward_smoother'):
+          nat.check(self.lib.pmg_backward_smoother(nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.alpha),
                                                  self.T, ctypes.byref(self._tr_c), float(likelihood_scale),
-                                                 self.C, int(sc.warmup), float(sc.tol),
+                                                 self.C, int(self.warmup), float(sc.tol),
                                                  nat.ptr(self.P) if P else None, nat.ptr(gamma), nat.ptr(rho),
                                                  nat.ptr(self.ws_fb), self.ws_fb.numel(), nat.stream_handle()),
                   "pmg_backward_smoother")
@@ -257,6 +342,7 @@ class DeviceEM:
         self.emission(likelihood_scale)
         self.forward(likelihood_scale, logz_out)
         self.backward(likelihood_scale, True, gamma, rho)
+        self._snapshot_repairs()
 
     def repairs(self):
         """(forward, backward) chunks repaired by the last scans (device read: syncs)."""
