@@ -1,0 +1,55 @@
+"""Restart sharding over torch.distributed ranks (model_selection_helper.py:35-60),
+world_size 2 on the gloo backend (CPU).  The per-restart fit is the CPU oracle
+(injected fit_fn) so the sharding/gather logic is exercised without a GPU."""
+import os
+import socket
+
+import numpy as np
+import torch.multiprocessing as mp
+
+from tests.synth import make
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _oracle_fit(model, y, key, fit_kwargs):
+    from oracle import gplvm_oracle as O
+    lp0 = O.init_latent_posterior_from_uniform(np.random.default_rng(key).random((y.shape[0], model.n_latent_bin)))
+    r = O.fit_em(y, model.params.astype(np.float64), model.tuning_basis.astype(np.float64), lp0,
+                 n_iter=fit_kwargs['n_iter'], m_step_maxiter=10, m_step_tol=0.0)
+    return {'log_marginal_l': r['log_marginal_l'], 'key': key}
+
+
+def _worker(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from poor_man_gplvm_amd import model_selection_helper as msh
+    d = make(8, 16, 40)
+    models, res = msh.fit_model_one_config({'n_latent_bin': 16, 'tuning_lengthscale': 3.0}, d['y'], key=11,
+                                           fit_kwargs={'n_iter': 2}, n_repeat=5, fit_fn=_oracle_fit)
+    out[rank] = [(r['key'], r['log_marginal_l']) for r in res]
+    dist.destroy_process_group()
+
+
+def test_restart_sharding_world2_matches_single_process():
+    from poor_man_gplvm_amd import model_selection_helper as msh
+    d = make(8, 16, 40)
+    _, ref = msh.fit_model_one_config({'n_latent_bin': 16, 'tuning_lengthscale': 3.0}, d['y'], key=11,
+                                      fit_kwargs={'n_iter': 2}, n_repeat=5, fit_fn=_oracle_fit)
+    ref = [(r['key'], r['log_marginal_l']) for r in ref]
+    mgr = mp.Manager()
+    out = mgr.dict()
+    port = _free_port()
+    mp.spawn(_worker, args=(2, port, out), nprocs=2, join=True)
+    for rank in range(2):
+        got = out[rank]
+        assert [k for k, _ in got] == [k for k, _ in ref]
+        for (_, a), (_, b) in zip(got, ref):
+            np.testing.assert_allclose(a, b, rtol=0, atol=0)

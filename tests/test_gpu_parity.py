@@ -1,0 +1,263 @@
+"""GPU parity: the HIP path (through the C ABI) vs the float64 oracle and the
+committed golden fixtures.
+
+Tolerances (BASELINE.json north_star: posterior_latent_marg and tuning within 1e-5
+rel-tol, argmax latent indices bit-exact):
+  * probabilities: |gpu - ref| <= 1e-5 * |ref| + 1e-12
+    (atol 1e-12: probabilities below ~1e-12 are compared in absolute terms)
+  * tuning: rel 1e-5 (fixed Adam iterations; see test_fit_em_stop_rule for n_iter)
+  * argmax of posterior_latent_marg: identical wherever the top-2 gap > 1e-5
+  * log marginal: rel 1e-7
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import gplvm_oracle as O
+from tests.synth import make
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+RT, AT = 1e-5, 1e-12
+
+
+def close_prob(a, b, rtol=RT, atol=AT):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    bad = np.abs(a - b) > rtol * np.abs(b) + atol
+    assert not bad.any(), f"{bad.sum()} / {bad.size} outside tol; max abs {np.abs(a - b).max():.3e}"
+
+
+def argmax_match(a, b):
+    b = np.asarray(b)
+    srt = np.sort(b, axis=1)
+    clear = (srt[:, -1] - srt[:, -2]) > 1e-5
+    assert np.all(np.argmax(a, 1)[clear] == np.argmax(b, 1)[clear])
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _dev():
+    torch.cuda.set_device(0)
+
+
+def _engine(d, L, mv=1.0, pmj=0.01, pjm=0.01, chunk=None, warmup=64, ma=None, ma_latent=None, y=None):
+    from poor_man_gplvm_amd.engine import SpikeData, DeviceEM, ScanConfig
+    from poor_man_gplvm_amd.gp_kernel import banded_transition
+    sp = SpikeData(d['y'] if y is None else y, ma)
+    eng = DeviceEM(sp, L, basis=d['B'], scan=ScanConfig(chunk=chunk, warmup=warmup))
+    eng.set_transition(banded_transition(L, mv, pmj, pjm))
+    eng.set_ma_latent(ma_latent)
+    return sp, eng
+
+
+# ----------------------------------------------------------------------------- emission
+@pytest.mark.parametrize("mask", ["none", "neuron1d", "latent", "neuron2d"])
+def test_emission(mask):
+    N, L, T = 40, 100, 300
+    d = make(N, L, T)
+    rng = np.random.default_rng(1)
+    ma = ml = None
+    if mask == "neuron1d":
+        ma = (rng.random(N) > 0.3).astype(np.float32)
+    if mask == "neuron2d":
+        ma = (rng.random((T, N)) > 0.3).astype(np.float32)
+    if mask == "latent":
+        ml = (rng.random(L) > 0.4).astype(np.float32)
+    sp, eng = _engine(d, L, ma=ma, ma_latent=ml)
+    assert sp.int_path == (mask != "neuron2d")
+    eng.set_tuning(d['tuning'])
+    eng.emission(1.0)
+    ll = eng.loglik().cpu().numpy().astype(np.float64)
+    ref = O.loglikelihood_poisson_all(d['y'], d['tuning'], ma, ml)
+    np.testing.assert_allclose(ll, ref, rtol=2e-7, atol=1e-5)
+    # precision near the row max (what the posterior sees): f64-accurate differences
+    dl = eng.delta.cpu().numpy().astype(np.float64) + np.repeat(eng.rblk.cpu().numpy(), 32, 1)[:, :L] \
+        - eng.mref.cpu().numpy()[:, None]
+    dr = ref - ref.max(1, keepdims=True)
+    m = dr > -40
+    assert np.max(np.abs(dl[m] - dr[m])) < 5e-6
+
+
+def test_emission_noninteger_counts_use_f64_path():
+    N, L, T = 16, 40, 100
+    d = make(N, L, T)
+    y = d['y'] + 0.5
+    sp, eng = _engine(d, L, y=y)
+    assert not sp.int_path
+    eng.set_tuning(d['tuning'])
+    eng.emission(1.0)
+    ref = O.loglikelihood_poisson_all(y, d['tuning'])
+    np.testing.assert_allclose(eng.loglik().cpu().numpy(), ref, rtol=2e-7, atol=1e-5)
+
+
+# ----------------------------------------------------------------------------- scan
+SCAN_CASES = [
+    # N, L, T, mv, pmj, pjm, chunk, warmup, s
+    (30, 100, 1000, 1.0, 0.01, 0.01, None, 64, 1.0),
+    (30, 100, 1000, 1.0, 0.01, 0.01, 16, 0, 1.0),       # every boundary repaired
+    (50, 37, 257, 0.5, 0.05, 0.02, 32, 8, 1.0),         # L not /32, T not /chunk
+    (64, 256, 2000, 2.0, 0.01, 0.01, 40, 32, 0.7),      # wider band, likelihood_scale
+    (20, 64, 1, 1.0, 0.01, 0.01, None, 64, 1.0),        # T = 1
+    (20, 64, 2, 1.0, 0.2, 0.3, None, 64, 1.0),          # T = 2
+    (24, 300, 700, 1.0, 0.01, 0.01, 100, 16, 1.0),      # L between 256 and 512
+]
+
+
+@pytest.mark.parametrize("case", SCAN_CASES)
+def test_forward_backward_vs_oracle(case):
+    N, L, T, mv, pmj, pjm, chunk, warm, s = case
+    d = make(N, L, T, mv=mv)
+    sp, eng = _engine(d, L, mv, pmj, pjm, chunk, warm)
+    eng.set_tuning(d['tuning'])
+    logz = torch.zeros(1, dtype=torch.float64, device='cuda')
+    gamma = torch.empty((T, 2, L), dtype=torch.float32, device='cuda')
+    rho = torch.zeros((T, 2, L), dtype=torch.float32, device='cuda')
+    eng.e_step(s, logz, gamma=gamma, rho=rho)
+    K, logK, A, logA = O.create_transition_prob_1d(L, mv, pmj, pjm)
+    lpa, lz, lca, cs, lj, _ = O.smooth_all_step_combined_ma_chunk(
+        d['y'], d['tuning'], logK, logA, likelihood_scale=s, with_joint=True)
+    post = np.exp(lpa)
+    g = gamma.cpu().numpy()
+    close_prob(g, post)
+    close_prob(g.sum(1), post.sum(1))
+    close_prob(eng.P.cpu().numpy(), post.sum(1))
+    argmax_match(g.sum(1), post.sum(1))
+    close_prob(eng.alpha.cpu().numpy(), np.exp(lca))
+    assert abs(logz.item() - lz) <= 1e-7 * abs(lz)
+    np.testing.assert_allclose(eng.logc.cpu().numpy(), cs, rtol=1e-6, atol=1e-5)
+    if T > 1:
+        S = eng.joint(rho).cpu().numpy().reshape(2, L, 2, L).transpose(0, 2, 1, 3)
+        J = np.exp(logA)[:, :, None, None] * K[None] * S
+        np.testing.assert_allclose(J, np.exp(lj), rtol=1e-4, atol=1e-5 * max(1.0, np.exp(lj).max()))
+
+
+def test_masked_latents_scan():
+    N, L, T = 30, 80, 500
+    d = make(N, L, T)
+    ml = np.ones(L)
+    ml[np.random.default_rng(2).choice(L, 30, replace=False)] = 0
+    sp, eng = _engine(d, L, ma_latent=ml, chunk=32, warmup=32)
+    eng.set_tuning(d['tuning'])
+    logz = torch.zeros(1, dtype=torch.float64, device='cuda')
+    gamma = torch.empty((T, 2, L), dtype=torch.float32, device='cuda')
+    eng.e_step(1.0, logz, gamma=gamma)
+    K, logK, A, logA = O.create_transition_prob_1d(L, 1.0)
+    lpa, lz, *_ = O.smooth_all_step_combined_ma_chunk(d['y'], d['tuning'], logK, logA, ma_latent=ml,
+                                                      with_joint=False)
+    close_prob(gamma.cpu().numpy(), np.exp(lpa))
+    assert np.all(gamma.cpu().numpy()[:, :, ml == 0] == 0)
+    assert abs(logz.item() - lz) <= 1e-7 * abs(lz)
+
+
+# ----------------------------------------------------------------------------- M-step
+def test_suffstats_vs_numpy():
+    N, L, T = 70, 100, 3000
+    d = make(N, L, T)
+    sp, eng = _engine(d, L)
+    P = np.random.default_rng(4).dirichlet(np.ones(L), size=T).astype(np.float32)
+    eng.P.copy_(torch.as_tensor(P, device='cuda'))
+    from poor_man_gplvm_amd import _native as nat
+    nat.check(eng.lib.pmg_suffstats(nat.ptr(eng.P), nat.ptr(sp.yext), T, L, N, sp.Np, nat.ptr(eng.yw),
+                                    nat.ptr(eng.tw), nat.ptr(eng.ws_ss), eng.ws_ss.numel(),
+                                    nat.stream_handle()), "suffstats")
+    yw, tw = O.get_statistics(np.log(P.astype(np.float64)), d['y'])
+    np.testing.assert_allclose(eng.yw.cpu().numpy(), yw, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(eng.tw.cpu().numpy(), tw, rtol=1e-6)
+
+
+@pytest.mark.parametrize("N,L,maxiter,tol", [(30, 100, 40, 0.0), (30, 100, 1000, 1e-6), (128, 256, 60, 0.0),
+                                             (7, 48, 1, 1e-6)])
+def test_adam_vs_oracle(N, L, maxiter, tol):
+    from poor_man_gplvm_amd.engine import AdamConfig
+    d = make(N, L, 500)
+    sp, eng = _engine(d, L)
+    P = np.exp(d['lp0'].astype(np.float64))
+    yw, tw = O.get_statistics(d['lp0'].astype(np.float64), d['y'])
+    eng.yw.copy_(torch.as_tensor(yw, device='cuda'))
+    eng.tw.copy_(torch.as_tensor(tw, device='cuda'))
+    W = torch.as_tensor(d['W0'].astype(np.float64), device='cuda').contiguous()
+    mu, nu = torch.zeros_like(W), torch.zeros_like(W)
+    cnt = torch.zeros(1, dtype=torch.int64, device='cuda')
+    stats = torch.zeros(4, dtype=torch.float64, device='cuda')
+    lh = torch.zeros(max(maxiter, 1), dtype=torch.float64, device='cuda')
+    eh = torch.zeros_like(lh)
+    eng.adam(W, mu, nu, cnt, AdamConfig(maxiter=maxiter, tol=tol), stats, lh, eh)
+    ref = O.adam_run(d['W0'].astype(np.float64), O.adam_init(d['W0']), 1.0, d['B'].astype(np.float64), yw, tw,
+                     maxiter=maxiter, tol=tol)
+    s = stats.cpu().numpy()
+    n = int(s[0])
+    assert n == ref['n_iter']
+    assert int(cnt.item()) == n - 1
+    B = d['B'].astype(np.float64)
+    np.testing.assert_allclose(np.logaddexp(B @ W.cpu().numpy(), 0), np.logaddexp(B @ ref['params'], 0), rtol=RT)
+    np.testing.assert_allclose(lh.cpu().numpy()[:n], ref['loss_history'][:n], rtol=1e-8)
+    np.testing.assert_allclose(eh.cpu().numpy()[:n], ref['error_history'][:n], rtol=1e-5)
+    np.testing.assert_allclose(s[1], ref['final_loss'], rtol=1e-8)
+    np.testing.assert_allclose(s[2], ref['final_error'], rtol=1e-5)
+
+
+# ----------------------------------------------------------------------------- full EM / decode
+def _fit_fixture(name):
+    import poor_man_gplvm_amd as P
+    f = np.load(os.path.join(HERE, 'golden', name))
+    L = f['basis'].shape[0]
+    res, info = P.run_em(f['y'].astype(np.float32), f['W0'], f['basis'], f['lp0'], n_iter=int(f['n_iter']),
+                         transition=P.banded_transition(L, float(f['mv'])),
+                         adam=P.AdamConfig(maxiter=int(f['maxiter']), tol=float(f['tol'])))
+    return f, res
+
+
+def test_fit_em_fixed_iterations_golden():
+    f, res = _fit_fixture('em_c1_fixed.npz')
+    np.testing.assert_allclose(res['tuning'], f['tuning'], rtol=RT)
+    close_prob(res['posterior_latent_marg'], f['posterior'].astype(np.float64).sum(1))
+    argmax_match(res['posterior_latent_marg'], f['posterior'].sum(1))
+    np.testing.assert_allclose(res['log_marginal_l'], f['log_marginal_l'], rtol=1e-7)
+    assert res['m_step_res_l']['n_iter'] == list(f['m_n_iter'])
+    np.testing.assert_allclose(res['m_step_res_l']['final_loss'], f['m_final_loss'], rtol=1e-8)
+    np.testing.assert_allclose(res['m_step_res_l']['loss_history'][0], f['m_loss_history_0'], rtol=1e-8)
+
+
+def test_fit_em_stop_rule_golden():
+    f, res = _fit_fixture('em_small_stoprule.npz')
+    assert res['m_step_res_l']['n_iter'] == list(f['m_n_iter'])
+    np.testing.assert_allclose(res['tuning'], f['tuning'], rtol=1e-4)
+    argmax_match(res['posterior_latent_marg'], f['posterior'].sum(1))
+    np.testing.assert_allclose(res['log_marginal_l'], f['log_marginal_l'], rtol=1e-6)
+
+
+def test_fit_em_api_dict():
+    import json
+    import poor_man_gplvm_amd as P
+    api = json.load(open(os.path.join(HERE, 'golden', 'reference_api.json')))
+    d = make(12, 32, 200)
+    m = P.PoissonGPLVMJump1D(12, n_latent_bin=32, tuning_lengthscale=5.)
+    res = m.fit_em(d['y'], key=3, n_iter=3, save_every=2)
+    assert list(res) == api['fit_em_keys']
+    assert res['iter_saved'] == [0, 2]
+    assert list(res['m_step_res_l']) == api['m_step_res_keys']
+    assert res['m_step_res_l']['params'] == [] and len(res['m_step_res_l']['n_iter']) == 3
+    assert res['posterior'].shape == (200, 2, 32)
+    np.testing.assert_allclose(res['posterior'].sum((1, 2)), 1.0, rtol=1e-5)
+    np.testing.assert_allclose(m.tuning, res['tuning'])
+
+
+@pytest.mark.parametrize("name", ['decode_small.npz', 'decode_masked.npz'])
+def test_decode_latent_golden(name):
+    import json
+    import poor_man_gplvm_amd as P
+    api = json.load(open(os.path.join(HERE, 'golden', 'reference_api.json')))
+    f = np.load(os.path.join(HERE, 'golden', name))
+    L = f['tuning'].shape[0]
+    m = P.PoissonGPLVMJump1D(f['y'].shape[1], n_latent_bin=L, tuning_lengthscale=5., movement_variance=float(f['mv']))
+    r = m.decode_latent(f['y'].astype(np.float32), tuning=f['tuning'],
+                        ma_latent=f['ma_latent'] if 'ma_latent' in f else None)
+    assert list(r) == api['decode_keys_recorded']
+    close_prob(r['posterior_all'], f['posterior_all'])
+    np.testing.assert_allclose(r['log_marginal_final'], float(f['log_marginal_final']), rtol=1e-7)
+    np.testing.assert_allclose(r['log_one_step_predictive_marginals_all'], f['log_one_step'], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(r['log_likelihood_all'], f['log_likelihood_all'], rtol=2e-7, atol=1e-5)
+    for k in ['p_transition_latent', 'p_transition_dynamics', 'p_joint_dynamics', 'p_joint_latent']:
+        np.testing.assert_allclose(r[k], f[k], rtol=1e-4, atol=1e-7)

@@ -1,0 +1,93 @@
+"""Host-side logic of the product package (no GPU): basis, banded transition,
+reference API facts, constructor.  The oracle is used only as the checker."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import gplvm_oracle as O
+import poor_man_gplvm_amd as P
+from poor_man_gplvm_amd.gp_kernel import banded_transition
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+API = json.load(open(os.path.join(HERE, 'golden', 'reference_api.json')))
+
+
+@pytest.mark.parametrize("L", [100, 256, 512])
+def test_generate_basis_matches_oracle(L):
+    b = P.generate_basis(10.0, L)
+    o = O.generate_basis(10.0, L)
+    assert b.shape == o.shape
+    assert b.shape[1] == API['n_basis_ls10'][str(L)]      # 18 / 41 / 79
+    np.testing.assert_allclose(np.abs(b), np.abs(o), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(b[:, 0], 1.0)
+
+
+@pytest.mark.parametrize("L,mv", [(100, 1.0), (512, 1.0), (37, 0.5), (256, 2.0), (64, 3.5)])
+def test_banded_transition_matches_dense(L, mv):
+    tr = banded_transition(L, mv, 0.02, 0.03)
+    K, logK, A, logA = P.create_transition_prob_1d(L, mv, 0.02, 0.03)
+    Ko, _, Ao, _ = O.create_transition_prob_1d(L, mv, 0.02, 0.03)
+    np.testing.assert_allclose(K, Ko, rtol=1e-12)
+    np.testing.assert_allclose(tr.A, Ao)
+    i, j = np.meshgrid(np.arange(L), np.arange(L), indexing='ij')
+    d = np.abs(i - j)
+    Kb = np.where(d <= tr.band, tr.g[np.minimum(d, tr.band)].astype(np.float64) * tr.invz[:, None], 0.0)
+    np.testing.assert_allclose(Kb, np.where(d <= tr.band, K[0], 0.0), rtol=1e-6, atol=1e-37)
+    assert np.max(np.where(d > tr.band, K[0], 0.0)) < 1e-29   # truncated mass is negligible
+
+
+def test_band_limit_raises():
+    with pytest.raises(NotImplementedError):
+        banded_transition(512, 10.0)
+
+
+def test_constructor_and_api_without_gpu():
+    m = P.PoissonGPLVMJump1D(30, n_latent_bin=100, tuning_lengthscale=10.)
+    assert m.tuning_basis.shape == (100, 18)
+    assert m.params.shape == (18, 30)
+    lp, p = m.init_latent_posterior(50, 3)
+    np.testing.assert_allclose(np.exp(lp).sum(1), 1.0, rtol=1e-5)
+    lat = m.sample_latent(200, key=1)
+    assert lat.shape == (200, 2) and lat[:, 0].max() <= 1 and lat[:, 1].max() < 100
+    import inspect
+    sig = inspect.signature(m.fit_em)
+    for k in ['y', 'hyperparam', 'key', 'n_iter', 'log_posterior_init', 'ma_neuron', 'ma_latent',
+              'n_time_per_chunk', 'dt', 'likelihood_scale', 'save_every', 'm_step_step_size',
+              'm_step_maxiter', 'm_step_tol']:
+        assert k in sig.parameters
+    assert sig.parameters['n_iter'].default == 20 and sig.parameters['m_step_maxiter'].default == 1000
+    sig = inspect.signature(m.decode_latent)
+    assert list(sig.parameters)[:8] == ['y', 'tuning', 'hyperparam', 'ma_neuron', 'ma_latent',
+                                        'likelihood_scale', 'n_time_per_chunk', 't_l']
+
+
+def test_product_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    m = P.PoissonGPLVMJump1D(5, n_latent_bin=16, tuning_lengthscale=3.)
+    with pytest.raises(Exception):
+        m.fit_em(np.zeros((10, 5)), n_iter=1)
+
+
+def test_transition_posterior_key_order_matches_notebook():
+    lj = np.log(np.random.default_rng(0).random((2, 2, 5, 5)))
+    r = P.compute_transition_posterior_prob(lj)
+    assert list(r) == API['decode_keys_recorded'][7:]
+    ro = O.compute_transition_posterior_prob(lj)
+    for k in r:
+        np.testing.assert_allclose(r[k], ro[k], rtol=1e-5, atol=1e-7)
+
+
+def test_product_does_not_import_oracle():
+    import ast
+    import glob
+    pkg = os.path.join(os.path.dirname(HERE), 'poor_man_gplvm_amd')
+    for f in glob.glob(os.path.join(pkg, '*.py')):
+        tree = ast.parse(open(f).read())
+        for node in ast.walk(tree):
+            if isinstance(node, (ast.Import, ast.ImportFrom)):
+                names = [a.name for a in node.names] + ([node.module] if getattr(node, 'module', None) else [])
+                assert not any(n and n.split('.')[0] == 'oracle' for n in names), f
