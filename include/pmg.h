@@ -78,8 +78,8 @@ int pmg_tuning_softplus(const float* basis, const double* W, int32_t L, int32_t 
 /*   delta (T,L) f32 = ll - r[t, l/32],  rblk (T, Lp/32) f64 = max over   */
 /*   the 32-latent block (Lp = roundup(L,32)).                           */
 /* Integer path (flags == 0, 1-D or no mask): exact int8 MFMA            */
-/* (v_mfma_i32_32x32x32_i8) on y and log(lam) in 4 balanced base-256     */
-/* digits of a 2^-24 fixed point.  Generic path: f64.                    */
+/* (v_mfma_i32_32x32x32_i8) on y and log(lam) in 5 balanced base-256     */
+/* digits of a 2^-32 fixed point (5 digits).  Generic path: f64.         */
 size_t pmg_emission_workspace_size(int64_t T, int32_t L, int32_t N);
 int pmg_emission_poisson(const int8_t* yq, const double* gconst, const double* tuning64,
                          const float* ma_neuron_1d, const uint8_t* ma_latent, double dt,
@@ -153,6 +153,16 @@ size_t pmg_fwdbwd_repair_counter_offset(int64_t T, int32_t L, int32_t chunk);
 size_t pmg_suffstats_workspace_size(int64_t T, int32_t L, int32_t Np);
 int pmg_suffstats(const float* P, const float* yext, int64_t T, int32_t L, int32_t N, int32_t Np,
                   double* yw, double* tw, void* workspace, size_t workspace_bytes, void* stream);
+/* Same statistics on bf16 MFMA with exact products, for integer spikes   */
+/* 0..127 (pmg_spikes_prepare flags without PMG_YFLAG_NONINT): P is split */
+/* exactly as hi+mid+lo bf16 (3 x v_mfma_f32_32x32x16_bf16), y is exact.   */
+/* ybt = spikes transposed to bf16 [Np][Tp], Tp = round_up(T, 64), from    */
+/* pmg_spikes_bf16t (once per data set).  t_w is summed from P in f64.     */
+int pmg_spikes_bf16t(const float* yext, int64_t T, int32_t Np, uint16_t* ybt, int64_t Tp, void* stream);
+size_t pmg_suffstats_bf16_workspace_size(int64_t T, int32_t L, int32_t N);
+int pmg_suffstats_bf16(const float* P, const uint16_t* ybt, int64_t T, int64_t Tp, int32_t L, int32_t N,
+                       int32_t Np, double* yw, double* tw, void* workspace, size_t workspace_bytes,
+                       void* stream);
 /* P = exp(logp) elementwise (the first M-step's exp at fit_tuning_helper.py:38). */
 int pmg_exp(const float* logp, int64_t n, float* p, void* stream);
 /* out = log(x) elementwise (log-space outputs; log(0) = -inf). */

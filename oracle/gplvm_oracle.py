@@ -23,9 +23,15 @@ Every function cites the reference file:line it restates.  Arithmetic is
 float64 and follows the reference's log-domain formulation exactly (dense
 logsumexp over the full L x L kernels, joint accumulated with logaddexp) --
 this is also the algorithm the CPU baseline times.
+
+``working_precision(np.float32)`` runs the same restatement in float32, the
+reference's own arithmetic type (all arrays fp32, no x64 anywhere in the
+reference): a *reference-mimic* used by the tests to measure the reference's
+own rounding noise against the float64 answer.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 
 import numpy as np
@@ -44,6 +50,19 @@ __all__ = [
 
 NEG_MASK = -1e20          # decoder.py:46  masked latent log-likelihood
 RATE_EPS = 1e-20          # decoder.py:39, fit_tuning_helper.py:78
+
+_F = np.float64           # working precision of the restatement
+
+
+@contextlib.contextmanager
+def working_precision(dtype):
+    """Run the restatement in `dtype` (np.float32 = reference-mimic)."""
+    global _F
+    old, _F = _F, dtype
+    try:
+        yield
+    finally:
+        _F = old
 
 
 # ----------------------------------------------------------------------------
@@ -121,7 +140,7 @@ def sigmoid(x):
 
 def get_tuning_softplus(params, basis):
     """fit_tuning_helper.py:19-25: softplus(basis @ params) -> (L, N)."""
-    return softplus(np.asarray(basis, np.float64) @ np.asarray(params, np.float64))
+    return softplus(np.asarray(basis, _F) @ np.asarray(params, _F))
 
 
 # ----------------------------------------------------------------------------
@@ -131,12 +150,12 @@ def loglikelihood_poisson_all(y, tuning, ma_neuron=None, ma_latent=None, dt=1.0)
     """decoder.py:30-48 vmapped over time (decoder.py:60-71; :73-85 for a per-time dt).
     ll[t,l] = sum_n m[t,n] * (xlogy(y[t,n], lam[l,n]) - lam[l,n] - gammaln(y[t,n]+1)),
     lam = tuning*dt + 1e-20; ll[:, ~ma_latent] = -1e20."""
-    y = np.asarray(y, np.float64)
-    tuning = np.asarray(tuning, np.float64)
+    y = np.asarray(y, _F)
+    tuning = np.asarray(tuning, _F)
     T, N = y.shape
     L = tuning.shape[0]
-    m = np.ones((T, N)) if ma_neuron is None else np.broadcast_to(np.asarray(ma_neuron, np.float64), (T, N))
-    dt = np.broadcast_to(np.asarray(dt, np.float64), (T,))
+    m = np.ones((T, N), _F) if ma_neuron is None else np.broadcast_to(np.asarray(ma_neuron, _F), (T, N))
+    dt = np.broadcast_to(np.asarray(dt, _F), (T,))
     if np.all(dt == dt[0]):
         lam = tuning * dt[0] + RATE_EPS                                     # (L, N)
         loglam = np.log(lam)
@@ -145,7 +164,7 @@ def loglikelihood_poisson_all(y, tuning, ma_neuron=None, ma_latent=None, dt=1.0)
         # xlogy(0, lam) = 0 exactly; log(lam) is finite (lam >= 1e-20) so the
         # matrix form is identical.
     else:
-        ll = np.empty((T, L))
+        ll = np.empty((T, L), _F)
         g = gammaln(y + 1.0)
         for t in range(T):
             lam = tuning * dt[t] + RATE_EPS
@@ -175,12 +194,12 @@ def filter_all_step(ll, logK, logA, carry_init=None, likelihood_scale=1.0):
     "at t=-1" and zero log marginal (decoder.py:181-183)."""
     D, L = logA.shape[0], logK.shape[1]
     if carry_init is None:
-        carry_init = (np.log(np.ones((D, L)) / (D * L)), 0.0)
+        carry_init = (np.log(np.ones((D, L), _F) / (D * L)), 0.0)
     post, logz = carry_init
     T = ll.shape[0]
-    posts = np.empty((T, D, L))
-    priors = np.empty((T, D, L))
-    cs = np.empty(T)
+    posts = np.empty((T, D, L), _F)
+    priors = np.empty((T, D, L), _F)
+    cs = np.empty(T, _F)
     for t in range(T):
         post, logz, prior, c = filter_one_step(post, logz, ll[t], logK, logA, likelihood_scale)
         posts[t], priors[t], cs[t] = post, prior, c
@@ -213,14 +232,14 @@ def smooth_all_step(causal_post, causal_prior, logK, logA, carry_init=None, with
     if carry_init is None:
         do_concat = True
         acausal = causal_post[-1]
-        joint = np.full((D, D, L, L), -np.inf)
+        joint = np.full((D, D, L, L), -np.inf, _F)
         xs_post = causal_post[:-1]
     else:
         do_concat = False
         acausal, joint = carry_init
         xs_post = causal_post
     n = xs_post.shape[0]
-    out = np.empty((n, D, L))
+    out = np.empty((n, D, L), _F)
     for k in range(n - 1, -1, -1):                                          # scan(reverse=True) :248
         acausal, joint = smooth_one_step(acausal, joint, xs_post[k], causal_prior[k], logK, logA, with_joint)
         out[k] = acausal
@@ -242,7 +261,7 @@ def smooth_all_step_combined_ma_chunk(y, tuning, logK, logA, ma_neuron=None, ma_
     L = tuning.shape[0]
     if ma_latent is None:
         ma_latent = np.ones(L)
-    ma_neuron_arr = None if ma_neuron is None else np.asarray(ma_neuron, np.float64)
+    ma_neuron_arr = None if ma_neuron is None else np.asarray(ma_neuron, _F)
     carry = None
     posts, priors, cs, lls, slices = [], [], [], [], []
     for n in range(n_chunks):
@@ -294,8 +313,8 @@ def compute_transition_posterior_prob(log_joint):
 # ----------------------------------------------------------------------------
 def get_statistics(log_posterior_probs, y):
     """fit_tuning_helper.py:28-42: P = exp(logpost); y_w = P^T y (L,N); t_w = sum_t P (L)."""
-    P = np.exp(np.asarray(log_posterior_probs, np.float64))
-    return P.T @ np.asarray(y, np.float64), P.sum(0)
+    P = np.exp(np.asarray(log_posterior_probs, _F))
+    return P.T @ np.asarray(y, _F), P.sum(0)
 
 
 def poisson_m_step_objective(W, param_prior_std, basis, yw, tw):
@@ -319,7 +338,7 @@ def poisson_m_step_grad(W, param_prior_std, basis, yw, tw):
 
 def adam_init(W):
     """optax.adam(lr).init: ScaleByAdamState(count=0, mu=0, nu=0)."""
-    return {'count': 0, 'mu': np.zeros_like(W, dtype=np.float64), 'nu': np.zeros_like(W, dtype=np.float64)}
+    return {'count': 0, 'mu': np.zeros_like(W, dtype=_F), 'nu': np.zeros_like(W, dtype=_F)}
 
 
 def adam_update(g, state, W, lr, b1=0.9, b2=0.999, eps=1e-8, eps_root=0.0):
@@ -338,8 +357,8 @@ def adam_run(W, state, param_prior_std, basis, yw, tw, lr=0.01, maxiter=1000, to
     while i < maxiter-1 and (i < 5 or |loss-loss_prev|/max(|loss|,1e-8) > tol):
     (loss, g) at current W; W <- adam(W, g); history[i+1] = loss; loss_prev <- old loss.
     Returns n_iter = i+1 and final_loss = last evaluated loss (before the last update)."""
-    basis = np.asarray(basis, np.float64)
-    W = np.asarray(W, np.float64)
+    basis = np.asarray(basis, _F)
+    W = np.asarray(W, _F)
     loss = poisson_m_step_objective(W, param_prior_std, basis, yw, tw)
     g = poisson_m_step_grad(W, param_prior_std, basis, yw, tw)
     err = float(np.sqrt(np.sum(g * g)))
@@ -377,15 +396,16 @@ def fit_em(y, params, basis, log_posterior_init, n_iter=20, movement_variance=1.
            m_step_step_size=0.01, m_step_maxiter=1000, m_step_tol=1e-6, custom_kernel=None):
     """core.py:829-849 + core.py:592-713 with injected params / basis /
     log_posterior_init (JAX PRNG is not reproducible without JAX)."""
-    y = np.asarray(y, np.float64)
+    y = np.asarray(y, _F)
     L = basis.shape[0]
     if save_every is None:
         save_every = n_iter
     _, logK, _, logA = create_transition_prob_1d(L, movement_variance, p_move_to_jump, p_jump_to_move, custom_kernel)
+    logK, logA = logK.astype(_F), logA.astype(_F)
     opt_state = adam_init(params)                                          # core.py:847
-    W = np.asarray(params, np.float64)
-    basis = np.asarray(basis, np.float64)
-    logpost = np.asarray(log_posterior_init, np.float64)
+    W = np.asarray(params, _F)
+    basis = np.asarray(basis, _F)
+    logpost = np.asarray(log_posterior_init, _F)
     log_marginal_l, saved = [], {'log_posterior_all_saved': [], 'params_saved': [],
                                  'tuning_saved': [], 'iter_saved': [], 'log_marginal_saved': []}
     m_step_res_l = {}
@@ -427,8 +447,9 @@ def decode_latent(y, tuning, movement_variance=1.0, p_move_to_jump=0.01, p_jump_
     """core.py:454-497 (+ decoder.compute_transition_posterior_prob)."""
     L = tuning.shape[0]
     _, logK, _, logA = create_transition_prob_1d(L, movement_variance, p_move_to_jump, p_jump_to_move, custom_kernel)
+    logK, logA = logK.astype(_F), logA.astype(_F)
     lpa, logz, _, cs, joint, ll = smooth_all_step_combined_ma_chunk(
-        np.asarray(y, np.float64), np.asarray(tuning, np.float64), logK, logA, ma_neuron, ma_latent,
+        np.asarray(y, _F), np.asarray(tuning, _F), logK, logA, ma_neuron, ma_latent,
         likelihood_scale, n_time_per_chunk, with_joint=True)
     post = np.exp(lpa)
     res = {'log_posterior_all': lpa, 'log_marginal_final': float(logz), 'posterior_all': post,
@@ -440,9 +461,9 @@ def decode_latent(y, tuning, movement_variance=1.0, p_move_to_jump=0.01, p_jump_
 
 def naive_bayes_chunk(y, tuning, ma_neuron=None, ma_latent=None, dt_l=1.0, n_time_per_chunk=10000):
     """decoder.py:88-149: per-time emission (dt per row), row-normalised."""
-    y = np.asarray(y, np.float64)
+    y = np.asarray(y, _F)
     T = y.shape[0]
-    dt_l = np.broadcast_to(np.asarray(dt_l, np.float64), (T,))
+    dt_l = np.broadcast_to(np.asarray(dt_l, _F), (T,))
     ll = loglikelihood_poisson_all(y, tuning, ma_neuron, ma_latent, dt_l)
     lm = logsumexp(ll, axis=-1, keepdims=True)
     return ll - lm, lm[:, 0], float(lm.sum()), ll

@@ -26,6 +26,7 @@ EXPORTED_SYMBOLS = (
     "pmg_emission_rowref", "pmg_loglik_materialize", "pmg_fwdbwd_workspace_size",
     "pmg_forward_filter", "pmg_backward_smoother", "pmg_fwdbwd_repair_counter_offset",
     "pmg_suffstats_workspace_size", "pmg_suffstats", "pmg_exp", "pmg_log",
+    "pmg_spikes_bf16t", "pmg_suffstats_bf16_workspace_size", "pmg_suffstats_bf16",
     "pmg_mstep_workspace_size", "pmg_mstep_adam", "pmg_joint_workspace_size",
     "pmg_joint_accumulate",
 )
@@ -74,6 +75,9 @@ _SIGS = {
     "pmg_fwdbwd_repair_counter_offset": ([_I64, _I32, _I32], _SZ),
     "pmg_suffstats_workspace_size": ([_I64, _I32, _I32], _SZ),
     "pmg_suffstats": ([_P, _P, _I64, _I32, _I32, _I32, _P, _P, _P, _SZ, _P], _I32),
+    "pmg_spikes_bf16t": ([_P, _I64, _I32, _P, _I64, _P], _I32),
+    "pmg_suffstats_bf16_workspace_size": ([_I64, _I32, _I32], _SZ),
+    "pmg_suffstats_bf16": ([_P, _P, _I64, _I64, _I32, _I32, _I32, _P, _P, _P, _SZ, _P], _I32),
     "pmg_exp": ([_P, _I64, _P, _P], _I32),
     "pmg_log": ([_P, _I64, _P, _P], _I32),
     "pmg_mstep_workspace_size": ([_I32, _I32], _SZ),

@@ -198,11 +198,12 @@ class PoissonGPLVMJump1D:
         gamma = torch.empty((T, 2, L), dtype=torch.float32, device=dev)
         rho = torch.zeros((T, 2, L), dtype=torch.float32, device=dev) if joint else None
         eng.e_step(likelihood_scale, logz, gamma=gamma, rho=rho)
+        ml = None if ma_latent is None else np.asarray(ma_latent).astype(bool)
         out = {
-            'log_posterior_all': _np(log_of(gamma)),
+            'log_posterior_all': _masked_log(_np(log_of(gamma)), ml),
             'log_marginal_final': float(_np(logz)[0]),
             'posterior_all': _np(gamma),
-            'log_causal_posterior_all': _np(log_of(eng.alpha)),
+            'log_causal_posterior_all': _masked_log(_np(log_of(eng.alpha)), ml),
             'log_one_step_predictive_marginals_all': _np(eng.logc).astype(np.float32),
             'log_likelihood_all': _np(eng.loglik()),
         }
@@ -213,8 +214,7 @@ class PoissonGPLVMJump1D:
             logK = np.asarray(logK, np.float64)
             logA = np.asarray(logA, np.float64)
             S4 = S.reshape(2, L, 2, L).transpose(0, 2, 1, 3)          # [d, d', i, j]
-            with np.errstate(divide='ignore'):
-                lj = logA[:, :, None, None] + logK[None, :, :, :] + np.log(np.maximum(S4, 0.0))
+            lj = log_joint_from_counts(S4, logK, logA, ml)
             out['log_accumulated_joint'] = lj
         return out
 
@@ -363,6 +363,32 @@ class PoissonGPLVMJump1D:
         self.__dict__.update(state)
 
 
+def log_joint_from_counts(S4, logK, logA, ml=None):
+    """log accumulated joint [d, d', i, j] = logA + logK + log S, where S = sum_t
+    alpha_t (x) rho_{t+1} is the device's linear-space joint count (decoder.py:215-221
+    accumulates the same quantity with logaddexp)."""
+    S4 = np.asarray(S4, np.float64)
+    with np.errstate(divide='ignore'):
+        logS = np.log(np.maximum(S4, 0.0))
+    if ml is not None and not ml.all():
+        # decoder.py:215 in log space carries ll = -1e20 (core.py:59-60) into every
+        # joint entry that starts or ends in a masked latent; those entries are exact
+        # zeros of S here.  Restore the sentinel sums so normalised transition rows
+        # match the reference's arithmetic.
+        nm = (~ml).astype(np.float64)
+        sent = -1e20 * (nm[:, None] + nm[None, :])
+        logS = np.where((S4 == 0.0) & (sent < 0.0), sent[None, None], logS)
+    return np.asarray(logA, np.float64)[:, :, None, None] + np.asarray(logK, np.float64)[None] + logS
+
+
+def _masked_log(logp, ml):
+    """Masked latents carry ll = -1e20 in the reference (core.py:59-60), so their
+    log posteriors are -1e20 (absorbed in float32), not log(0) = -inf."""
+    if ml is not None and not ml.all():
+        logp[..., ~ml] = np.float32(-1e20)
+    return logp
+
+
 def compute_transition_posterior_prob(log_accumulated_joint_total):
     """decoder.py:334-375 on the host (f64), keys in jax's sorted pytree order."""
     from scipy.special import logsumexp
@@ -398,6 +424,7 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
     eng = DeviceEM(sp, L, basis=B, scan=scan)
     eng.set_transition(transition)
     eng.set_ma_latent(ma_latent)
+    mlat = None if ma_latent is None else np.asarray(ma_latent).astype(bool)
     eng.set_log_posterior(log_posterior_init)
     dev = eng.dev
     W = torch.as_tensor(np.asarray(params, np.float64), device=dev).contiguous()
@@ -426,7 +453,7 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
         want_gamma = (i == n_iter - 1) or (i % save_every == 0)
         eng.e_step(likelihood_scale, logz[i:i + 1], gamma=gamma if want_gamma else None)
         if i % save_every == 0:
-            saved['log_posterior_all_saved'].append(_np(log_of(gamma)))
+            saved['log_posterior_all_saved'].append(_masked_log(_np(log_of(gamma)), mlat))
             saved['params_saved'].append(_np(W).astype(np.float32))
             saved['tuning_saved'].append(_np(eng.tuning32))
             saved['iter_saved'].append(i)
@@ -455,7 +482,7 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
            'iter_saved': saved['iter_saved'],
            'params': _np(W).astype(np.float32),
            'tuning': _np(eng.tuning32),
-           'log_posterior_final': _np(log_of(gamma)),
+           'log_posterior_final': _masked_log(_np(log_of(gamma)), mlat),
            'log_marginal': float(lz[n_iter - 1]) if n_iter else float('nan'),
            'log_marginal_l': [float(v) for v in lz[:n_iter]],
            'log_marginal_saved': saved['log_marginal_saved'],

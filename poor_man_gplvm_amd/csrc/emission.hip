@@ -10,11 +10,12 @@
 // Precision: the posterior depends on differences ll[t,l]-ll[t,l'] of sums of ~N
 // terms of size O(1-10); fp32 accumulation would cost ~1e-5 absolute.  The fast
 // path is therefore EXACT integer arithmetic: y (0..127) as int8 and log(lam) as a
-// 2^-24 fixed-point number split into 4 balanced base-256 int8 digits; the digit
+// 2^-32 fixed-point number split into 5 balanced base-256 int8 digits; the digit
 // GEMMs run on v_mfma_i32_32x32x32_i8 with exact int32 accumulation and are
-// recombined in int64 (quantisation error <= 2^-25 per log(lam)).  Anything the
-// integer path cannot represent (non-integer / >127 counts, weighted or 2-D masks)
-// goes through the f64 kernel at the bottom.
+// recombined in int64 (quantisation error <= 2^-33 per log(lam), i.e. ll exact to
+// ~1e-9 for any realistic spike count).  Anything the integer path cannot represent
+// (non-integer / >127 counts, weighted or 2-D masks) goes through the f64 kernel at
+// the bottom.
 //
 // Output format (both paths): delta[t,l] = f32(ll[t,l] - r[t,b]) with
 // r[t,b] = max over the 32-latent block b (f64), so an fp32 consumer recovers
@@ -26,10 +27,11 @@ namespace pmg {
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-constexpr double kQScale = 16777216.0;  // 2^24
-constexpr double kQInv = 1.0 / 16777216.0;
+constexpr int kDig = 5;
+constexpr double kQScale = 4294967296.0;  // 2^32
+constexpr double kQInv = 1.0 / 4294967296.0;
 
-// One wave per latent row: log(lam) -> 4 int8 digits, lamsum = sum_n m_n lam.
+// One wave per latent row: log(lam) -> 5 int8 digits, lamsum = sum_n m_n lam.
 __global__ void __launch_bounds__(256) k_rates_prepare(
     const double* __restrict__ tuning, int L, int N, const float* __restrict__ ma, double dt,
     int Lp, int Kp, int8_t* __restrict__ qd, double* __restrict__ lamsum, int* __restrict__ bad) {
@@ -40,30 +42,25 @@ __global__ void __launch_bounds__(256) k_rates_prepare(
   double ls = 0.0;
   int flag = 0;
   for (int n = lane; n < Kp; n += 64) {
-    int8_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+    int8_t dg[kDig] = {0, 0, 0, 0, 0};
     if (l < L && n < N) {
       const double lam = tuning[(size_t)l * N + n] * dt + 1e-20;
       const double lg = log(lam);
       if (!(fabs(lg) < 60.0)) flag = 1;
       long long q = llrint(lg * kQScale);
-      long long r0 = ((q + 128) & 255) - 128;
-      q = (q - r0) >> 8;
-      long long r1 = ((q + 128) & 255) - 128;
-      q = (q - r1) >> 8;
-      long long r2 = ((q + 128) & 255) - 128;
-      q = (q - r2) >> 8;
-      d0 = (int8_t)r0;
-      d1 = (int8_t)r1;
-      d2 = (int8_t)r2;
-      d3 = (int8_t)q;  // |q| <= 64 for |lg| < 60
+#pragma unroll
+      for (int d = 0; d < kDig - 1; ++d) {
+        const long long rr = ((q + 128) & 255) - 128;
+        dg[d] = (int8_t)rr;
+        q = (q - rr) >> 8;
+      }
+      dg[kDig - 1] = (int8_t)q;  // |q| <= 61 for |lg| < 60
       const float m = ma ? ma[n] : 1.f;
       ls += (double)m * lam;
     }
     const size_t o = (size_t)l * Kp + n;
-    qd[o] = d0;
-    qd[plane + o] = d1;
-    qd[2 * plane + o] = d2;
-    qd[3 * plane + o] = d3;
+#pragma unroll
+    for (int d = 0; d < kDig; ++d) qd[d * plane + o] = dg[d];
   }
   ls = wave_sum_f64(ls);
   if (lane == 0) lamsum[l] = ls;
@@ -72,76 +69,128 @@ __global__ void __launch_bounds__(256) k_rates_prepare(
   }
 }
 
-// Wave tile: 32 latents (MFMA rows, A = digits of log lam) x 64 time bins
-// (2 x 32 MFMA columns, B = y^T) x 4 digits: 8 v16i accumulators.
-// A fragment: lane (r = lane&31, h = lane>>5) holds A[row r][k0+16h .. +15];
-// B fragment: lane holds B[k0+16h .. +15][col r].  The same (h, element) -> k
-// assignment on both operands makes the K pairing consistent.
-// C/D: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*h  (cdna_hip_programming §3).
-__global__ void __launch_bounds__(256) k_emission_i8(
+// Workgroup tile 128 time bins x 64 latents, 4 waves as 2 (time) x 2 (latent); each
+// wave owns 64 t x 32 l for all 5 digits (2 x 5 v16i accumulators).  MFMA operand A =
+// y (rows = time), B = digits (cols = latent), so C[t][l] rows leave as 128-byte
+// coalesced stores.  K (neurons) advances in 64-byte chunks staged through
+// double-buffered LDS (rows of 80 B: the 16-byte fragment reads of 16 consecutive
+// rows hit distinct bank quads).
+// Fragment map (i8 32x32x32): lane (r = lane&31, h = lane>>5) supplies
+// A[row r][k = 16h .. 16h+15] and B[k = 16h ..][col r]; the same (h, byte) -> k
+// assignment on both operands keeps the K pairing consistent.
+// C/D: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*h.
+constexpr int ET = 128, EL = 64, EKC = 64, EROW = EKC + 16;
+
+__device__ __forceinline__ int xcd_group(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+__global__ void __launch_bounds__(256, 2) k_emission_i8(
     const int8_t* __restrict__ yq, const int8_t* __restrict__ qd,
     const double* __restrict__ lamsum, const double* __restrict__ gconst,
-    const uint8_t* __restrict__ ma_latent, int64_t T, int L, int Lp, int Kp, int nLB,
-    int64_t nTB, float* __restrict__ delta, double* __restrict__ rblk) {
-  const int lane = threadIdx.x & 63;
-  const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (w >= (int64_t)nLB * nTB) return;
-  const int lb = (int)(w % nLB);
-  const int64_t tb = w / nLB;
+    const uint8_t* __restrict__ ma_latent, int64_t T, int64_t Tp, int L, int Lp, int Kp, int nLT,
+    float* __restrict__ delta, double* __restrict__ rblk) {
+  __shared__ __attribute__((aligned(16))) int8_t sY[2][ET][EROW];
+  __shared__ __attribute__((aligned(16))) int8_t sQ[2][kDig][EL][EROW];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int lb = xcd_group(blockIdx.x, gridDim.x);   // l-tiles of one t-tile share an XCD
+  const int lt = lb % nLT;
+  const int64_t tt = lb / nLT;
+  const int64_t t0 = tt * ET;
+  const int l0 = lt * EL;
   const int r = lane & 31, h = lane >> 5;
+  const int wt = wid & 1, wl = wid >> 1;
   const size_t plane = (size_t)Lp * Kp;
 
-  const int8_t* a_ptr = qd + (size_t)(lb * 32 + r) * Kp + 16 * h;
-  const int8_t* b_ptr0 = yq + (size_t)(tb * 64 + r) * Kp + 16 * h;
-  const int8_t* b_ptr1 = b_ptr0 + (size_t)32 * Kp;
-
-  v16i acc[4][2];
+  // staging map: Y 128 rows x 4 x 16 B (2 per thread), Q 5 x 64 rows x 4 x 16 B (5 per thread)
+  uint4 ry[2], rq[kDig];
+  auto load_chunk = [&](int k0) {
 #pragma unroll
-  for (int d = 0; d < 4; ++d) {
+    for (int q = 0; q < 2; ++q) {
+      const int e = tid + 256 * q;
+      const int row = e >> 2, c = (e & 3) * 16;
+      const int64_t t = t0 + row;
+      ry[q] = (t < Tp && k0 + c < Kp) ? *reinterpret_cast<const uint4*>(yq + t * Kp + k0 + c)
+                                       : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int d = 0; d < kDig; ++d) {
+      const int row = tid >> 2, c = (tid & 3) * 16;
+      const int l = l0 + row;
+      rq[d] = (l < Lp && k0 + c < Kp)
+                  ? *reinterpret_cast<const uint4*>(qd + d * plane + (size_t)l * Kp + k0 + c)
+                  : make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  auto store_chunk = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int e = tid + 256 * q;
+      *reinterpret_cast<uint4*>(&sY[buf][e >> 2][(e & 3) * 16]) = ry[q];
+    }
+#pragma unroll
+    for (int d = 0; d < kDig; ++d)
+      *reinterpret_cast<uint4*>(&sQ[buf][d][tid >> 2][(tid & 3) * 16]) = rq[d];
+  };
+
+  v16i acc[kDig][2];
+#pragma unroll
+  for (int d = 0; d < kDig; ++d) {
     acc[d][0] = (v16i){0};
     acc[d][1] = (v16i){0};
   }
-  for (int k0 = 0; k0 < Kp; k0 += 32) {
-    const v4i b0 = *reinterpret_cast<const v4i*>(b_ptr0 + k0);
-    const v4i b1 = *reinterpret_cast<const v4i*>(b_ptr1 + k0);
+  const int nch = (Kp + EKC - 1) / EKC;
+  load_chunk(0);
+  store_chunk(0);
+  __syncthreads();
+  for (int ch = 0; ch < nch; ++ch) {
+    const int buf = ch & 1;
+    if (ch + 1 < nch) load_chunk((ch + 1) * EKC);   // in flight during the MFMAs
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      const v4i a = *reinterpret_cast<const v4i*>(a_ptr + d * plane + k0);
-      acc[d][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b0, acc[d][0], 0, 0, 0);
-      acc[d][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b1, acc[d][1], 0, 0, 0);
+    for (int ks = 0; ks < EKC; ks += 32) {
+      const v4i a0 = *reinterpret_cast<const v4i*>(&sY[buf][wt * 64 + r][ks + 16 * h]);
+      const v4i a1 = *reinterpret_cast<const v4i*>(&sY[buf][wt * 64 + 32 + r][ks + 16 * h]);
+#pragma unroll
+      for (int d = 0; d < kDig; ++d) {
+        const v4i b = *reinterpret_cast<const v4i*>(&sQ[buf][d][wl * 32 + r][ks + 16 * h]);
+        acc[d][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b, acc[d][0], 0, 0, 0);
+        acc[d][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b, acc[d][1], 0, 0, 0);
+      }
+    }
+    if (ch + 1 < nch) {
+      store_chunk(buf ^ 1);   // the other buffer was last read one iteration ago
+      __syncthreads();
     }
   }
 
+  // epilogue: int64 recombination, f64 ll, 32-latent block max, coalesced rows
   const int nblk = Lp >> 5;
+  const int l = l0 + wl * 32 + r;
+  const int blk = (l0 >> 5) + wl;
+  const bool lvalid = l < L;
+  const bool lmask = lvalid && ma_latent && ma_latent[l] == 0;
+  const double lsum = (l < Lp) ? lamsum[l] : 0.0;
+  if (blk >= nblk) return;
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    const int64_t t = tb * 64 + s * 32 + r;
-    const bool tvalid = t < T;
-    const double gc = tvalid ? gconst[t] : 0.0;
-    double ll[16];
-    double mx = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int l = lb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-      long long q = (long long)acc[0][s][i] + ((long long)acc[1][s][i] << 8) +
-                    ((long long)acc[2][s][i] << 16) + ((long long)acc[3][s][i] << 24);
-      double v = (double)q * kQInv - lamsum[l] - gc;
-      if (l < L) {
-        if (ma_latent && ma_latent[l] == 0) v = -1e20;
-        mx = fmax(mx, v);
-      } else {
-        v = -INFINITY;
-      }
-      ll[i] = v;
-    }
-    mx = fmax(mx, __shfl_xor(mx, 32, 64));
-    if (tvalid) {
-      if (h == 0) rblk[t * nblk + lb] = mx;
-      float* drow = delta + t * (int64_t)L;
+      const int64_t t = t0 + wt * 64 + s * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+      long long q = (long long)acc[0][s][i];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int l = lb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-        if (l < L) drow[l] = (float)(ll[i] - mx);
+      for (int d = 1; d < kDig; ++d) q += (long long)acc[d][s][i] << (8 * d);
+      const bool tvalid = t < T;
+      double v = -INFINITY;
+      if (lvalid) v = lmask ? -1e20 : (double)q * kQInv - lsum - (tvalid ? gconst[t] : 0.0);
+      float mf = (float)v;
+#pragma unroll
+      for (int o = 16; o >= 1; o >>= 1) mf = fmaxf(mf, __shfl_xor(mf, o, 32));
+      const double mx = (double)mf;
+      if (tvalid) {
+        if (r == 0) rblk[t * nblk + blk] = mx;
+        if (lvalid) delta[t * (int64_t)L + l] = (float)(v - mx);
       }
     }
   }
@@ -229,7 +278,7 @@ size_t pmg_emission_workspace_size(int64_t T, int32_t L, int32_t N) {
   (void)T;
   const int64_t Lp = round_up(L, 32), Kp = round_up(N, 32);
   Carver c(nullptr);
-  c.take<int8_t>(4 * Lp * Kp);
+  c.take<int8_t>(kDig * Lp * Kp);
   c.take<double>(Lp);
   c.take<int>(4);
   return c.off + 256;
@@ -247,18 +296,18 @@ int pmg_emission_poisson(const int8_t* yq, const double* gconst, const double* t
   hipStream_t st = as_stream(stream);
   const int Lp = (int)round_up(L, 32);
   Carver c(workspace);
-  int8_t* qd = c.take<int8_t>(4 * (size_t)Lp * Kp);
+  int8_t* qd = c.take<int8_t>(kDig * (size_t)Lp * Kp);
   double* lamsum = c.take<double>(Lp);
   int* bad = c.take<int>(4);
   PMG_HIP(hipMemsetAsync(bad, 0, sizeof(int), st));
   hipLaunchKernelGGL(k_rates_prepare, dim3((Lp + 3) / 4), dim3(256), 0, st, tuning64, L, N,
                      ma_neuron_1d, dt, Lp, Kp, qd, lamsum, bad);
   PMG_LAUNCH_CHECK();
-  const int nLB = Lp / 32;
-  const int64_t nTB = (T + 63) / 64;
-  const int64_t waves = nLB * nTB;
-  hipLaunchKernelGGL(k_emission_i8, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, yq,
-                     qd, lamsum, gconst, ma_latent, T, L, Lp, Kp, nLB, nTB, delta, rblk);
+  const int nLT = (Lp + EL - 1) / EL;
+  const int64_t nTT = (T + ET - 1) / ET;
+  const int64_t Tp = round_up(T, 64);   // rows of yq (pmg_spikes_prepare zero-pads to Tp)
+  hipLaunchKernelGGL(k_emission_i8, dim3((unsigned)(nLT * nTT)), dim3(256), 0, st, yq, qd, lamsum,
+                     gconst, ma_latent, T, Tp, L, Lp, Kp, nLT, delta, rblk);
   PMG_LAUNCH_CHECK();
   return PMG_OK;
 }

@@ -114,7 +114,7 @@ __device__ __forceinline__ void em_load(const FBParams& p, int64_t t, int j0, Em
 template <int J>
 __device__ __forceinline__ void em_exp(const FBParams& p, int j0, const EmRaw<J>& r, float e[J]) {
 #pragma unroll
-  for (int j = 0; j < J; ++j) e[j] = (j0 + j < p.L) ? __expf(fmaf(p.s, r.d[j], r.ph)) : 0.f;
+  for (int j = 0; j < J; ++j) e[j] = (j0 + j < p.L) ? exp_acc(fmaf(p.s, r.d[j], r.ph)) : 0.f;
 }
 
 // out[j] = sum_{k=-WP..WP} g[|k|] * in[j+k]  over the whole latent line (zero halo)

@@ -168,8 +168,8 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
   constexpr int NBR = BS::NBR, NBL = BS::NBL, STRIDE = BS::STRIDE;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sBl = smem;                                   // [kThreads][STRIDE]
-  float* sW = sBl + kThreads * STRIDE;                 // [NBM][4] current W (f32)
-  float* sRed = sW + NBM * kSMax;                      // [8 waves][NBM][4] partial B^T G
+  double* sW = reinterpret_cast<double*>(sBl + kThreads * STRIDE);  // [NBM][4] current W (f64)
+  float* sRed = reinterpret_cast<float*>(sW + NBM * kSMax);         // [8 waves][NBM][4] partial B^T G
   double* sSum = reinterpret_cast<double*>(sRed + (kThreads / 64) * NBM * kSMax);  // [2][8]
   double* sYw = sSum + 2 * (kThreads / 64);                                         // [kThreads][4]
   int* sCtl = reinterpret_cast<int*>(sYw + kThreads * kSMax);                       // [4]
@@ -199,7 +199,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
   const float twf = (float)twd;
   const int ek = tid % NB, en = tid / NB;
   const bool is_el = en < S;
-  for (int q = tid; q < NBM * kSMax; q += blockDim.x) sW[q] = 0.f;
+  for (int q = tid; q < NBM * kSMax; q += blockDim.x) sW[q] = 0.0;
   if (tid < 4) sCtl[tid] = 0;
   // element state (W, mu, nu) of this thread's weight, and its global ring
   double w_cur = 0.0, mu_cur = 0.0, nu_cur = 0.0;
@@ -211,7 +211,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
     w_cur = p.W[o];
     mu_cur = p.mu[o];
     nu_cur = p.nu[o];
-    sW[e] = (float)w_cur;
+    sW[e] = w_cur;
     ring[(0 * 3 + 0) * NBM * kSMax + e] = w_cur;
     ring[(0 * 3 + 1) * NBM * kSMax + e] = mu_cur;
     ring[(0 * 3 + 2) * NBM * kSMax + e] = nu_cur;
@@ -235,24 +235,34 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
     // neurons one at a time (runtime loop, not unrolled: one neuron's registers live)
 #pragma unroll 1
     for (int s = 0; s < S; ++s) {
-      float F = 0.f;
+      // F = B W in f64 (f32 basis x f64 weights): the gradient factor
+      // (y_w/f - t_w) cancels near the optimum, so f must be f64-accurate.
+      double F = 0.0;
 #pragma unroll
-      for (int q = 0; q < NBR; ++q) F = fmaf(brow[q], sW[q * kSMax + s], F);
-#pragma unroll
+      for (int q = 0; q < NBR; ++q) {
+        asm volatile("" : "+v"(brow[q]));   // keep the f32->f64 conversion local (no hoisted f64 copy)
+        F = fma((double)brow[q], sW[q * kSMax + s], F);
+      }
+#pragma unroll 2
       for (int q4 = 0; q4 < NBL; q4 += 4) {
         const float4 b4 = *reinterpret_cast<const float4*>(&sBl[tid * STRIDE + q4]);
-        F = fmaf(b4.x, sW[(NBR + q4) * kSMax + s], F);
-        F = fmaf(b4.y, sW[(NBR + q4 + 1) * kSMax + s], F);
-        F = fmaf(b4.z, sW[(NBR + q4 + 2) * kSMax + s], F);
-        F = fmaf(b4.w, sW[(NBR + q4 + 3) * kSMax + s], F);
+        F = fma((double)b4.x, sW[(NBR + q4) * kSMax + s], F);
+        F = fma((double)b4.y, sW[(NBR + q4 + 1) * kSMax + s], F);
+        F = fma((double)b4.z, sW[(NBR + q4 + 2) * kSMax + s], F);
+        F = fma((double)b4.w, sW[(NBR + q4 + 3) * kSMax + s], F);
       }
       const double ywd = is_row ? sYw[tid * kSMax + s] : 0.0;
-      const float f = softplus_f(F);
-      const float sg = sigmoid_f(F);
-      const float gr = is_row ? ((float)ywd / (f + 1e-20f) - twf) * sg : 0.f;
+      // softplus / sigmoid in f32 at Fh = f32(F), corrected to first order in the
+      // exact residual r = F - Fh (|r| <= 2^-24 |F|): f = softplus(Fh) + sigmoid(Fh) r
+      const float Fh = (float)F;
+      const double r = F - (double)Fh;
+      const float f32 = fmaxf(Fh, 0.f) + log1pf(expf(-fabsf(Fh)));
+      const float sg = 1.f / (1.f + expf(-Fh));
+      const double fd = (double)f32 + (double)sg * r;
+      const float gr = is_row ? (float)((ywd / (fd + 1e-20) - twd) * (double)sg) : 0.f;
       if (is_row) {
-        const double xl = (ywd != 0.0) ? ywd * (double)__logf(f + 1e-20f) : 0.0;
-        lpart -= xl - (double)f * twd;
+        const double xl = (ywd != 0.0) ? ywd * ((double)logf(f32 + 1e-20f) + (double)sg * r / (double)f32) : 0.0;
+        lpart -= xl - fd * twd;
       }
       // per-wave partial of B^T G for this neuron, 32 columns per chunk
       float* sr = &sRed[(wid * NBM) * kSMax] + s;
@@ -300,7 +310,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
       ring[(ns * 3 + 0) * NBM * kSMax + e] = w_cur;
       ring[(ns * 3 + 1) * NBM * kSMax + e] = mu_cur;
       ring[(ns * 3 + 2) * NBM * kSMax + e] = nu_cur;
-      sW[e] = (float)w_cur;
+      sW[e] = w_cur;
     }
     lpart = wave_sum_f64(lpart);
     gsq = wave_sum_f64(gsq);
@@ -417,7 +427,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
 template <int NBM>
 static size_t adam_lds_bytes() {
   using BS = BasisSplit<NBM>;
-  return sizeof(float) * ((size_t)kThreads * BS::STRIDE + NBM * kSMax +
+  return sizeof(float) * ((size_t)kThreads * BS::STRIDE + 2 * NBM * kSMax +
                           (kThreads / 64) * NBM * kSMax) +
          sizeof(double) * (2 * (kThreads / 64) + kThreads * kSMax) + sizeof(int) * 4 + 64;
 }

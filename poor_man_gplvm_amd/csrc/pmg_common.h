@@ -98,6 +98,19 @@ __device__ __forceinline__ void wave_sum2(float& a, float& b) {
   b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(b), 63));
 }
 
+// exp(x) to ~1 ulp: 2^(x log2 e) with the rounding error of the f32 product x*log2e
+// (and log2e's own f32 residual) restored to first order; __expf drops that error,
+// ~|x| * 6e-8 relative, which matters for |x| of a few units.
+__device__ __forceinline__ float exp_acc(float x) {
+  constexpr float kL2E = 1.44269502162933349609375f;   // f32(log2 e)
+  constexpr float kL2E_lo = 1.925963033500011e-08f;    // log2 e - kL2E
+  const float y = x * kL2E;
+  float err = fmaf(x, kL2E, -y);
+  err = fmaf(x, kL2E_lo, err);
+  const float r = __builtin_amdgcn_exp2f(y);
+  return fmaf(r, err * 0.693147180559945309f, r);
+}
+
 __device__ __forceinline__ float wave_max(float v) {
   v = fmaxf(v, dppf<0xB1>(v));
   v = fmaxf(v, dppf<0x4E>(v));

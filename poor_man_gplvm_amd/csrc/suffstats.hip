@@ -199,6 +199,225 @@ static int atb_run(const float* A, int64_t lda, int Mdim, const float* B, int64_
   return PMG_OK;
 }
 
+
+// ---------------------------------------------------------------------------------
+// Sufficient statistics on bf16 MFMA, exact products (integer spikes 0..127).
+//
+// y is an integer <= 127, exact in bf16.  P (f32) is split by truncation into
+// P = hi + mid + lo with each part exact in bf16 (hi takes the top 8 significant
+// bits, mid the next 8, lo the last 8; both remainders are exact in f32), so
+// y_w = sum_t (hi + mid + lo) y is three v_mfma_f32_32x32x16_bf16 per tile whose
+// products are exact; accumulation is f32 inside a 128-step segment and f64 across
+// segments (same as the f32 path), at the bf16 MFMA rate instead of the f32 one.
+//
+// Operand layout: lane (r, h) of the 32x32x16 MFMA holds A[m=r][t=8h..8h+7] and
+// B[t=8h..8h+7][n=r], i.e. 8 consecutive TIME steps.  P is time-major, so the
+// transpose happens on the LDS write (each thread gathers 32 time rows of one m
+// column with coalesced dword loads and writes 16-byte runs of its LDS row); the
+// spikes are pre-transposed once per data set to bf16 [Np][Tp].
+// LDS rows are 64 + 8 bf16 (144 B): the 16-byte reads/writes of 16 consecutive
+// rows land on distinct bank quads.
+// ---------------------------------------------------------------------------------
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+constexpr int KB3 = 64, ROW3 = KB3 + 8;
+
+__device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32_t& l) {
+  const uint32_t u = __float_as_uint(x);
+  h = u >> 16;
+  const float r1 = x - __uint_as_float(u & 0xFFFF0000u);
+  const uint32_t u1 = __float_as_uint(r1);
+  m = u1 >> 16;
+  const float r2 = r1 - __uint_as_float(u1 & 0xFFFF0000u);
+  l = __float_as_uint(r2) >> 16;
+}
+
+// bijective XCD-grouping of workgroup ids (consecutive logical ids share an XCD)
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+__global__ void __launch_bounds__(256) k_ptb3(const float* __restrict__ P, int L,
+                                              const uint16_t* __restrict__ Ybt, int64_t Tp, int Np,
+                                              int64_t K, int64_t KT, int nMT, int nNT, int nKS,
+                                              int Mp, int Npd, double* __restrict__ part,
+                                              double* __restrict__ twpart) {
+  __shared__ __attribute__((aligned(16))) uint16_t sA[3][TM][ROW3];
+  __shared__ __attribute__((aligned(16))) uint16_t sB[TN][ROW3];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = lb % nMT;
+  const int nt = (lb / nMT) % nNT;
+  const int ks = lb / (nMT * nNT);
+  const int wm = wid & 1, wn = wid >> 1;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t kb = (int64_t)ks * KT;
+  const int64_t ke = kb + KT < K ? kb + KT : K;
+
+  // staging: A column m_l = tid & 127, time rows 32*tg .. 32*tg+31 of the K-tile;
+  // B row n_l = tid >> 1, time half hb = tid & 1 (32 bf16 = 4 x 16 B)
+  const int m_l = tid & 127, tg = tid >> 7;
+  const int n_l = tid >> 1, hb = tid & 1;
+  const int mg = mt * TM + m_l;
+  const int ng = nt * TN + n_l;
+  float ra[32];
+  uint4 rb[4];
+  auto load_tile = [&](int64_t t0) {
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const int64_t t = t0 + 32 * tg + i;
+      ra[i] = (t < ke && mg < L) ? P[t * L + mg] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      rb[q] = ng < Np ? *reinterpret_cast<const uint4*>(Ybt + (size_t)ng * Tp + t0 + 32 * hb + 8 * q)
+                      : make_uint4(0u, 0u, 0u, 0u);
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t hw[4], mw[4], lw[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint32_t h0, m0, l0, h1, m1, l1;
+        split3(ra[8 * q + 2 * j], h0, m0, l0);
+        split3(ra[8 * q + 2 * j + 1], h1, m1, l1);
+        hw[j] = h0 | (h1 << 16);
+        mw[j] = m0 | (m1 << 16);
+        lw[j] = l0 | (l1 << 16);
+      }
+      const int c = 32 * tg + 8 * q;
+      *reinterpret_cast<uint4*>(&sA[0][m_l][c]) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+      *reinterpret_cast<uint4*>(&sA[1][m_l][c]) = make_uint4(mw[0], mw[1], mw[2], mw[3]);
+      *reinterpret_cast<uint4*>(&sA[2][m_l][c]) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+      *reinterpret_cast<uint4*>(&sB[n_l][32 * hb + 8 * q]) = rb[q];
+    }
+  };
+
+  double acc64[4][16];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc64[q][i] = 0.0;
+  v16f c00 = {0}, c01 = {0}, c10 = {0}, c11 = {0};
+  int rows_in_seg = 0;
+  double tsum = 0.0;                 // t_w partial of column mg (f64, nt == 0 only)
+  const bool do_tw = nt == 0;
+
+  const int am0 = wm * 64 + r, am1 = am0 + 32;
+  const int bn0 = wn * 64 + r, bn1 = bn0 + 32;
+  if (kb < ke) load_tile(kb);
+  for (int64_t t0 = kb; t0 < ke; t0 += KB3) {
+    __syncthreads();
+    if (do_tw) {
+#pragma unroll
+      for (int i = 0; i < 32; ++i) tsum += (double)ra[i];
+    }
+    store_tile();
+    __syncthreads();
+    if (t0 + KB3 < ke) load_tile(t0 + KB3);  // in flight during the MFMAs below
+#pragma unroll
+    for (int kk = 0; kk < KB3; kk += 16) {
+      const v8bf b0 = *reinterpret_cast<const v8bf*>(&sB[bn0][kk + 8 * h]);
+      const v8bf b1 = *reinterpret_cast<const v8bf*>(&sB[bn1][kk + 8 * h]);
+#pragma unroll
+      for (int sp = 0; sp < 3; ++sp) {
+        const v8bf a0 = *reinterpret_cast<const v8bf*>(&sA[sp][am0][kk + 8 * h]);
+        const v8bf a1 = *reinterpret_cast<const v8bf*>(&sA[sp][am1][kk + 8 * h]);
+        c00 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, c00, 0, 0, 0);
+        c01 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, c01, 0, 0, 0);
+        c10 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, c10, 0, 0, 0);
+        c11 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, c11, 0, 0, 0);
+      }
+    }
+    rows_in_seg += KB3;
+    if (rows_in_seg >= kFlush || t0 + KB3 >= ke) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        acc64[0][i] += (double)c00[i];
+        acc64[1][i] += (double)c01[i];
+        acc64[2][i] += (double)c10[i];
+        acc64[3][i] += (double)c11[i];
+        c00[i] = c01[i] = c10[i] = c11[i] = 0.f;
+      }
+      rows_in_seg = 0;
+    }
+  }
+  double* pp = part + (size_t)ks * Mp * Npd;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int mi = q >> 1, ni = q & 1;
+    const int col = nt * TN + wn * 64 + ni * 32 + r;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = mt * TM + wm * 64 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+      pp[(size_t)row * Npd + col] = acc64[q][i];
+    }
+  }
+  if (do_tw) twpart[((size_t)ks * 2 + tg) * Mp + mg] = tsum;
+}
+
+__global__ void k_tw_reduce(const double* __restrict__ twpart, int nKS, int Mp, int L,
+                            double* __restrict__ tw) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= L) return;
+  double s = 0.0;
+  for (int k = 0; k < 2 * nKS; ++k) s += twpart[(size_t)k * Mp + m];
+  tw[m] = s;
+}
+
+// yext (T, Np) f32 -> ybt (Np, Tp) bf16 bits (truncation; exact for integers <= 256),
+// zero for t >= T.  64 x 64 tiles through LDS.
+__global__ void __launch_bounds__(256) k_spikes_bf16t(const float* __restrict__ yext, int64_t T,
+                                                      int Np, uint16_t* __restrict__ ybt, int64_t Tp) {
+  __shared__ uint16_t tile[64][66];
+  const int64_t t0 = (int64_t)blockIdx.x * 64;
+  const int n0 = blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t t = t0 + i;
+    const int n = n0 + tx;
+    const float v = (t < T && n < Np) ? yext[t * Np + n] : 0.f;
+    tile[i][tx] = (uint16_t)(__float_as_uint(v) >> 16);
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int n = n0 + i;
+    const int64_t t = t0 + tx;
+    if (n < Np && t < Tp) ybt[(size_t)n * Tp + t] = tile[tx][i];
+  }
+}
+
+static int device_cus() {
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      ncu = 256;
+  }
+  return ncu;
+}
+
+// One workgroup per CU (the kernel runs at one wave per SIMD: 73.7 KB LDS, 406
+// registers), all in ONE round: tiles x K-slices <= #CUs.
+static int ptb3_geometry(int64_t K, int Mdim, int Ndim, int& nMT, int& nNT, int& nKS, int64_t& KT,
+                         int& Mp, int& Npd) {
+  nMT = (Mdim + TM - 1) / TM;
+  nNT = (Ndim + TN - 1) / TN;
+  Mp = nMT * TM;
+  Npd = nNT * TN;
+  const int64_t tiles = (int64_t)nMT * nNT;
+  int64_t want = device_cus() / tiles;
+  if (want < 1) want = 1;
+  KT = (K + want - 1) / want;
+  KT = round_up(KT < kFlush ? kFlush : KT, kFlush);
+  nKS = (int)((K + KT - 1) / KT);
+  if (nKS < 1) nKS = 1;
+  return 0;
+}
+
 }  // namespace pmg
 
 using namespace pmg;
@@ -216,6 +435,50 @@ int pmg_suffstats(const float* P, const float* yext, int64_t T, int32_t L, int32
   PMG_REQUIRE(workspace_bytes >= pmg_suffstats_workspace_size(T, L, Np),
               "pmg_suffstats: workspace too small");
   return atb_run(P, L, L, yext, Np, Np, 0, T, yw, N, N, N, tw, workspace, as_stream(stream));
+}
+
+int pmg_spikes_bf16t(const float* yext, int64_t T, int32_t Np, uint16_t* ybt, int64_t Tp, void* stream) {
+  PMG_REQUIRE(yext && ybt && T > 0 && Np > 0 && Tp == round_up(T, KB3), "pmg_spikes_bf16t: bad args");
+  dim3 grid((unsigned)(Tp / 64), (unsigned)((Np + 63) / 64));
+  hipLaunchKernelGGL(k_spikes_bf16t, grid, dim3(256), 0, as_stream(stream), yext, T, Np, ybt, Tp);
+  PMG_LAUNCH_CHECK();
+  return PMG_OK;
+}
+
+size_t pmg_suffstats_bf16_workspace_size(int64_t T, int32_t L, int32_t N) {
+  int nMT, nNT, nKS, Mp, Npd;
+  int64_t KT;
+  ptb3_geometry(T, L, N, nMT, nNT, nKS, KT, Mp, Npd);
+  return (size_t)nKS * Mp * (Npd + 2) * sizeof(double) + 256;
+}
+
+int pmg_suffstats_bf16(const float* P, const uint16_t* ybt, int64_t T, int64_t Tp, int32_t L, int32_t N,
+                       int32_t Np, double* yw, double* tw, void* workspace, size_t workspace_bytes,
+                       void* stream) {
+  PMG_REQUIRE(T > 0 && L > 0 && N > 0 && Np >= N + 1 && Np % 64 == 0 && Tp == round_up(T, KB3),
+              "pmg_suffstats_bf16: bad shape");
+  PMG_REQUIRE(P && ybt && yw && tw && workspace, "pmg_suffstats_bf16: null");
+  PMG_REQUIRE(workspace_bytes >= pmg_suffstats_bf16_workspace_size(T, L, N),
+              "pmg_suffstats_bf16: workspace too small");
+  int nMT, nNT, nKS, Mp, Npd;
+  int64_t KT;
+  // the ones column of yext is not used: t_w comes from the staged P values
+  ptb3_geometry(T, L, N, nMT, nNT, nKS, KT, Mp, Npd);
+  double* part = reinterpret_cast<double*>(workspace);
+  double* twpart = part + (size_t)nKS * Mp * Npd;
+  hipStream_t st = as_stream(stream);
+  const int64_t wgs = (int64_t)nMT * nNT * nKS;
+  hipLaunchKernelGGL(k_ptb3, dim3((unsigned)wgs), dim3(256), 0, st, P, L, ybt, Tp, N, T, KT, nMT, nNT,
+                     nKS, Mp, Npd, part, twpart);
+  PMG_LAUNCH_CHECK();
+  const int64_t total = (int64_t)L * Npd;
+  hipLaunchKernelGGL(k_atb_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                     (const double*)part, nKS, Mp, Npd, L, N, N, yw, -1, (double*)nullptr);
+  PMG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_tw_reduce, dim3((unsigned)((L + 255) / 256)), dim3(256), 0, st,
+                     (const double*)twpart, nKS, Mp, L, tw);
+  PMG_LAUNCH_CHECK();
+  return PMG_OK;
 }
 
 size_t pmg_joint_workspace_size(int64_t T, int32_t L) {

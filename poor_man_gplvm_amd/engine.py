@@ -106,6 +106,12 @@ class SpikeData:
         self.flags = int(flags.item())
         # exact int8 path: integer counts in [0,127], 0/1 mask, no per-time mask
         self.int_path = self.flags == 0 and not self.ma_2d
+        # integer counts are exact in bf16: suff-stats on the bf16 MFMA (exact products)
+        self.ybt = None
+        if not (self.flags & 1):
+            self.ybt = torch.empty((self.Np, self.Tp), dtype=torch.int16, device=dev)
+            nat.check(lib.pmg_spikes_bf16t(nat.ptr(self.yext), self.T, self.Np, nat.ptr(self.ybt), self.Tp,
+                                           nat.stream_handle()), "pmg_spikes_bf16t")
 
 
 class KernelTimer:
@@ -190,7 +196,9 @@ class DeviceEM:
         self.tw = torch.empty(L, dtype=f64, device=dev)
         self.ws_em = torch.empty(int(self.lib.pmg_emission_workspace_size(T, L, N)), dtype=torch.uint8, device=dev)
         self.ws_fb = torch.empty(int(self.lib.pmg_fwdbwd_workspace_size(T, L, self.C)), dtype=torch.uint8, device=dev)
-        self.ws_ss = torch.empty(int(self.lib.pmg_suffstats_workspace_size(T, L, spikes.Np)), dtype=torch.uint8, device=dev)
+        ss_bytes = (self.lib.pmg_suffstats_bf16_workspace_size(T, L, N) if spikes.ybt is not None
+                    else self.lib.pmg_suffstats_workspace_size(T, L, spikes.Np))
+        self.ws_ss = torch.empty(int(ss_bytes), dtype=torch.uint8, device=dev)
         if self.ws_fb.numel() == 0:
             raise nat.NativeError(f"n_latent_bin={L} unsupported by the scan kernels (max 1024)")
         self.ws_ad = None
@@ -246,9 +254,15 @@ class DeviceEM:
         """Sufficient statistics of self.P, then the Adam loop; W/mu/nu/count in place."""
         sh = nat.stream_handle()
         with self._t('suffstats'):
-          nat.check(self.lib.pmg_suffstats(nat.ptr(self.P), nat.ptr(self.sp.yext), self.T, self.L, self.N,
-                                         self.sp.Np, nat.ptr(self.yw), nat.ptr(self.tw),
-                                         nat.ptr(self.ws_ss), self.ws_ss.numel(), sh), "pmg_suffstats")
+          if self.sp.ybt is not None:
+            nat.check(self.lib.pmg_suffstats_bf16(nat.ptr(self.P), nat.ptr(self.sp.ybt), self.T, self.sp.Tp,
+                                                  self.L, self.N, self.sp.Np, nat.ptr(self.yw), nat.ptr(self.tw),
+                                                  nat.ptr(self.ws_ss), self.ws_ss.numel(), sh),
+                      "pmg_suffstats_bf16")
+          else:
+            nat.check(self.lib.pmg_suffstats(nat.ptr(self.P), nat.ptr(self.sp.yext), self.T, self.L, self.N,
+                                             self.sp.Np, nat.ptr(self.yw), nat.ptr(self.tw),
+                                             nat.ptr(self.ws_ss), self.ws_ss.numel(), sh), "pmg_suffstats")
         self.adam(W, mu, nu, count, cfg, stats_out, lh_out, eh_out)
 
     def adam(self, W, mu, nu, count, cfg: AdamConfig, stats_out, lh_out, eh_out):

@@ -24,6 +24,11 @@ def em_case(name, N, L, T, n_iter, maxiter, tol, ls=10.0, mv=1.0, seed=0):
     d = make(N, L, T, ls=ls, mv=mv, seed=seed)
     r = O.fit_em(d['y'], d['W0'].astype(np.float64), d['B'].astype(np.float64), d['lp0'].astype(np.float64),
                  n_iter=n_iter, movement_variance=mv, m_step_maxiter=maxiter, m_step_tol=tol)
+    # the same fit in the reference's own arithmetic (float32 reference-mimic): its
+    # distance to the float64 answer is the reference's rounding noise floor
+    with O.working_precision(np.float32):
+        r32 = O.fit_em(d['y'], d['W0'], d['B'], d['lp0'], n_iter=n_iter, movement_variance=mv,
+                       m_step_maxiter=maxiter, m_step_tol=tol)
     m = r['m_step_res_l']
     np.savez_compressed(os.path.join(HERE, name),
                         y=d['y'].astype(np.int16), basis=d['B'], W0=d['W0'], lp0=d['lp0'],
@@ -33,7 +38,9 @@ def em_case(name, N, L, T, n_iter, maxiter, tol, ls=10.0, mv=1.0, seed=0):
                         log_marginal_l=np.array(r['log_marginal_l']),
                         m_n_iter=np.array(m['n_iter']), m_final_loss=np.array(m['final_loss']),
                         m_final_error=np.array(m['final_error']),
-                        m_loss_history_0=m['loss_history'][0])
+                        m_loss_history_0=m['loss_history'][0],
+                        mimic32_tuning=r32['tuning'].astype(np.float32),
+                        mimic32_posterior_latent=r32['posterior_latent_marg'].astype(np.float32))
 
 
 def decode_case(name, N, L, T, mv=1.0, seed=5, ma_latent=None):
@@ -54,6 +61,7 @@ def decode_case(name, N, L, T, mv=1.0, seed=5, ma_latent=None):
 
 def main():
     em_case('em_c1_fixed.npz', N=30, L=100, T=400, n_iter=3, maxiter=40, tol=0.0)
+    em_case('em_c1_one.npz', N=30, L=100, T=400, n_iter=1, maxiter=40, tol=0.0)
     em_case('em_small_stoprule.npz', N=20, L=64, T=300, n_iter=3, maxiter=1000, tol=1e-6)
     decode_case('decode_small.npz', N=24, L=48, T=200)
     ml = np.ones(48)

@@ -91,3 +91,27 @@ def test_product_does_not_import_oracle():
             if isinstance(node, (ast.Import, ast.ImportFrom)):
                 names = [a.name for a in node.names] + ([node.module] if getattr(node, 'module', None) else [])
                 assert not any(n and n.split('.')[0] == 'oracle' for n in names), f
+
+
+def test_masked_joint_sentinel_matches_fixture():
+    """Linear-space joint counts S (exact zeros in masked rows/columns) assembled by
+    log_joint_from_counts reproduce the reference's -1e20 sentinel arithmetic for the
+    transition posteriors of masked latents (decode_masked.npz, oracle-made)."""
+    from oracle import gplvm_oracle as O
+    from poor_man_gplvm_amd.core import log_joint_from_counts, compute_transition_posterior_prob
+    f = np.load(os.path.join(HERE, 'golden', 'decode_masked.npz'))
+    ml = f['ma_latent'].astype(bool)
+    L = ml.size
+    _, logK, _, logA = O.create_transition_prob_1d(L, float(f['mv']))
+    lpa, logz, _, cs, joint, ll = O.smooth_all_step_combined_ma_chunk(
+        f['y'].astype(np.float64), f['tuning'].astype(np.float64), logK, logA, None, ml.astype(float),
+        1.0, 10000, with_joint=True)
+    with np.errstate(invalid='ignore'):
+        S4 = np.exp(joint - logA[:, :, None, None] - logK[None])
+    keep = (ml[:, None] & ml[None, :])[None, None] & np.isfinite(joint)
+    S4 = np.where(keep, np.nan_to_num(S4), 0.0)
+    r = compute_transition_posterior_prob(log_joint_from_counts(S4, logK, logA, ml))
+    for k in ['p_transition_latent', 'p_transition_dynamics', 'p_joint_dynamics', 'p_joint_latent']:
+        np.testing.assert_allclose(r[k], f[k], rtol=1e-6, atol=1e-9, err_msg=k)
+    # the masked rows are the sentinel pattern: 1 at unmasked destinations in K's support
+    assert np.all(r['p_transition_latent'][~ml][:, ~ml] == 0.0)

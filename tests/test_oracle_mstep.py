@@ -1,6 +1,7 @@
 """Oracle M-step: objective gradient, optax-0.2.2 Adam, the while-loop stop rule
 (fit_tuning_helper.py:63-81, :124-196).  CPU only."""
 import math
+import os
 
 import numpy as np
 
@@ -91,3 +92,16 @@ def test_fixed_iterations_with_tol_zero():
     B, W, yw, tw = _problem(3)
     r = O.adam_run(W, O.adam_init(W), 1.0, B, yw, tw, maxiter=17, tol=0.0)
     assert r['n_iter'] == 17
+
+
+def test_working_precision_mimic_is_float32_and_restores():
+    """oracle.working_precision(np.float32) = the reference's own fp32 arithmetic
+    (used to size the reference's rounding noise in the EM goldens)."""
+    f = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'decode_small.npz'))
+    with O.working_precision(np.float32):
+        r32 = O.decode_latent(f['y'], f['tuning'].astype(np.float32), movement_variance=float(f['mv']))
+    assert r32['posterior_all'].dtype == np.float32
+    assert O._F is np.float64
+    r64 = O.decode_latent(f['y'].astype(np.float64), f['tuning'], movement_variance=float(f['mv']))
+    d = np.abs(r32['posterior_all'] - r64['posterior_all']).max()
+    assert 0 < d < 1e-2
