@@ -52,7 +52,7 @@ const char* pmg_last_error(void);
 /* fit_tuning_helper.get_statistics (fit_tuning_helper.py:28-42).       */
 /*   y        (T,N) f32 spike counts                                     */
 /*   ma_neuron (N) f32 or (T,N) f32 (ma_is_2d) or NULL (all ones)        */
-/*   yq_out   (Tp,Kp) int8, Tp = roundup(T,64), Kp = roundup(N,32):       */
+/*   yq_out   (Tp,Kp) int8, Tp = roundup(T,64), Kp = roundup(N,128):      */
 /*            y*ma (zero padded), the integer emission operand           */
 /*   gconst_out (T) f64: sum_n ma[t,n]*gammaln(y[t,n]+1)                 */
 /*   yext_out (T,Np) f32, Np = roundup(N+1,64): y, then a ones column    */

@@ -69,24 +69,25 @@ __global__ void __launch_bounds__(256) k_rates_prepare(
   }
 }
 
-// Workgroup tile 128 time bins x 64 latents, 4 waves as 2 (time) x 2 (latent); each
-// wave owns 64 t x 32 l for all 5 digits (2 x 5 v16i accumulators).  MFMA operand A =
-// y (rows = time), B = digits (cols = latent), so C[t][l] rows leave as 128-byte
-// coalesced stores.  K (neurons) advances in 64-byte chunks staged through
-// double-buffered LDS (rows of 80 B: the 16-byte fragment reads of 16 consecutive
-// rows hit distinct bank quads).
+// Workgroup tile 128 time bins x 64 latents, 8 waves as 4 (time) x 2 (latent); each
+// wave owns 32 t x 32 l for all 5 digits (5 v16i accumulators).  MFMA operand A = y
+// (rows = time), B = digits (cols = latent), so C[t][l] rows leave as 128-byte
+// coalesced stores.  K (neurons) advances in 128-byte chunks staged through
+// double-buffered LDS (rows of 144 B: the 16-byte fragment reads of 16 consecutive
+// rows hit distinct bank quads); the next chunk's global loads are in flight during
+// the current chunk's MFMAs.
 // Fragment map (i8 32x32x32): lane (r = lane&31, h = lane>>5) supplies
 // A[row r][k = 16h .. 16h+15] and B[k = 16h ..][col r]; the same (h, byte) -> k
 // assignment on both operands keeps the K pairing consistent.
 // C/D: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*h.
-constexpr int ET = 128, EL = 64, EKC = 64, EROW = EKC + 16;
+constexpr int ET = 128, EL = 64, EKC = 128, EROW = EKC + 16;
 
 __device__ __forceinline__ int xcd_group(int bid, int nwg) {
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-__global__ void __launch_bounds__(256, 2) k_emission_i8(
+__global__ void __launch_bounds__(512) k_emission_i8(
     const int8_t* __restrict__ yq, const int8_t* __restrict__ qd,
     const double* __restrict__ lamsum, const double* __restrict__ gconst,
     const uint8_t* __restrict__ ma_latent, int64_t T, int64_t Tp, int L, int Lp, int Kp, int nLT,
@@ -101,97 +102,90 @@ __global__ void __launch_bounds__(256, 2) k_emission_i8(
   const int64_t t0 = tt * ET;
   const int l0 = lt * EL;
   const int r = lane & 31, h = lane >> 5;
-  const int wt = wid & 1, wl = wid >> 1;
+  const int wt = wid & 3, wl = wid >> 2;
   const size_t plane = (size_t)Lp * Kp;
 
-  // staging map: Y 128 rows x 4 x 16 B (2 per thread), Q 5 x 64 rows x 4 x 16 B (5 per thread)
-  uint4 ry[2], rq[kDig];
-  auto load_chunk = [&](int k0) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int e = tid + 256 * q;
-      const int row = e >> 2, c = (e & 3) * 16;
-      const int64_t t = t0 + row;
-      ry[q] = (t < Tp && k0 + c < Kp) ? *reinterpret_cast<const uint4*>(yq + t * Kp + k0 + c)
-                                       : make_uint4(0u, 0u, 0u, 0u);
-    }
-#pragma unroll
-    for (int d = 0; d < kDig; ++d) {
-      const int row = tid >> 2, c = (tid & 3) * 16;
-      const int l = l0 + row;
-      rq[d] = (l < Lp && k0 + c < Kp)
-                  ? *reinterpret_cast<const uint4*>(qd + d * plane + (size_t)l * Kp + k0 + c)
-                  : make_uint4(0u, 0u, 0u, 0u);
-    }
-  };
-  auto store_chunk = [&](int buf) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int e = tid + 256 * q;
-      *reinterpret_cast<uint4*>(&sY[buf][e >> 2][(e & 3) * 16]) = ry[q];
-    }
-#pragma unroll
-    for (int d = 0; d < kDig; ++d)
-      *reinterpret_cast<uint4*>(&sQ[buf][d][tid >> 2][(tid & 3) * 16]) = rq[d];
-  };
+  // branch-free staging loads (Kp is a multiple of EKC): rows past Tp / Lp are
+  // clamped -- their outputs are never written.
+  const int sc = (tid & 7) * 16;
+  int64_t ty0 = t0 + (tid >> 3), ty1 = ty0 + 64;
+  ty0 = ty0 < Tp ? ty0 : Tp - 1;
+  ty1 = ty1 < Tp ? ty1 : Tp - 1;
+  const int8_t* yrow0 = yq + ty0 * Kp + sc;
+  const int8_t* yrow1 = yq + ty1 * Kp + sc;
+  int lq = l0 + (tid >> 3);
+  lq = lq < Lp ? lq : Lp - 1;
+  const int8_t* qrow = qd + (size_t)lq * Kp + sc;
+#define PMG_EM_LOAD(k0)                                                      \
+  ry0 = *reinterpret_cast<const uint4*>(yrow0 + (k0));                      \
+  ry1 = *reinterpret_cast<const uint4*>(yrow1 + (k0));                      \
+  rq0 = *reinterpret_cast<const uint4*>(qrow + (k0));                       \
+  rq1 = *reinterpret_cast<const uint4*>(qrow + plane + (k0));               \
+  rq2 = *reinterpret_cast<const uint4*>(qrow + 2 * plane + (k0));           \
+  rq3 = *reinterpret_cast<const uint4*>(qrow + 3 * plane + (k0));           \
+  rq4 = *reinterpret_cast<const uint4*>(qrow + 4 * plane + (k0));
+#define PMG_EM_STORE(b)                                                      \
+  *reinterpret_cast<uint4*>(&sY[b][tid >> 3][sc]) = ry0;                    \
+  *reinterpret_cast<uint4*>(&sY[b][64 + (tid >> 3)][sc]) = ry1;             \
+  *reinterpret_cast<uint4*>(&sQ[b][0][tid >> 3][sc]) = rq0;                 \
+  *reinterpret_cast<uint4*>(&sQ[b][1][tid >> 3][sc]) = rq1;                 \
+  *reinterpret_cast<uint4*>(&sQ[b][2][tid >> 3][sc]) = rq2;                 \
+  *reinterpret_cast<uint4*>(&sQ[b][3][tid >> 3][sc]) = rq3;                 \
+  *reinterpret_cast<uint4*>(&sQ[b][4][tid >> 3][sc]) = rq4;
+  uint4 ry0, ry1, rq0, rq1, rq2, rq3, rq4;
 
-  v16i acc[kDig][2];
+  v16i acc[kDig];
 #pragma unroll
-  for (int d = 0; d < kDig; ++d) {
-    acc[d][0] = (v16i){0};
-    acc[d][1] = (v16i){0};
-  }
-  const int nch = (Kp + EKC - 1) / EKC;
-  load_chunk(0);
-  store_chunk(0);
+  for (int d = 0; d < kDig; ++d) acc[d] = (v16i){0};
+  const int nch = Kp / EKC;
+  PMG_EM_LOAD(0)
+  PMG_EM_STORE(0)
   __syncthreads();
   for (int ch = 0; ch < nch; ++ch) {
     const int buf = ch & 1;
-    if (ch + 1 < nch) load_chunk((ch + 1) * EKC);   // in flight during the MFMAs
+    const bool more = ch + 1 < nch;
+    if (more) {   // in flight during the MFMAs
+      PMG_EM_LOAD((ch + 1) * EKC)
+    }
 #pragma unroll
     for (int ks = 0; ks < EKC; ks += 32) {
-      const v4i a0 = *reinterpret_cast<const v4i*>(&sY[buf][wt * 64 + r][ks + 16 * h]);
-      const v4i a1 = *reinterpret_cast<const v4i*>(&sY[buf][wt * 64 + 32 + r][ks + 16 * h]);
+      const v4i a = *reinterpret_cast<const v4i*>(&sY[buf][wt * 32 + r][ks + 16 * h]);
 #pragma unroll
       for (int d = 0; d < kDig; ++d) {
         const v4i b = *reinterpret_cast<const v4i*>(&sQ[buf][d][wl * 32 + r][ks + 16 * h]);
-        acc[d][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b, acc[d][0], 0, 0, 0);
-        acc[d][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b, acc[d][1], 0, 0, 0);
+        acc[d] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc[d], 0, 0, 0);
       }
     }
-    if (ch + 1 < nch) {
-      store_chunk(buf ^ 1);   // the other buffer was last read one iteration ago
+    if (more) {
+      PMG_EM_STORE(buf ^ 1)   // the other buffer was last read before the previous barrier
       __syncthreads();
     }
   }
+#undef PMG_EM_LOAD
+#undef PMG_EM_STORE
 
   // epilogue: int64 recombination, f64 ll, 32-latent block max, coalesced rows
   const int nblk = Lp >> 5;
-  const int l = l0 + wl * 32 + r;
   const int blk = (l0 >> 5) + wl;
+  if (blk >= nblk) return;
+  const int l = l0 + wl * 32 + r;
   const bool lvalid = l < L;
   const bool lmask = lvalid && ma_latent && ma_latent[l] == 0;
-  const double lsum = (l < Lp) ? lamsum[l] : 0.0;
-  if (blk >= nblk) return;
+  const double lsum = lamsum[l];           // l < Lp here
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
+  for (int i = 0; i < 16; ++i) {
+    const int64_t t = t0 + wt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+    long long q = (long long)acc[0][i];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int64_t t = t0 + wt * 64 + s * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-      long long q = (long long)acc[0][s][i];
-#pragma unroll
-      for (int d = 1; d < kDig; ++d) q += (long long)acc[d][s][i] << (8 * d);
-      const bool tvalid = t < T;
-      double v = -INFINITY;
-      if (lvalid) v = lmask ? -1e20 : (double)q * kQInv - lsum - (tvalid ? gconst[t] : 0.0);
-      float mf = (float)v;
-#pragma unroll
-      for (int o = 16; o >= 1; o >>= 1) mf = fmaxf(mf, __shfl_xor(mf, o, 32));
-      const double mx = (double)mf;
-      if (tvalid) {
-        if (r == 0) rblk[t * nblk + blk] = mx;
-        if (lvalid) delta[t * (int64_t)L + l] = (float)(v - mx);
-      }
+    for (int d = 1; d < kDig; ++d) q += (long long)acc[d][i] << (8 * d);
+    const double gc = gconst[t < T ? t : T - 1];
+    double v = (double)q * kQInv - lsum - gc;
+    v = lmask ? -1e20 : v;
+    v = lvalid ? v : -INFINITY;
+    const double mx = (double)half_max32((float)v);
+    if (t < T) {
+      if (r == 0) rblk[t * nblk + blk] = mx;
+      if (lvalid) delta[t * (int64_t)L + l] = (float)(v - mx);
     }
   }
 }
@@ -276,7 +270,7 @@ extern "C" {
 
 size_t pmg_emission_workspace_size(int64_t T, int32_t L, int32_t N) {
   (void)T;
-  const int64_t Lp = round_up(L, 32), Kp = round_up(N, 32);
+  const int64_t Lp = round_up(L, 32), Kp = round_up(N, 128);
   Carver c(nullptr);
   c.take<int8_t>(kDig * Lp * Kp);
   c.take<double>(Lp);
@@ -289,7 +283,7 @@ int pmg_emission_poisson(const int8_t* yq, const double* gconst, const double* t
                          int64_t T, int32_t L, int32_t N, int32_t Kp, float* delta,
                          double* rblk, void* workspace, size_t workspace_bytes, void* stream) {
   PMG_REQUIRE(T > 0 && L > 0 && N > 0, "pmg_emission_poisson: bad shape");
-  PMG_REQUIRE(Kp == round_up(N, 32), "pmg_emission_poisson: Kp must be roundup(N,32)");
+  PMG_REQUIRE(Kp == round_up(N, 128), "pmg_emission_poisson: Kp must be roundup(N,128)");
   PMG_REQUIRE(yq && gconst && tuning64 && delta && rblk && workspace, "pmg_emission_poisson: null");
   PMG_REQUIRE(workspace_bytes >= pmg_emission_workspace_size(T, L, N),
               "pmg_emission_poisson: workspace too small");
@@ -306,7 +300,7 @@ int pmg_emission_poisson(const int8_t* yq, const double* gconst, const double* t
   const int nLT = (Lp + EL - 1) / EL;
   const int64_t nTT = (T + ET - 1) / ET;
   const int64_t Tp = round_up(T, 64);   // rows of yq (pmg_spikes_prepare zero-pads to Tp)
-  hipLaunchKernelGGL(k_emission_i8, dim3((unsigned)(nLT * nTT)), dim3(256), 0, st, yq, qd, lamsum,
+  hipLaunchKernelGGL(k_emission_i8, dim3((unsigned)(nLT * nTT)), dim3(512), 0, st, yq, qd, lamsum,
                      gconst, ma_latent, T, Tp, L, Lp, Kp, nLT, delta, rblk);
   PMG_LAUNCH_CHECK();
   return PMG_OK;

@@ -121,6 +121,18 @@ __device__ __forceinline__ float wave_max(float v) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
+// max over each 32-lane half of the wave, result in every lane of the half:
+// quad_perm xor1 / xor2, row_half_mirror, row_mirror (16-lane row max), then
+// permlane16_swap pairs rows 0<->1 and 2<->3.
+__device__ __forceinline__ float half_max32(float v) {
+  v = fmaxf(v, dppf<0xB1>(v));
+  v = fmaxf(v, dppf<0x4E>(v));
+  v = fmaxf(v, dppf<0x141>(v));
+  v = fmaxf(v, dppf<0x140>(v));
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
 // f64 reductions via shuffles (used off the critical path)
 __device__ __forceinline__ double wave_sum_f64(double v) {
 #pragma unroll

@@ -237,125 +237,139 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-__global__ void __launch_bounds__(256) k_ptb3(const float* __restrict__ P, int L,
+__global__ void __launch_bounds__(512) k_ptb3(const float* __restrict__ P, int L,
                                               const uint16_t* __restrict__ Ybt, int64_t Tp, int Np,
                                               int64_t K, int64_t KT, int nMT, int nNT, int nKS,
                                               int Mp, int Npd, double* __restrict__ part,
                                               double* __restrict__ twpart) {
-  __shared__ __attribute__((aligned(16))) uint16_t sA[3][TM][ROW3];
-  __shared__ __attribute__((aligned(16))) uint16_t sB[TN][ROW3];
+  // double-buffered operands: 2 x (3 x 128 x 72 + 128 x 72) x 2 B = 147456 B
+  __shared__ __attribute__((aligned(16))) uint16_t sA[2][3][TM][ROW3];
+  __shared__ __attribute__((aligned(16))) uint16_t sB[2][TN][ROW3];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
   const int mt = lb % nMT;
   const int nt = (lb / nMT) % nNT;
   const int ks = lb / (nMT * nNT);
-  const int wm = wid & 1, wn = wid >> 1;
+  const int wm = wid & 3, wn = wid >> 2;       // wave tile: 32 m x 64 n
   const int r = lane & 31, h = lane >> 5;
   const int64_t kb = (int64_t)ks * KT;
   const int64_t ke = kb + KT < K ? kb + KT : K;
 
-  // staging: A column m_l = tid & 127, time rows 32*tg .. 32*tg+31 of the K-tile;
-  // B row n_l = tid >> 1, time half hb = tid & 1 (32 bf16 = 4 x 16 B)
+  // staging: A column m_l = tid & 127, time rows 16*tg .. 16*tg+15 of the K-tile (tg
+  // wave-uniform); B row n_l = tid >> 2, time quarter hq = tid & 3 (16 bf16 = 2 x 16 B).
+  // Branch-free: clamped addresses, rows past the K-slice end selected to zero; rows
+  // m >= L / n >= N only feed output rows/columns the reduction drops.
   const int m_l = tid & 127, tg = tid >> 7;
-  const int n_l = tid >> 1, hb = tid & 1;
+  const int n_l = tid >> 2, hq = tid & 3;
   const int mg = mt * TM + m_l;
   const int ng = nt * TN + n_l;
-  float ra[32];
-  uint4 rb[4];
-  auto load_tile = [&](int64_t t0) {
+  const int mgc = mg < L ? mg : L - 1;
+  const uint16_t* yrow = Ybt + (size_t)(ng < Np ? ng : Np - 1) * Tp + 16 * hq;
+  float ra[16];
+  uint4 rb0, rb1;
+  // row pointers are wave-uniform (tg is): scalar address arithmetic
+#define PMG_SS_LOAD(t0_)                                                          \
+  {                                                                               \
+    const int64_t tl0 = __builtin_amdgcn_readfirstlane((int)((t0_) + 16 * tg - kb)) + kb; \
+    _Pragma("unroll") for (int i = 0; i < 16; ++i) {                              \
+      const int64_t t = tl0 + i;                                                  \
+      const float* prow = P + (t < K ? t : K - 1) * (int64_t)L;                   \
+      const float v = prow[mgc];                                                  \
+      ra[i] = t < ke ? v : 0.f;                                                   \
+    }                                                                             \
+    const int64_t tb = (t0_) < Tp - KB3 ? (t0_) : Tp - KB3;                       \
+    rb0 = *reinterpret_cast<const uint4*>(yrow + tb);                             \
+    rb1 = *reinterpret_cast<const uint4*>(yrow + tb + 8);                         \
+  }
+  double tsum = 0.0;                 // t_w partial of column mg (f64)
+#define PMG_SS_STORE(buf)                                                         \
+  {                                                                               \
+    _Pragma("unroll") for (int i = 0; i < 16; ++i) tsum += (double)ra[i];        \
+    _Pragma("unroll") for (int q = 0; q < 2; ++q) {                               \
+      uint32_t hw[4], mw[4], lw[4];                                               \
+      _Pragma("unroll") for (int j = 0; j < 4; ++j) {                             \
+        uint32_t h0, m0, l0, h1, m1, l1;                                          \
+        split3(ra[8 * q + 2 * j], h0, m0, l0);                                    \
+        split3(ra[8 * q + 2 * j + 1], h1, m1, l1);                                \
+        hw[j] = h0 | (h1 << 16);                                                  \
+        mw[j] = m0 | (m1 << 16);                                                  \
+        lw[j] = l0 | (l1 << 16);                                                  \
+      }                                                                           \
+      const int c = 16 * tg + 8 * q;                                              \
+      *reinterpret_cast<uint4*>(&sA[buf][0][m_l][c]) = make_uint4(hw[0], hw[1], hw[2], hw[3]); \
+      *reinterpret_cast<uint4*>(&sA[buf][1][m_l][c]) = make_uint4(mw[0], mw[1], mw[2], mw[3]); \
+      *reinterpret_cast<uint4*>(&sA[buf][2][m_l][c]) = make_uint4(lw[0], lw[1], lw[2], lw[3]); \
+    }                                                                             \
+    *reinterpret_cast<uint4*>(&sB[buf][n_l][16 * hq]) = rb0;                      \
+    *reinterpret_cast<uint4*>(&sB[buf][n_l][16 * hq + 8]) = rb1;                  \
+  }
+  double acc64[2][16];
 #pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      const int64_t t = t0 + 32 * tg + i;
-      ra[i] = (t < ke && mg < L) ? P[t * L + mg] : 0.f;
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      rb[q] = ng < Np ? *reinterpret_cast<const uint4*>(Ybt + (size_t)ng * Tp + t0 + 32 * hb + 8 * q)
-                      : make_uint4(0u, 0u, 0u, 0u);
-  };
-  auto store_tile = [&]() {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      uint32_t hw[4], mw[4], lw[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        uint32_t h0, m0, l0, h1, m1, l1;
-        split3(ra[8 * q + 2 * j], h0, m0, l0);
-        split3(ra[8 * q + 2 * j + 1], h1, m1, l1);
-        hw[j] = h0 | (h1 << 16);
-        mw[j] = m0 | (m1 << 16);
-        lw[j] = l0 | (l1 << 16);
-      }
-      const int c = 32 * tg + 8 * q;
-      *reinterpret_cast<uint4*>(&sA[0][m_l][c]) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
-      *reinterpret_cast<uint4*>(&sA[1][m_l][c]) = make_uint4(mw[0], mw[1], mw[2], mw[3]);
-      *reinterpret_cast<uint4*>(&sA[2][m_l][c]) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
-      *reinterpret_cast<uint4*>(&sB[n_l][32 * hb + 8 * q]) = rb[q];
-    }
-  };
-
-  double acc64[4][16];
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < 2; ++q)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc64[q][i] = 0.0;
-  v16f c00 = {0}, c01 = {0}, c10 = {0}, c11 = {0};
-  int rows_in_seg = 0;
-  double tsum = 0.0;                 // t_w partial of column mg (f64, nt == 0 only)
-  const bool do_tw = nt == 0;
-
-  const int am0 = wm * 64 + r, am1 = am0 + 32;
+  v16f c0 = {0}, c1 = {0};
+  const int am = wm * 32 + r;
   const int bn0 = wn * 64 + r, bn1 = bn0 + 32;
-  if (kb < ke) load_tile(kb);
-  for (int64_t t0 = kb; t0 < ke; t0 += KB3) {
+// the empty asm pins the staging registers after the MFMAs, so their loads' waits (and
+// the split arithmetic reading them) are not hoisted in front of the MFMA block
+#define PMG_SS_PIN()                                                                       \
+  _Pragma("unroll") for (int i = 0; i < 16; ++i) asm volatile("" : "+v"(ra[i]));         \
+  asm volatile("" : "+v"(rb0.x), "+v"(rb0.y), "+v"(rb0.z), "+v"(rb0.w));                  \
+  asm volatile("" : "+v"(rb1.x), "+v"(rb1.y), "+v"(rb1.z), "+v"(rb1.w));
+#define PMG_SS_MFMA(buf)                                                                   \
+  _Pragma("unroll") for (int kk = 0; kk < KB3; kk += 16) {                                 \
+    const v8bf b0 = *reinterpret_cast<const v8bf*>(&sB[buf][bn0][kk + 8 * h]);            \
+    const v8bf b1 = *reinterpret_cast<const v8bf*>(&sB[buf][bn1][kk + 8 * h]);            \
+    _Pragma("unroll") for (int sp = 0; sp < 3; ++sp) {                                    \
+      const v8bf a = *reinterpret_cast<const v8bf*>(&sA[buf][sp][am][kk + 8 * h]);        \
+      c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b0, c0, 0, 0, 0);                   \
+      c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b1, c1, 0, 0, 0);                   \
+    }                                                                                     \
+  }
+
+  // pipeline: tile k's MFMAs (buffer k&1) overlap the split/store of tile k+1 (other
+  // buffer, last read before the previous barrier) and the loads of tile k+2.
+  if (kb < ke) {
+    PMG_SS_LOAD(kb)
+    PMG_SS_STORE(0)
+    PMG_SS_LOAD(kb + KB3)
     __syncthreads();
-    if (do_tw) {
-#pragma unroll
-      for (int i = 0; i < 32; ++i) tsum += (double)ra[i];
-    }
-    store_tile();
-    __syncthreads();
-    if (t0 + KB3 < ke) load_tile(t0 + KB3);  // in flight during the MFMAs below
-#pragma unroll
-    for (int kk = 0; kk < KB3; kk += 16) {
-      const v8bf b0 = *reinterpret_cast<const v8bf*>(&sB[bn0][kk + 8 * h]);
-      const v8bf b1 = *reinterpret_cast<const v8bf*>(&sB[bn1][kk + 8 * h]);
-#pragma unroll
-      for (int sp = 0; sp < 3; ++sp) {
-        const v8bf a0 = *reinterpret_cast<const v8bf*>(&sA[sp][am0][kk + 8 * h]);
-        const v8bf a1 = *reinterpret_cast<const v8bf*>(&sA[sp][am1][kk + 8 * h]);
-        c00 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, c00, 0, 0, 0);
-        c01 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, c01, 0, 0, 0);
-        c10 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, c10, 0, 0, 0);
-        c11 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, c11, 0, 0, 0);
-      }
-    }
-    rows_in_seg += KB3;
-    if (rows_in_seg >= kFlush || t0 + KB3 >= ke) {
+    for (int64_t t0 = kb; t0 < ke; t0 += 2 * KB3) {   // 2 tiles = one kFlush segment
+      PMG_SS_STORE(1)
+      PMG_SS_LOAD(t0 + 2 * KB3)
+      PMG_SS_MFMA(0)
+      PMG_SS_PIN()
+      __syncthreads();
+      PMG_SS_STORE(0)
+      PMG_SS_LOAD(t0 + 3 * KB3)
+      PMG_SS_MFMA(1)
+      PMG_SS_PIN()
+      __syncthreads();
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        acc64[0][i] += (double)c00[i];
-        acc64[1][i] += (double)c01[i];
-        acc64[2][i] += (double)c10[i];
-        acc64[3][i] += (double)c11[i];
-        c00[i] = c01[i] = c10[i] = c11[i] = 0.f;
+        acc64[0][i] += (double)c0[i];
+        acc64[1][i] += (double)c1[i];
+        c0[i] = c1[i] = 0.f;
       }
-      rows_in_seg = 0;
     }
   }
   double* pp = part + (size_t)ks * Mp * Npd;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int mi = q >> 1, ni = q & 1;
-    const int col = nt * TN + wn * 64 + ni * 32 + r;
+  for (int q = 0; q < 2; ++q) {
+    const int col = nt * TN + wn * 64 + q * 32 + r;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int row = mt * TM + wm * 64 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+      const int row = mt * TM + wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
       pp[(size_t)row * Npd + col] = acc64[q][i];
     }
   }
-  if (do_tw) twpart[((size_t)ks * 2 + tg) * Mp + mg] = tsum;
+  if (nt == 0) twpart[((size_t)ks * 4 + tg) * Mp + mg] = tsum;
+#undef PMG_SS_LOAD
+#undef PMG_SS_STORE
+#undef PMG_SS_MFMA
+#undef PMG_SS_PIN
 }
 
 __global__ void k_tw_reduce(const double* __restrict__ twpart, int nKS, int Mp, int L,
@@ -363,7 +377,7 @@ __global__ void k_tw_reduce(const double* __restrict__ twpart, int nKS, int Mp, 
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= L) return;
   double s = 0.0;
-  for (int k = 0; k < 2 * nKS; ++k) s += twpart[(size_t)k * Mp + m];
+  for (int k = 0; k < 4 * nKS; ++k) s += twpart[(size_t)k * Mp + m];
   tw[m] = s;
 }
 
@@ -449,7 +463,7 @@ size_t pmg_suffstats_bf16_workspace_size(int64_t T, int32_t L, int32_t N) {
   int nMT, nNT, nKS, Mp, Npd;
   int64_t KT;
   ptb3_geometry(T, L, N, nMT, nNT, nKS, KT, Mp, Npd);
-  return (size_t)nKS * Mp * (Npd + 2) * sizeof(double) + 256;
+  return (size_t)nKS * Mp * (Npd + 4) * sizeof(double) + 256;
 }
 
 int pmg_suffstats_bf16(const float* P, const uint16_t* ybt, int64_t T, int64_t Tp, int32_t L, int32_t N,
@@ -468,7 +482,7 @@ int pmg_suffstats_bf16(const float* P, const uint16_t* ybt, int64_t T, int64_t T
   double* twpart = part + (size_t)nKS * Mp * Npd;
   hipStream_t st = as_stream(stream);
   const int64_t wgs = (int64_t)nMT * nNT * nKS;
-  hipLaunchKernelGGL(k_ptb3, dim3((unsigned)wgs), dim3(256), 0, st, P, L, ybt, Tp, N, T, KT, nMT, nNT,
+  hipLaunchKernelGGL(k_ptb3, dim3((unsigned)wgs), dim3(512), 0, st, P, L, ybt, Tp, N, T, KT, nMT, nNT,
                      nKS, Mp, Npd, part, twpart);
   PMG_LAUNCH_CHECK();
   const int64_t total = (int64_t)L * Npd;

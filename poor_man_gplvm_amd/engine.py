@@ -79,7 +79,7 @@ class SpikeData:
         self.T, self.N = int(y.shape[0]), int(y.shape[1])
         self.device = dev
         self.y = torch.as_tensor(np.ascontiguousarray(y, dtype=np.float32), device=dev)
-        self.Kp = _ru(self.N, 32)
+        self.Kp = _ru(self.N, 128)
         self.Np = _ru(self.N + 1, 64)
         self.Tp = _ru(self.T, 64)
         self.ma_2d = False
