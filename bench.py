@@ -207,6 +207,7 @@ def main():
         "adam_iters_mean": adam_iters,
         "chunk": eng.C,
         "repairs_last": repairs,
+        "scan_warmup_fwd_bwd": list(eng.warm),
     }
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(N, T, L, adam_iters)

@@ -137,6 +137,72 @@ __device__ __forceinline__ void band_conv(const FBParams& p, float* lds, int j0,
   __syncthreads();
 }
 
+
+// ---------------------------------------------------------------------------
+// Teams: the threads that carry ONE chain.  The chunk-parallel kernels use one wave
+// per chunk (DPP reductions, no block barriers); the sequential repair of a long
+// cascade uses NW waves on the same chain (wave DPP + LDS partials behind a block
+// barrier; the scratch is double-buffered so one barrier per reduction suffices).
+// Thread t owns latents j0 = t*J .. t*J+J-1 in both cases.
+// ---------------------------------------------------------------------------
+struct WaveTeam {
+  static constexpr int NW = 1;
+  __device__ explicit WaveTeam(float*) {}
+  __device__ void sum2(float& a, float& b) { wave_sum2(a, b); }
+  __device__ float sum(float a) { return wave_sum(a); }
+  __device__ float vmax(float a) { return wave_max_shfl(a); }
+  __device__ float vmin(float a) { return wave_min_shfl(a); }
+  __device__ bool any(bool b) { return __ballot(b) != 0ull; }
+};
+
+template <int NW_>
+struct BlockTeam {
+  static constexpr int NW = NW_;
+  float* red;  // LDS scratch, 2 x 2 x NW floats
+  int buf = 0;
+  __device__ explicit BlockTeam(float* r) : red(r) {}
+  __device__ float* slot() {
+    float* r = red + buf * 2 * NW;
+    buf ^= 1;
+    return r;
+  }
+  __device__ void sum2(float& a, float& b) {
+    wave_sum2(a, b);
+    float* r = slot();
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+      r[w] = a;
+      r[NW + w] = b;
+    }
+    __syncthreads();
+    float A = 0.f, B = 0.f;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      A += r[i];
+      B += r[NW + i];
+    }
+    a = A;
+    b = B;
+  }
+  __device__ float sum(float a) {
+    float b = 0.f;
+    sum2(a, b);
+    return a;
+  }
+  __device__ float vmax(float a) {
+    a = wave_max_shfl(a);
+    float* r = slot();
+    if ((threadIdx.x & 63) == 0) r[threadIdx.x >> 6] = a;
+    __syncthreads();
+    float m = r[0];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) m = fmaxf(m, r[i]);
+    return m;
+  }
+  __device__ float vmin(float a) { return -vmax(-a); }
+  __device__ bool any(bool b) { return vmax(__ballot(b) ? 1.f : 0.f) > 0.f; }
+};
+
 // Hilbert projective distance between two non-negative (2, Lpad) states held in
 // memory; components below 1e-30 of the max on both sides are ignored, a
 // component significant (> 1e-20) on one side only counts as a failure.
@@ -171,8 +237,8 @@ __device__ float hilbert_dist(const float* __restrict__ x, const float* __restri
 }
 
 // same metric, x held in registers with the (2, Lpad) lane layout, y in memory
-template <int J>
-__device__ float hilbert_reg(const float x0[J], const float x1[J], const float* __restrict__ y,
+template <int J, class Team>
+__device__ float hilbert_reg(Team& tm, const float x0[J], const float x1[J], const float* __restrict__ y,
                              int Lpad, int j0) {
   float xm = 0.f, ym = 0.f;
 #pragma unroll
@@ -180,8 +246,8 @@ __device__ float hilbert_reg(const float x0[J], const float x1[J], const float* 
     xm = fmaxf(xm, fmaxf(x0[j], x1[j]));
     ym = fmaxf(ym, fmaxf(y[j0 + j], y[Lpad + j0 + j]));
   }
-  xm = wave_max_shfl(xm);
-  ym = wave_max_shfl(ym);
+  xm = tm.vmax(xm);
+  ym = tm.vmax(ym);
   if (!(xm > 0.f) || !(ym > 0.f)) return INFINITY;
   const float ix = 1.f / xm, iy = 1.f / ym;
   float lo = INFINITY, hi = -INFINITY;
@@ -198,9 +264,9 @@ __device__ float hilbert_reg(const float x0[J], const float x1[J], const float* 
       bad = 1;
     }
   }
-  lo = wave_min_shfl(lo);
-  hi = wave_max_shfl(hi);
-  if (__ballot(bad)) return INFINITY;
+  lo = tm.vmin(lo);
+  hi = tm.vmax(hi);
+  if (tm.any(bad != 0)) return INFINITY;
   if (hi < lo) return 0.f;
   return hi - lo;
 }
@@ -208,7 +274,7 @@ __device__ float hilbert_reg(const float x0[J], const float x1[J], const float* 
 // ---------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------
-template <int J, int WP>
+template <int J, int WP, class Team = WaveTeam>
 struct Fwd {
   float p0[J], p1[J];
   float P0, P1;  // sum of p0, p1 (wave-uniform)
@@ -223,7 +289,7 @@ struct Fwd {
     P0 = 0.5f;
     P1 = 0.5f;
   }
-  __device__ void load_state(const FBParams& p, const float* src, int j0) {
+  __device__ void load_state(Team& tm, const FBParams& p, const float* src, int j0) {
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       p0[j] = src[j0 + j];
@@ -235,7 +301,7 @@ struct Fwd {
       a += p0[j];
       b += p1[j];
     }
-    wave_sum2(a, b);
+    tm.sum2(a, b);
     const float inv = 1.f / (a + b);
 #pragma unroll
     for (int j = 0; j < J; ++j) {
@@ -253,7 +319,8 @@ struct Fwd {
     }
   }
   // one filter step with emission e; returns the normaliser S
-  __device__ float step(const FBParams& p, float* lds, int j0, const float invz[J], const float e[J]) {
+  __device__ float step(Team& tm, const FBParams& p, float* lds, int j0, const float invz[J],
+                        const float e[J]) {
     float a0[J];
 #pragma unroll
     for (int j = 0; j < J; ++j) a0[j] = fmaf(p0[j], p.A00, p1[j] * p.A10) * invz[j];
@@ -268,7 +335,7 @@ struct Fwd {
       U0 += p0[j];
       U1 += p1[j];
     }
-    wave_sum2(U0, U1);
+    tm.sum2(U0, U1);
     const float S = U0 + U1;
     const float inv = 1.f / S;
 #pragma unroll
@@ -284,10 +351,9 @@ struct Fwd {
 
 // run forward from t0 (state initialised) to t_e; writes outputs for t >= t_c and the
 // state at t_c-1 into s_in_dst (if given)
-template <int J, int WP>
-__device__ double fwd_run(const FBParams& p, Fwd<J, WP>& st, float* lds, int j0, const float invz[J],
-                          int64_t t0, int64_t t_c, int64_t t_e, float* s_in_dst) {
-  const int lane = threadIdx.x & 63;
+template <int J, int WP, class Team>
+__device__ double fwd_run(Team& tm, const FBParams& p, Fwd<J, WP, Team>& st, float* lds, int j0,
+                          const float invz[J], int64_t t0, int64_t t_c, int64_t t_e, float* s_in_dst) {
   double logz = 0.0;
   if (t0 >= t_e) return 0.0;
   EmRaw<J> nxt;
@@ -296,13 +362,13 @@ __device__ double fwd_run(const FBParams& p, Fwd<J, WP>& st, float* lds, int j0,
     float e[J];
     em_exp<J>(p, j0, nxt, e);
     if (t + 1 < t_e) em_load<J>(p, t + 1, j0, nxt);
-    const float S = st.step(p, lds, j0, invz, e);
+    const float S = st.step(tm, p, lds, j0, invz, e);
     if (t >= t_c) {
       float* arow = p.alpha + t * 2 * (int64_t)p.L;
       store_row<J>(arow, p.L, j0, st.p0);
       store_row<J>(arow + p.L, p.L, j0, st.p1);
       const double lc = (double)__logf(S) + p.s_d * p.m[t];
-      if (lane == 0) p.logc[t] = lc;
+      if (threadIdx.x == 0) p.logc[t] = lc;
       logz += lc;
     } else if (t == t_c - 1 && s_in_dst) {
       st.save_state(p, s_in_dst, j0);
@@ -311,10 +377,25 @@ __device__ double fwd_run(const FBParams& p, Fwd<J, WP>& st, float* lds, int j0,
   return logz;
 }
 
+#define PMG_FB_PROLOGUE_T(JJ, NWW)                                      \
+  __shared__ __attribute__((aligned(16))) float lds[64 * (NWW) * (JJ) + 2 * WP + 4 * (NWW)]; \
+  float* team_red = lds + 64 * (NWW) * (JJ) + 2 * WP;                   \
+  const int lane = threadIdx.x & 63;                                    \
+  (void)lane;                                                           \
+  const int j0 = threadIdx.x * (JJ);                                    \
+  for (int k = threadIdx.x; k < 64 * (NWW) * (JJ) + 2 * WP; k += 64 * (NWW)) lds[k] = 0.f; \
+  __syncthreads();                                                      \
+  float invz[JJ];                                                       \
+  _Pragma("unroll") for (int j = 0; j < (JJ); ++j) invz[j] = (j0 + j < p.L) ? p.invz[j0 + j] : 0.f; \
+  const size_t SZ = (size_t)2 * p.Lpad;                                 \
+  (void)SZ;                                                             \
+  (void)team_red;
+
 #define PMG_FB_PROLOGUE                                                 \
   __shared__ __attribute__((aligned(16))) float lds[64 * J + 2 * WP];  \
   const int lane = threadIdx.x & 63;                                    \
   const int j0 = lane * J;                                              \
+  WaveTeam tm(nullptr);                                                 \
   for (int k = lane; k < 64 * J + 2 * WP; k += 64) lds[k] = 0.f;        \
   __syncthreads();                                                      \
   float invz[J];                                                        \
@@ -336,7 +417,7 @@ __global__ void __launch_bounds__(64) k_forward(FBParams p) {
   st.init_uniform(p, j0);
   float* sin = p.s_in + (size_t)c * SZ;
   if (c > 0 && t0 == t_c) st.save_state(p, sin, j0);  // no warm-up: the guess itself
-  const double lz = fwd_run<J, WP>(p, st, lds, j0, invz, t0, t_c, t_e, c > 0 ? sin : nullptr);
+  const double lz = fwd_run(tm, p, st, lds, j0, invz, t0, t_c, t_e, c > 0 ? sin : nullptr);
   st.save_state(p, p.s_out + (size_t)c * SZ, j0);
   if (lane == 0) p.chunk_logz[c] = lz;
 }
@@ -350,8 +431,8 @@ __global__ void __launch_bounds__(64) k_forward_fix(FBParams p) {
   const int64_t t_c = (int64_t)c * p.C;
   const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
   Fwd<J, WP> st;
-  st.load_state(p, p.s_in + (size_t)c * SZ, j0);
-  const double lz = fwd_run<J, WP>(p, st, lds, j0, invz, t_c, t_c, t_e, nullptr);
+  st.load_state(tm, p, p.s_in + (size_t)c * SZ, j0);
+  const double lz = fwd_run(tm, p, st, lds, j0, invz, t_c, t_c, t_e, nullptr);
   st.save_state(p, p.s_out + (size_t)c * SZ, j0);
   if (lane == 0) {
     p.chunk_logz[c] = lz;
@@ -359,16 +440,22 @@ __global__ void __launch_bounds__(64) k_forward_fix(FBParams p) {
   }
 }
 
-// sequential fallback for whatever is still flagged after the parallel rounds
+// sequential fallback for whatever is still flagged after the parallel rounds.  A long
+// cascade (slowly forgetting chain, e.g. the flat tuning of the first EM iterations)
+// is latency-critical, so NW waves carry the one chain (J/NW latents per thread).
+template <int J> constexpr int repair_nw() { return J >= 8 ? 8 : J; }
+
 template <int J, int WP>
-__global__ void __launch_bounds__(64) k_forward_repair(FBParams p) {
-  PMG_FB_PROLOGUE
+__global__ void __launch_bounds__(64 * repair_nw<J>()) k_forward_repair(FBParams p) {
+  constexpr int NW = repair_nw<J>(), JB = J / NW;
+  PMG_FB_PROLOGUE_T(JB, NW)
+  BlockTeam<NW> tm(team_red);
   int repairs = 0;
   bool changed = false;
   int c = 1;
-  Fwd<J, WP> st;
+  Fwd<JB, WP, BlockTeam<NW>> st;
   while (c < p.M) {
-    if (!changed) {  // jump to the next flagged chunk, 64 flags at a time
+    if (!changed) {  // jump to the next flagged chunk, 64 flags at a time (every wave alike)
       int found = -1;
       for (int base = c; base < p.M && found < 0; base += 64) {
         const int idx = base + lane;
@@ -378,22 +465,24 @@ __global__ void __launch_bounds__(64) k_forward_repair(FBParams p) {
       }
       if (found < 0) break;
       c = found;
-      st.load_state(p, p.s_out + (size_t)(c - 1) * SZ, j0);
+      st.load_state(tm, p, p.s_out + (size_t)(c - 1) * SZ, j0);
     }
     const int64_t t_c = (int64_t)c * p.C;
     const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
     st.save_state(p, p.s_in + (size_t)c * SZ, j0);
-    const double lz = fwd_run<J, WP>(p, st, lds, j0, invz, t_c, t_c, t_e, nullptr);
+    const double lz = fwd_run(tm, p, st, lds, j0, invz, t_c, t_c, t_e, (float*)nullptr);
     float* sout = p.s_out + (size_t)c * SZ;
-    const float d = hilbert_reg<J>(st.p0, st.p1, sout, p.Lpad, j0);
+    const float d = hilbert_reg<JB>(tm, st.p0, st.p1, sout, p.Lpad, j0);
     changed = !(d <= p.tol);
+    __syncthreads();  // every wave has read sout before it is overwritten
     st.save_state(p, sout, j0);
-    if (lane == 0) p.chunk_logz[c] = lz;
+    if (threadIdx.x == 0) p.chunk_logz[c] = lz;
     __threadfence();
+    __syncthreads();
     ++repairs;
     ++c;
   }
-  if (lane == 0) p.repairs[0] += repairs;
+  if (threadIdx.x == 0) p.repairs[0] += repairs;
 }
 
 // boundary verification: flags[c] = hilbert(x[c], y[c + off]) > tol; a failing
@@ -432,7 +521,7 @@ __global__ void k_sum_f64(const double* __restrict__ x, int n, double* __restric
 // on the warm-up and on the output path, so two chunks that have converged to
 // the same beta produce bit-identical continuations (as the forward does).
 // ---------------------------------------------------------------------------
-template <int J, int WP>
+template <int J, int WP, class Team = WaveTeam>
 struct Bwd {
   float b0[J], b1[J];  // beta at the current time
 
@@ -480,9 +569,9 @@ struct Bwd {
 };
 
 // one plain backward step at time t (beta_t -> beta_{t-1}); v kept in (v0, v1)
-template <int J, int WP>
-__device__ __forceinline__ void bwd_plain(const FBParams& p, Bwd<J, WP>& st, float* lds, int j0,
-                                          const float invz[J], int64_t t, float v0[J], float v1[J]) {
+template <int J, int WP, class Team>
+__device__ __forceinline__ void bwd_plain(Team& tm, const FBParams& p, Bwd<J, WP, Team>& st, float* lds,
+                                          int j0, const float invz[J], int64_t t, float v0[J], float v1[J]) {
   EmRaw<J> r;
   em_load<J>(p, t, j0, r);
   float e[J];
@@ -493,16 +582,16 @@ __device__ __forceinline__ void bwd_plain(const FBParams& p, Bwd<J, WP>& st, flo
     V0 += e[j] * st.b0[j];
     V1 += e[j] * st.b1[j];
   }
-  wave_sum2(V0, V1);
+  tm.sum2(V0, V1);
   st.step_back(p, lds, j0, invz, e, V0, V1, v0, v1);
 }
 
 // output steps t = t_e-1 .. t_c.  On entry st holds beta_{t_e-1} and (vp0, vp1) the v that
 // produced it (has_prev false at the sequence end).  Writes beta_{t_c} to bf (registers).
-template <int J, int WP>
-__device__ void bwd_out(const FBParams& p, Bwd<J, WP>& st, float* lds, int j0, const float invz[J],
-                        int64_t t_c, int64_t t_e, float vp0[J], float vp1[J], bool has_prev,
-                        float bf0[J], float bf1[J]) {
+template <int J, int WP, class Team>
+__device__ void bwd_out(Team& tm, const FBParams& p, Bwd<J, WP, Team>& st, float* lds, int j0,
+                        const float invz[J], int64_t t_c, int64_t t_e, float vp0[J], float vp1[J],
+                        bool has_prev, float bf0[J], float bf1[J]) {
   const int64_t L = p.L;
   for (int64_t t = t_e - 1; t >= t_c; --t) {
     EmRaw<J> r;
@@ -522,8 +611,8 @@ __device__ void bwd_out(const FBParams& p, Bwd<J, WP>& st, float* lds, int j0, c
       V0 += e[j] * st.b0[j];
       V1 += e[j] * st.b1[j];
     }
-    wave_sum2(V0, V1);
-    G = wave_sum(G);
+    tm.sum2(V0, V1);
+    G = tm.sum(G);
     const float iG = 1.f / G;
     float pp[J];
 #pragma unroll
@@ -576,13 +665,13 @@ __global__ void __launch_bounds__(64) k_backward(FBParams p) {
   if (c < p.M - 1) {
     int64_t t_w = t_e + p.B;  // beta guess (ones) at t_w, exact when t_w is the last bin
     if (t_w > p.T - 1) t_w = p.T - 1;
-    for (int64_t t = t_w; t > t_e; --t) bwd_plain<J, WP>(p, st, lds, j0, invz, t, vp0, vp1);
+    for (int64_t t = t_w; t > t_e; --t) bwd_plain(tm, p, st, lds, j0, invz, t, vp0, vp1);
     st.save_state(p, p.b_in + (size_t)c * SZ, j0);                 // beta_{t_e}
-    bwd_plain<J, WP>(p, st, lds, j0, invz, t_e, vp0, vp1);          // -> beta_{t_e-1}
+    bwd_plain(tm, p, st, lds, j0, invz, t_e, vp0, vp1);          // -> beta_{t_e-1}
     has_prev = true;
   }
   float bf0[J], bf1[J];
-  bwd_out<J, WP>(p, st, lds, j0, invz, t_c, t_e, vp0, vp1, has_prev, bf0, bf1);
+  bwd_out(tm, p, st, lds, j0, invz, t_c, t_e, vp0, vp1, has_prev, bf0, bf1);
   float* bf = p.b_first + (size_t)c * SZ;
 #pragma unroll
   for (int j = 0; j < J; ++j) {
@@ -602,9 +691,9 @@ __global__ void __launch_bounds__(64) k_backward_fix(FBParams p) {
   Bwd<J, WP> st;
   st.load_state(p, p.b_in + (size_t)c * SZ, j0);
   float vp0[J], vp1[J];
-  bwd_plain<J, WP>(p, st, lds, j0, invz, t_e, vp0, vp1);
+  bwd_plain(tm, p, st, lds, j0, invz, t_e, vp0, vp1);
   float bf0[J], bf1[J];
-  bwd_out<J, WP>(p, st, lds, j0, invz, t_c, t_e, vp0, vp1, true, bf0, bf1);
+  bwd_out(tm, p, st, lds, j0, invz, t_c, t_e, vp0, vp1, true, bf0, bf1);
   float* bf = p.b_first + (size_t)c * SZ;
 #pragma unroll
   for (int j = 0; j < J; ++j) {
@@ -614,10 +703,12 @@ __global__ void __launch_bounds__(64) k_backward_fix(FBParams p) {
   if (lane == 0) atomicAdd(&p.repairs[1], 1);
 }
 
-// sequential fallback (descending chunks)
+// sequential fallback (descending chunks), NW waves on the one chain
 template <int J, int WP>
-__global__ void __launch_bounds__(64) k_backward_repair(FBParams p) {
-  PMG_FB_PROLOGUE
+__global__ void __launch_bounds__(64 * repair_nw<J>()) k_backward_repair(FBParams p) {
+  constexpr int NW = repair_nw<J>(), JB = J / NW;
+  PMG_FB_PROLOGUE_T(JB, NW)
+  BlockTeam<NW> tm(team_red);
   int repairs = 0;
   bool changed = false;
   int c = p.M - 2;
@@ -635,26 +726,28 @@ __global__ void __launch_bounds__(64) k_backward_repair(FBParams p) {
     }
     const int64_t t_c = (int64_t)c * p.C;
     const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
-    Bwd<J, WP> st;
+    Bwd<JB, WP, BlockTeam<NW>> st;
     st.load_state(p, p.b_first + (size_t)(c + 1) * SZ, j0);
     st.save_state(p, p.b_in + (size_t)c * SZ, j0);
-    float vp0[J], vp1[J];
-    bwd_plain<J, WP>(p, st, lds, j0, invz, t_e, vp0, vp1);
-    float bf0[J], bf1[J];
-    bwd_out<J, WP>(p, st, lds, j0, invz, t_c, t_e, vp0, vp1, true, bf0, bf1);
+    float vp0[JB], vp1[JB];
+    bwd_plain(tm, p, st, lds, j0, invz, t_e, vp0, vp1);
+    float bf0[JB], bf1[JB];
+    bwd_out(tm, p, st, lds, j0, invz, t_c, t_e, vp0, vp1, true, bf0, bf1);
     float* bf = p.b_first + (size_t)c * SZ;
-    const float d = hilbert_reg<J>(bf0, bf1, bf, p.Lpad, j0);
+    const float d = hilbert_reg<JB>(tm, bf0, bf1, bf, p.Lpad, j0);
     changed = !(d <= p.tol);
+    __syncthreads();  // every wave has read bf before it is overwritten
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
+    for (int j = 0; j < JB; ++j) {
       bf[j0 + j] = bf0[j];
       bf[p.Lpad + j0 + j] = bf1[j];
     }
     __threadfence();
+    __syncthreads();
     ++repairs;
     --c;
   }
-  if (lane == 0) p.repairs[1] += repairs;
+  if (threadIdx.x == 0) p.repairs[1] += repairs;
 }
 
 // ---------------------------------------------------------------------------
@@ -692,36 +785,54 @@ static int pick_J(int L) {
   if (L <= 1024) return 16;
   return -1;
 }
+// band = ceil(8.31 mv): 5 (mv 0.5), 9 (mv 1, the default), 17 (mv 2), 25 (mv 3) are exact
 static int pick_WP(int band) {
-  if (band <= 4) return 4;
-  if (band <= 8) return 8;
-  if (band <= 12) return 12;
-  if (band <= 16) return 16;
-  if (band <= 24) return 24;
+  if (band <= 5) return 5;
+  if (band <= 9) return 9;
+  if (band <= 13) return 13;
+  if (band <= 17) return 17;
+  if (band <= 25) return 25;
   if (band <= 32) return 32;
   return -1;
 }
 
 typedef void (*fb_kernel_t)(FBParams);
 
+static int repair_nw_rt(int J) { return J >= 8 ? 8 : J; }
+
 #define PMG_FB_TABLE(NAME)                                                                 \
   static fb_kernel_t NAME##_table(int J, int WP) {                                         \
     switch (J * 100 + WP) {                                                                \
-      case 104: return NAME<1, 4>;   case 108: return NAME<1, 8>;                          \
-      case 112: return NAME<1, 12>;  case 116: return NAME<1, 16>;                         \
-      case 124: return NAME<1, 24>;  case 132: return NAME<1, 32>;                         \
-      case 204: return NAME<2, 4>;   case 208: return NAME<2, 8>;                          \
-      case 212: return NAME<2, 12>;  case 216: return NAME<2, 16>;                         \
-      case 224: return NAME<2, 24>;  case 232: return NAME<2, 32>;                         \
-      case 404: return NAME<4, 4>;   case 408: return NAME<4, 8>;                          \
-      case 412: return NAME<4, 12>;  case 416: return NAME<4, 16>;                         \
-      case 424: return NAME<4, 24>;  case 432: return NAME<4, 32>;                         \
-      case 804: return NAME<8, 4>;   case 808: return NAME<8, 8>;                          \
-      case 812: return NAME<8, 12>;  case 816: return NAME<8, 16>;                         \
-      case 824: return NAME<8, 24>;  case 832: return NAME<8, 32>;                         \
-      case 1604: return NAME<16, 4>; case 1608: return NAME<16, 8>;                        \
-      case 1612: return NAME<16, 12>; case 1616: return NAME<16, 16>;                      \
-      case 1624: return NAME<16, 24>; case 1632: return NAME<16, 32>;                      \
+      case 105: return NAME<1, 5>;                                                    \
+      case 109: return NAME<1, 9>;                                                    \
+      case 113: return NAME<1, 13>;                                                   \
+      case 117: return NAME<1, 17>;                                                   \
+      case 125: return NAME<1, 25>;                                                   \
+      case 132: return NAME<1, 32>;                                                   \
+      case 205: return NAME<2, 5>;                                                    \
+      case 209: return NAME<2, 9>;                                                    \
+      case 213: return NAME<2, 13>;                                                   \
+      case 217: return NAME<2, 17>;                                                   \
+      case 225: return NAME<2, 25>;                                                   \
+      case 232: return NAME<2, 32>;                                                   \
+      case 405: return NAME<4, 5>;                                                    \
+      case 409: return NAME<4, 9>;                                                    \
+      case 413: return NAME<4, 13>;                                                   \
+      case 417: return NAME<4, 17>;                                                   \
+      case 425: return NAME<4, 25>;                                                   \
+      case 432: return NAME<4, 32>;                                                   \
+      case 805: return NAME<8, 5>;                                                    \
+      case 809: return NAME<8, 9>;                                                    \
+      case 813: return NAME<8, 13>;                                                   \
+      case 817: return NAME<8, 17>;                                                   \
+      case 825: return NAME<8, 25>;                                                   \
+      case 832: return NAME<8, 32>;                                                   \
+      case 1605: return NAME<16, 5>;                                                  \
+      case 1609: return NAME<16, 9>;                                                  \
+      case 1613: return NAME<16, 13>;                                                 \
+      case 1617: return NAME<16, 17>;                                                 \
+      case 1625: return NAME<16, 25>;                                                 \
+      case 1632: return NAME<16, 32>;                                                 \
       default: return nullptr;                                                             \
     }                                                                                      \
   }
@@ -822,7 +933,7 @@ int pmg_forward_filter(const float* delta, const float* phi, const double* m, in
       if (round < kFixRounds) {
         hipLaunchKernelGGL(kfix, dim3(p.M), dim3(64), 0, st, p);
       } else {
-        hipLaunchKernelGGL(kr, dim3(1), dim3(64), 0, st, p);
+        hipLaunchKernelGGL(kr, dim3(1), dim3(64 * repair_nw_rt(J)), 0, st, p);
       }
       PMG_LAUNCH_CHECK();
     }
@@ -872,7 +983,7 @@ int pmg_backward_smoother(const float* delta, const float* phi, const float* alp
       if (round < kFixRounds) {
         hipLaunchKernelGGL(kfix, dim3(p.M), dim3(64), 0, st, p);
       } else {
-        hipLaunchKernelGGL(kr, dim3(1), dim3(64), 0, st, p);
+        hipLaunchKernelGGL(kr, dim3(1), dim3(64 * repair_nw_rt(J)), 0, st, p);
       }
       PMG_LAUNCH_CHECK();
     }

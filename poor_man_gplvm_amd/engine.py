@@ -52,8 +52,10 @@ class ScanConfig:
     chunk: int | None = None     # time steps per chunk (None: ~2048 chunks)
     warmup: int = 64             # forgetting warm-up before each chunk (initial value)
     tol: float = 1e-6            # Hilbert-metric boundary tolerance
-    adaptive: bool = True        # double the warm-up when >1% of chunks needed repair
+    adaptive: bool = True        # per pass: double the warm-up when >1% of chunks needed
+                                 # repair, halve it after two E-steps with <=0.1%
     max_warmup: int = 1024
+    min_warmup: int = 16
 
     def chunk_for(self, T):
         if self.chunk:
@@ -202,7 +204,8 @@ class DeviceEM:
         if self.ws_fb.numel() == 0:
             raise nat.NativeError(f"n_latent_bin={L} unsupported by the scan kernels (max 1024)")
         self.ws_ad = None
-        self.warmup = int(self.scan.warmup)
+        self.warm = [int(self.scan.warmup), int(self.scan.warmup)]   # forward, backward
+        self._clean = [0, 0]
         self._rep_host = torch.zeros(2, dtype=torch.int32).pin_memory()
         self._rep_evt = None
         self.timer = None       # optional KernelTimer (bench): per-call HIP events
@@ -322,9 +325,17 @@ class DeviceEM:
         if not self.scan.adaptive or self._rep_evt is None or not self._rep_evt.query():
             return
         M = (self.T + self.C - 1) // self.C
-        f, b = (int(v) for v in self._rep_host.tolist())
-        if max(f, b) > max(1, M // 100) and self.warmup < self.scan.max_warmup:
-            self.warmup = min(self.scan.max_warmup, 2 * self.warmup)
+        for i, r in enumerate(int(v) for v in self._rep_host.tolist()):
+            if r > max(1, M // 100):
+                self.warm[i] = min(self.scan.max_warmup, 2 * self.warm[i])
+                self._clean[i] = 0
+            elif r <= M // 1000:
+                self._clean[i] += 1
+                if self._clean[i] >= 2 and self.warm[i] > self.scan.min_warmup:
+                    self.warm[i] = max(self.scan.min_warmup, self.warm[i] // 2)
+                    self._clean[i] = 0
+            else:
+                self._clean[i] = 0
         self._rep_evt = None
 
     def _snapshot_repairs(self):
@@ -338,7 +349,7 @@ class DeviceEM:
         with self._t('forward_filter'):
           nat.check(self.lib.pmg_forward_filter(nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.mref), self.T,
                                               ctypes.byref(self._tr_c), float(likelihood_scale), self.C,
-                                              int(self.warmup), float(sc.tol), nat.ptr(self.alpha),
+                                              int(self.warm[0]), float(sc.tol), nat.ptr(self.alpha),
                                               nat.ptr(self.logc), nat.ptr(logz_out), nat.ptr(self.ws_fb),
                                               self.ws_fb.numel(), nat.stream_handle()), "pmg_forward_filter")
 
@@ -347,7 +358,7 @@ class DeviceEM:
         with self._t('backward_smoother'):
           nat.check(self.lib.pmg_backward_smoother(nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.alpha),
                                                  self.T, ctypes.byref(self._tr_c), float(likelihood_scale),
-                                                 self.C, int(self.warmup), float(sc.tol),
+                                                 self.C, int(self.warm[1]), float(sc.tol),
                                                  nat.ptr(self.P) if P else None, nat.ptr(gamma), nat.ptr(rho),
                                                  nat.ptr(self.ws_fb), self.ws_fb.numel(), nat.stream_handle()),
                   "pmg_backward_smoother")
