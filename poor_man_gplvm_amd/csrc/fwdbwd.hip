@@ -351,27 +351,37 @@ struct Fwd {
 
 // run forward from t0 (state initialised) to t_e; writes outputs for t >= t_c and the
 // state at t_c-1 into s_in_dst (if given)
-template <int J, int WP, class Team>
+template <int J, int WP, class Team, int PF = 1>
 __device__ double fwd_run(Team& tm, const FBParams& p, Fwd<J, WP, Team>& st, float* lds, int j0,
                           const float invz[J], int64_t t0, int64_t t_c, int64_t t_e, float* s_in_dst) {
   double logz = 0.0;
   if (t0 >= t_e) return 0.0;
-  EmRaw<J> nxt;
-  em_load<J>(p, t0, j0, nxt);
-  for (int64_t t = t0; t < t_e; ++t) {
-    float e[J];
-    em_exp<J>(p, j0, nxt, e);
-    if (t + 1 < t_e) em_load<J>(p, t + 1, j0, nxt);
-    const float S = st.step(tm, p, lds, j0, invz, e);
-    if (t >= t_c) {
-      float* arow = p.alpha + t * 2 * (int64_t)p.L;
-      store_row<J>(arow, p.L, j0, st.p0);
-      store_row<J>(arow + p.L, p.L, j0, st.p1);
-      const double lc = (double)__logf(S) + p.s_d * p.m[t];
-      if (threadIdx.x == 0) p.logc[t] = lc;
-      logz += lc;
-    } else if (t == t_c - 1 && s_in_dst) {
-      st.save_state(p, s_in_dst, j0);
+  // emission rows PF steps ahead (the sequential repair chain is latency-bound; the
+  // chunk-parallel kernels hide latency across waves and use PF = 1)
+  EmRaw<J> ring[PF];
+#pragma unroll
+  for (int q = 0; q < PF; ++q)
+    if (t0 + q < t_e) em_load<J>(p, t0 + q, j0, ring[q]);
+  for (int64_t tb = t0; tb < t_e; tb += PF) {
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int64_t t = tb + q;
+      if (t < t_e) {
+        float e[J];
+        em_exp<J>(p, j0, ring[q], e);
+        if (t + PF < t_e) em_load<J>(p, t + PF, j0, ring[q]);
+        const float S = st.step(tm, p, lds, j0, invz, e);
+        if (t >= t_c) {
+          float* arow = p.alpha + t * 2 * (int64_t)p.L;
+          store_row<J>(arow, p.L, j0, st.p0);
+          store_row<J>(arow + p.L, p.L, j0, st.p1);
+          const double lc = (double)__logf(S) + p.s_d * p.m[t];
+          if (threadIdx.x == 0) p.logc[t] = lc;
+          logz += lc;
+        } else if (t == t_c - 1 && s_in_dst) {
+          st.save_state(p, s_in_dst, j0);
+        }
+      }
     }
   }
   return logz;
@@ -470,7 +480,7 @@ __global__ void __launch_bounds__(64 * repair_nw<J>()) k_forward_repair(FBParams
     const int64_t t_c = (int64_t)c * p.C;
     const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
     st.save_state(p, p.s_in + (size_t)c * SZ, j0);
-    const double lz = fwd_run(tm, p, st, lds, j0, invz, t_c, t_c, t_e, (float*)nullptr);
+    const double lz = fwd_run<JB, WP, BlockTeam<NW>, 16 / JB>(tm, p, st, lds, j0, invz, t_c, t_c, t_e, (float*)nullptr);
     float* sout = p.s_out + (size_t)c * SZ;
     const float d = hilbert_reg<JB>(tm, st.p0, st.p1, sout, p.Lpad, j0);
     changed = !(d <= p.tol);
@@ -588,64 +598,88 @@ __device__ __forceinline__ void bwd_plain(Team& tm, const FBParams& p, Bwd<J, WP
 
 // output steps t = t_e-1 .. t_c.  On entry st holds beta_{t_e-1} and (vp0, vp1) the v that
 // produced it (has_prev false at the sequence end).  Writes beta_{t_c} to bf (registers).
-template <int J, int WP, class Team>
+template <int J>
+struct BwdRow {
+  EmRaw<J> em;
+  float a0[J], a1[J];
+};
+
+template <int J>
+__device__ __forceinline__ void bwd_row_load(const FBParams& p, int64_t t, int j0, BwdRow<J>& r) {
+  em_load<J>(p, t, j0, r.em);
+  const float* arow = p.alpha_in + t * 2 * (int64_t)p.L;
+  load_row<J>(arow, p.L, j0, r.a0);
+  load_row<J>(arow + p.L, p.L, j0, r.a1);
+}
+
+template <int J, int WP, class Team, int PF = 1>
 __device__ void bwd_out(Team& tm, const FBParams& p, Bwd<J, WP, Team>& st, float* lds, int j0,
                         const float invz[J], int64_t t_c, int64_t t_e, float vp0[J], float vp1[J],
                         bool has_prev, float bf0[J], float bf1[J]) {
   const int64_t L = p.L;
-  for (int64_t t = t_e - 1; t >= t_c; --t) {
-    EmRaw<J> r;
-    em_load<J>(p, t, j0, r);
-    float a0[J], a1[J];
-    const float* arow = p.alpha_in + t * 2 * L;
-    load_row<J>(arow, p.L, j0, a0);
-    load_row<J>(arow + L, p.L, j0, a1);
-    float e[J];
-    em_exp<J>(p, j0, r, e);
-    float G = 0.f, V0 = 0.f, V1 = 0.f;
+  BwdRow<J> ring[PF];
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
-      a0[j] *= st.b0[j];
-      a1[j] *= st.b1[j];
-      G += a0[j] + a1[j];
-      V0 += e[j] * st.b0[j];
-      V1 += e[j] * st.b1[j];
-    }
-    tm.sum2(V0, V1);
-    G = tm.sum(G);
-    const float iG = 1.f / G;
-    float pp[J];
+  for (int q = 0; q < PF; ++q)
+    if (t_e - 1 - q >= t_c) bwd_row_load<J>(p, t_e - 1 - q, j0, ring[q]);
+  for (int64_t tb = t_e - 1; tb >= t_c; tb -= PF) {
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
-      a0[j] *= iG;
-      a1[j] *= iG;
-      pp[j] = a0[j] + a1[j];
-    }
-    if (p.P) store_row<J>(p.P + t * L, p.L, j0, pp);
-    if (p.gamma) {
-      store_row<J>(p.gamma + t * 2 * L, p.L, j0, a0);
-      store_row<J>(p.gamma + t * 2 * L + L, p.L, j0, a1);
-    }
-    if (p.rho && has_prev && t + 1 < p.T) {  // rho_{t+1} = v_{t+1} / sum(alpha_t * beta_t)
-      float r0[J], r1[J];
+    for (int q = 0; q < PF; ++q) {
+      const int64_t t = tb - q;
+      if (t >= t_c) {
+        float a0[J], a1[J], e[J];
 #pragma unroll
-      for (int j = 0; j < J; ++j) {
-        r0[j] = vp0[j] * iG;
-        r1[j] = vp1[j] * iG;
+        for (int j = 0; j < J; ++j) {
+          a0[j] = ring[q].a0[j];
+          a1[j] = ring[q].a1[j];
+        }
+        em_exp<J>(p, j0, ring[q].em, e);
+        if (t - PF >= t_c) bwd_row_load<J>(p, t - PF, j0, ring[q]);
+        float G = 0.f, V0 = 0.f, V1 = 0.f;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+          a0[j] *= st.b0[j];
+          a1[j] *= st.b1[j];
+          G += a0[j] + a1[j];
+          V0 += e[j] * st.b0[j];
+          V1 += e[j] * st.b1[j];
+        }
+        tm.sum2(V0, V1);
+        G = tm.sum(G);
+        const float iG = 1.f / G;
+        float pp[J];
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+          a0[j] *= iG;
+          a1[j] *= iG;
+          pp[j] = a0[j] + a1[j];
+        }
+        if (p.P) store_row<J>(p.P + t * L, p.L, j0, pp);
+        if (p.gamma) {
+          store_row<J>(p.gamma + t * 2 * L, p.L, j0, a0);
+          store_row<J>(p.gamma + t * 2 * L + L, p.L, j0, a1);
+        }
+        if (p.rho && has_prev && t + 1 < p.T) {  // rho_{t+1} = v_{t+1} / sum(alpha_t * beta_t)
+          float r0[J], r1[J];
+#pragma unroll
+          for (int j = 0; j < J; ++j) {
+            r0[j] = vp0[j] * iG;
+            r1[j] = vp1[j] * iG;
+          }
+          store_row<J>(p.rho + (t + 1) * 2 * L, p.L, j0, r0);
+          store_row<J>(p.rho + (t + 1) * 2 * L + L, p.L, j0, r1);
+        }
+        if (t == t_c) {
+#pragma unroll
+          for (int j = 0; j < J; ++j) {
+            bf0[j] = st.b0[j];
+            bf1[j] = st.b1[j];
+          }
+        } else {
+          st.step_back(p, lds, j0, invz, e, V0, V1, vp0, vp1);
+          has_prev = true;
+        }
       }
-      store_row<J>(p.rho + (t + 1) * 2 * L, p.L, j0, r0);
-      store_row<J>(p.rho + (t + 1) * 2 * L + L, p.L, j0, r1);
     }
-    if (t == t_c) {
-#pragma unroll
-      for (int j = 0; j < J; ++j) {
-        bf0[j] = st.b0[j];
-        bf1[j] = st.b1[j];
-      }
-      break;
-    }
-    st.step_back(p, lds, j0, invz, e, V0, V1, vp0, vp1);
-    has_prev = true;
   }
 }
 
@@ -732,7 +766,7 @@ __global__ void __launch_bounds__(64 * repair_nw<J>()) k_backward_repair(FBParam
     float vp0[JB], vp1[JB];
     bwd_plain(tm, p, st, lds, j0, invz, t_e, vp0, vp1);
     float bf0[JB], bf1[JB];
-    bwd_out(tm, p, st, lds, j0, invz, t_c, t_e, vp0, vp1, true, bf0, bf1);
+    bwd_out<JB, WP, BlockTeam<NW>, 16 / JB>(tm, p, st, lds, j0, invz, t_c, t_e, vp0, vp1, true, bf0, bf1);
     float* bf = p.b_first + (size_t)c * SZ;
     const float d = hilbert_reg<JB>(tm, bf0, bf1, bf, p.Lpad, j0);
     changed = !(d <= p.tol);

@@ -18,6 +18,9 @@
 // "stop after body j" from the globally summed partials of iteration j (summed in
 // the same fixed order by every workgroup, hence identical decisions); a small
 // ring of (W, mu, nu) states lets it return exactly the state after body j+1.
+#include <stdio.h>
+#include <stdlib.h>
+
 #include "pmg_common.h"
 
 namespace pmg {
@@ -51,7 +54,11 @@ struct AdamParams {
   unsigned long long* gpart;  // [..][G]
   double* ring;               // [G][kRing][3][NBM*4] (W, mu, nu) after each body
   int* timeout;
+  long long* prof;            // optional (PMG_ADAM_PROF): s_memtime stamps of WG 0, bodies < 64
 };
+
+#define PMG_ADAM_STAMP(k, i)                                                   \
+  if (p.prof && g == 0 && tid == 0 && (k) < 64) p.prof[(k) * 8 + (i)] = __builtin_amdgcn_s_memtime();
 
 // signalling NaN with a payload: no arithmetic result has this bit pattern
 constexpr unsigned long long kSentinel = 0x7FF4DEADBEEF0001ull;
@@ -162,20 +169,35 @@ struct BasisSplit {
   static constexpr int STRIDE = NBL > 0 ? NBL + 4 : 4;
 };
 
+// Threads: thread = latent row (L <= 512).  Per body: rows (f, G, B^T G partials) |
+// barrier | Adam element update (threads < NB*S, i.e. the first waves) while the LAST
+// wave, which owns no weight, runs the stop-rule decision pipeline | barrier |
+// publish.  The stop flag is seen by every wave right after the second barrier.
+//
+// f = softplus(F), F = B W_k, is needed to f64 accuracy (the factor y_w/f - t_w
+// cancels near the optimum).  F is carried per (row, neuron) in f64 registers and
+// advanced by the f32 product B (W_k - W_{k-1}) of the small Adam step (error ~1e-9
+// per body), and recomputed exactly in f64 every kRefresh bodies.
+constexpr int kNW = kThreads / 64;          // waves (the last one also runs the decision)
+constexpr int kThreadsAll = kThreads;
+constexpr int kRefresh = 16;
+
 template <int NBM, int LGM, int SP>
-__global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
+__global__ void __launch_bounds__(kThreadsAll) k_adam(AdamParams p) {
   using BS = BasisSplit<NBM>;
   constexpr int NBR = BS::NBR, NBL = BS::NBL, STRIDE = BS::STRIDE;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sBl = smem;                                   // [kThreads][STRIDE]
-  double* sW = reinterpret_cast<double*>(sBl + kThreads * STRIDE);  // [NBM][4] current W (f64)
-  float* sRed = reinterpret_cast<float*>(sW + NBM * kSMax);         // [8 waves][NBM][4] partial B^T G
-  double* sSum = reinterpret_cast<double*>(sRed + (kThreads / 64) * NBM * kSMax);  // [2][8]
-  double* sYw = sSum + 2 * (kThreads / 64);                                         // [kThreads][4]
-  int* sCtl = reinterpret_cast<int*>(sYw + kThreads * kSMax);                       // [4]
+  float* sBl = smem;                                                   // [kThreads][STRIDE]
+  double* sW = reinterpret_cast<double*>(sBl + kThreads * STRIDE);     // [4][NBM] W_k (f64)
+  float* sD = reinterpret_cast<float*>(sW + NBM * kSMax);              // [4][NBM] W_k - W_{k-1}
+  float* sRed = sD + NBM * kSMax;                                      // [kNW][NBM][4] partial B^T G
+  double* sSum = reinterpret_cast<double*>(sRed + kNW * NBM * kSMax);  // [2][kNW]
+  double* sYw = sSum + 2 * kNW;                                        // [kThreads][4]
+  int* sCtl = reinterpret_cast<int*>(sYw + kThreads * kSMax);          // [4]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
+  const bool ctl = wid == kNW - 1;                     // runs the decision pipeline
   const int g = blockIdx.x;
   const int n0 = g * p.S;
   const int S = (p.N - n0) < p.S ? (p.N - n0) : p.S;  // neurons owned
@@ -194,12 +216,14 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
   }
   double twd = 0.0;
   for (int s = 0; s < kSMax; ++s)
-    sYw[tid * kSMax + s] = (is_row && s < S) ? p.yw[(size_t)tid * p.N + n0 + s] : 0.0;
+      sYw[tid * kSMax + s] = (is_row && s < S) ? p.yw[(size_t)tid * p.N + n0 + s] : 0.0;
   if (is_row) twd = p.tw[tid];
-  const float twf = (float)twd;
   const int ek = tid % NB, en = tid / NB;
   const bool is_el = en < S;
-  for (int q = tid; q < NBM * kSMax; q += blockDim.x) sW[q] = 0.0;
+  for (int q = tid; q < NBM * kSMax; q += blockDim.x) {
+    sW[q] = 0.0;
+    sD[q] = 0.f;
+  }
   if (tid < 4) sCtl[tid] = 0;
   // element state (W, mu, nu) of this thread's weight, and its global ring
   double w_cur = 0.0, mu_cur = 0.0, nu_cur = 0.0;
@@ -211,7 +235,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
     w_cur = p.W[o];
     mu_cur = p.mu[o];
     nu_cur = p.nu[o];
-    sW[e] = w_cur;
+    sW[en * NBM + ek] = w_cur;
     ring[(0 * 3 + 0) * NBM * kSMax + e] = w_cur;
     ring[(0 * 3 + 1) * NBM * kSMax + e] = mu_cur;
     ring[(0 * 3 + 2) * NBM * kSMax + e] = nu_cur;
@@ -220,83 +244,111 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
   double b1t = pow(p.b1, (double)count0), b2t = pow(p.b2, (double)count0);
   __syncthreads();
 
+  // control-wave state
   double loss_prev = 0.0, loss0 = 0.0;
-  int dj = 0;                              // next body to decide (wave 0)
+  int dj = 0;                              // next body to decide
   unsigned long long lv0[kPartPerLane];    // body dj loss partials (in flight)
   unsigned long long lv1[kPartPerLane];    // body dj+1
   bool issued0 = false, issued1 = false;
   double fin_loss = 0.0;
   const int maxiter = p.maxiter;
   const bool eval_only = maxiter <= 1;
+  // running F of this row for neurons 0..3 (f64)
+  double F0 = 0.0, F1 = 0.0, F2 = 0.0, F3 = 0.0;
 
   for (int k = 0;; ++k) {
     // ---- body k: evaluate at W_k ---------------------------------------------
+    PMG_ADAM_STAMP(k, 0)
     double lpart = 0.0;
-    // neurons one at a time (runtime loop, not unrolled: one neuron's registers live)
+    {
+      const bool exact = (k % kRefresh) == 0;
+      // neurons one at a time (runtime loop, not unrolled: one neuron's registers live)
 #pragma unroll 1
-    for (int s = 0; s < S; ++s) {
-      // F = B W in f64 (f32 basis x f64 weights): the gradient factor
-      // (y_w/f - t_w) cancels near the optimum, so f must be f64-accurate.
-      double F = 0.0;
+      for (int s = 0; s < S; ++s) {
+        double F;
+        if (exact) {
+          F = 0.0;
 #pragma unroll
-      for (int q = 0; q < NBR; ++q) {
-        asm volatile("" : "+v"(brow[q]));   // keep the f32->f64 conversion local (no hoisted f64 copy)
-        F = fma((double)brow[q], sW[q * kSMax + s], F);
-      }
+          for (int q = 0; q < NBR; ++q) {
+            asm volatile("" : "+v"(brow[q]));   // keep the f32->f64 conversion local
+            F = fma((double)brow[q], sW[s * NBM + q], F);
+          }
 #pragma unroll 2
-      for (int q4 = 0; q4 < NBL; q4 += 4) {
-        const float4 b4 = *reinterpret_cast<const float4*>(&sBl[tid * STRIDE + q4]);
-        F = fma((double)b4.x, sW[(NBR + q4) * kSMax + s], F);
-        F = fma((double)b4.y, sW[(NBR + q4 + 1) * kSMax + s], F);
-        F = fma((double)b4.z, sW[(NBR + q4 + 2) * kSMax + s], F);
-        F = fma((double)b4.w, sW[(NBR + q4 + 3) * kSMax + s], F);
-      }
-      const double ywd = is_row ? sYw[tid * kSMax + s] : 0.0;
-      // softplus / sigmoid in f32 at Fh = f32(F), corrected to first order in the
-      // exact residual r = F - Fh (|r| <= 2^-24 |F|): f = softplus(Fh) + sigmoid(Fh) r
-      const float Fh = (float)F;
-      const double r = F - (double)Fh;
-      const float f32 = fmaxf(Fh, 0.f) + log1pf(expf(-fabsf(Fh)));
-      const float sg = 1.f / (1.f + expf(-Fh));
-      const double fd = (double)f32 + (double)sg * r;
-      const float gr = is_row ? (float)((ywd / (fd + 1e-20) - twd) * (double)sg) : 0.f;
-      if (is_row) {
-        const double xl = (ywd != 0.0) ? ywd * ((double)logf(f32 + 1e-20f) + (double)sg * r / (double)f32) : 0.0;
-        lpart -= xl - fd * twd;
-      }
-      // per-wave partial of B^T G for this neuron, 32 columns per chunk
-      float* sr = &sRed[(wid * NBM) * kSMax] + s;
-      ChunkLoop<0, NBR, 0>::run(brow, gr, sr, lane);
+          for (int q4 = 0; q4 < NBL; q4 += 4) {
+            const float4 b4 = *reinterpret_cast<const float4*>(&sBl[tid * STRIDE + q4]);
+            F = fma((double)b4.x, sW[s * NBM + NBR + q4], F);
+            F = fma((double)b4.y, sW[s * NBM + NBR + q4 + 1], F);
+            F = fma((double)b4.z, sW[s * NBM + NBR + q4 + 2], F);
+            F = fma((double)b4.w, sW[s * NBM + NBR + q4 + 3], F);
+          }
+        } else {
+          float dF = 0.f;
 #pragma unroll
-      for (int c0 = 0; c0 < NBL; c0 += 32) {
-        float bl[32];
+          for (int q = 0; q < NBR; ++q) dF = fmaf(brow[q], sD[s * NBM + q], dF);
 #pragma unroll
-        for (int q4 = 0; q4 < 32; q4 += 4) {
-          const float4 b4 = (c0 + q4 < NBL)
-                                ? *reinterpret_cast<const float4*>(&sBl[tid * STRIDE + c0 + q4])
-                                : make_float4(0.f, 0.f, 0.f, 0.f);
-          bl[q4] = b4.x;
-          bl[q4 + 1] = b4.y;
-          bl[q4 + 2] = b4.z;
-          bl[q4 + 3] = b4.w;
+          for (int q4 = 0; q4 < NBL; q4 += 4) {
+            const float4 b4 = *reinterpret_cast<const float4*>(&sBl[tid * STRIDE + q4]);
+            const float4 d4 = *reinterpret_cast<const float4*>(&sD[s * NBM + NBR + q4]);
+            dF = fmaf(b4.x, d4.x, dF);
+            dF = fmaf(b4.y, d4.y, dF);
+            dF = fmaf(b4.z, d4.z, dF);
+            dF = fmaf(b4.w, d4.w, dF);
+          }
+          F = (s == 0 ? F0 : s == 1 ? F1 : s == 2 ? F2 : F3) + (double)dF;
         }
-        const float gg[1] = {gr};
-        const float red = wave_products_reduce32<1, 0, 32>(bl, gg);
-        const int v = c0 + bitrev5(lane & 31);
-        if (lane < 32 && v < NBL) sr[(NBR + v) * kSMax] = red;
+        F0 = s == 0 ? F : F0;
+        F1 = s == 1 ? F : F1;
+        F2 = s == 2 ? F : F2;
+        F3 = s == 3 ? F : F3;
+        const double ywd = is_row ? sYw[tid * kSMax + s] : 0.0;
+        // softplus / sigmoid in f32 at Fh = f32(F), corrected to first order in the
+        // exact residual r = F - Fh (|r| <= 2^-24 |F|): f = softplus(Fh) + sigmoid(Fh) r
+        const float Fh = (float)F;
+        const double r = F - (double)Fh;
+        const float f32 = fmaxf(Fh, 0.f) + log1pf(expf(-fabsf(Fh)));
+        const float sg = 1.f / (1.f + expf(-Fh));
+        const double fd = (double)f32 + (double)sg * r;
+        const float gr = is_row ? (float)((ywd / (fd + 1e-20) - twd) * (double)sg) : 0.f;
+        if (is_row) {
+          const double xl = (ywd != 0.0) ? ywd * ((double)logf(f32 + 1e-20f) + (double)sg * r / (double)f32) : 0.0;
+          lpart -= xl - fd * twd;
+        }
+        // per-wave partial of B^T G for this neuron, 32 columns per chunk
+        float* sr = &sRed[(wid * NBM) * kSMax] + s;
+        ChunkLoop<0, NBR, 0>::run(brow, gr, sr, lane);
+#pragma unroll
+        for (int c0 = 0; c0 < NBL; c0 += 32) {
+          float bl[32];
+#pragma unroll
+          for (int q4 = 0; q4 < 32; q4 += 4) {
+            const float4 b4 = (c0 + q4 < NBL)
+                                  ? *reinterpret_cast<const float4*>(&sBl[tid * STRIDE + c0 + q4])
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+            bl[q4] = b4.x;
+            bl[q4 + 1] = b4.y;
+            bl[q4 + 2] = b4.z;
+            bl[q4 + 3] = b4.w;
+          }
+          const float gg[1] = {gr};
+          const float red = wave_products_reduce32<1, 0, 32>(bl, gg);
+          const int v = c0 + bitrev5(lane & 31);
+          if (lane < 32 && v < NBL) sr[(NBR + v) * kSMax] = red;
+        }
       }
     }
+    PMG_ADAM_STAMP(k, 1)
     PMG_LDS_BARRIER();
+    PMG_ADAM_STAMP(k, 2)
     double gsq = 0.0;
     b1t *= p.b1;
     b2t *= p.b2;
     if (is_el) {
       float gsum = 0.f;
-      const int nw = (int)(blockDim.x >> 6);
-      for (int q = 0; q < nw; ++q) gsum += sRed[(q * NBM) * kSMax + e];
+      for (int q = 0; q < kNW; ++q) gsum += sRed[(q * NBM) * kSMax + e];
       const double gr = -(double)gsum + w_cur * isd2;
       gsq = gr * gr;
       lpart += 0.5 * w_cur * w_cur * isd2 + lconst;
+      const double w_old = w_cur;
       if (!eval_only) {  // optax 0.2.2 scale_by_adam + scale(-lr)
         const double mu = (1.0 - p.b1) * gr + p.b1 * mu_cur;
         const double nu = (1.0 - p.b2) * gr * gr + p.b2 * nu_cur;
@@ -310,36 +362,26 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
       ring[(ns * 3 + 0) * NBM * kSMax + e] = w_cur;
       ring[(ns * 3 + 1) * NBM * kSMax + e] = mu_cur;
       ring[(ns * 3 + 2) * NBM * kSMax + e] = nu_cur;
-      sW[e] = w_cur;
+      sW[en * NBM + ek] = w_cur;
+      sD[en * NBM + ek] = (float)(w_cur - w_old);
     }
     lpart = wave_sum_f64(lpart);
     gsq = wave_sum_f64(gsq);
     if (lane == 0) {
       sSum[wid] = lpart;
-      sSum[(kThreads / 64) + wid] = gsq;
+      sSum[kNW + wid] = gsq;
     }
-    PMG_LDS_BARRIER();
-    if (tid == 0) {
-      double a = 0.0, b = 0.0;
-      for (int q = 0; q < (int)(blockDim.x >> 6); ++q) {
-        a += sSum[q];
-        b += sSum[(kThreads / 64) + q];
-      }
-      st_sc1(&p.lpart[(size_t)k * p.G + g], a);
-      st_sc1(&p.gpart[(size_t)k * p.G + g], b);
-    }
-
-    // ---- decision pipeline (wave 0) -------------------------------------------
-    // Partials are pre-filled with a signalling-NaN sentinel (never produced by
-    // arithmetic) and each is written once by one 8-byte atomic store, so a load
-    // returns either the sentinel (not published yet) or the final value.  Loads for
-    // bodies dj and dj+1 are issued in one body and consumed in the next, so the
-    // cross-XCD latency overlaps the following body's arithmetic; only when the
-    // pipeline is kLag bodies behind does wave 0 block (bounded spin).
-    if (wid == 0) {
+    if (ctl && k > 0) {
+      // ---- decision pipeline (control wave) over bodies dj .. k-1 ---------------
+      // Partials are pre-filled with a signalling-NaN sentinel (never produced by
+      // arithmetic) and each is written once by one 8-byte atomic store, so a load
+      // returns either the sentinel (not published yet) or the final value.  Loads
+      // for bodies dj and dj+1 are kept in flight across bodies; the wave blocks
+      // (bounded spin) only when the pipeline is kLag bodies behind.
+      const int last = k - 1;                // latest body this workgroup has published
       for (int rep = 0; rep < 2; ++rep) {
-        const bool must = eval_only || (k - dj) >= kLag;
-        if (!issued0 || dj > k) break;
+        const bool must = eval_only || (last - dj) >= kLag;
+        if (!issued0 || dj > last) break;
         bool ok = true;
 #pragma unroll
         for (int q = 0; q < kPartPerLane; ++q) ok &= (lv0[q] != kSentinel);
@@ -392,19 +434,30 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
         issued0 = issued1;
         issued1 = false;
       }
-      if (!sCtl[0]) {  // keep bodies dj and dj+1 in flight (both <= k)
-        if (!issued0 && dj <= k) {
+      if (!sCtl[0]) {  // keep bodies dj and dj+1 in flight (both <= last)
+        if (!issued0 && dj <= last) {
           load_parts(p, dj, lane, lv0);
           issued0 = true;
         }
-        if (!issued1 && dj + 1 <= k) {
+        if (!issued1 && dj + 1 <= last) {
           load_parts(p, dj + 1, lane, lv1);
           issued1 = true;
         }
       }
     }
+    PMG_ADAM_STAMP(k, 3)
     PMG_LDS_BARRIER();
     if (sCtl[0] || sCtl[2]) break;
+    if (tid == 0) {
+      double a = 0.0, b = 0.0;
+      for (int q = 0; q < kNW; ++q) {
+        a += sSum[q];
+        b += sSum[kNW + q];
+      }
+      st_sc1(&p.lpart[(size_t)k * p.G + g], a);
+      st_sc1(&p.gpart[(size_t)k * p.G + g], b);
+    }
+    PMG_ADAM_STAMP(k, 4)
   }
   const int stop_j = sCtl[1];
   // ---- write the state after body stop_j (W_{stop_j+1}) from the ring ---------
@@ -415,7 +468,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
     p.mu[o] = ring[(fs * 3 + 1) * NBM * kSMax + e];
     p.nu[o] = ring[(fs * 3 + 2) * NBM * kSMax + e];
   }
-  if (g == 0 && tid == 0 && !sCtl[2]) {
+  if (g == 0 && ctl && lane == 0 && !sCtl[2]) {
     const int n_iter = eval_only ? 1 : stop_j + 2;
     p.stats[0] = (double)n_iter;
     p.stats[1] = fin_loss;
@@ -427,9 +480,9 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
 template <int NBM>
 static size_t adam_lds_bytes() {
   using BS = BasisSplit<NBM>;
-  return sizeof(float) * ((size_t)kThreads * BS::STRIDE + 2 * NBM * kSMax +
-                          (kThreads / 64) * NBM * kSMax) +
-         sizeof(double) * (2 * (kThreads / 64) + kThreads * kSMax) + sizeof(int) * 4 + 64;
+  return sizeof(float) * ((size_t)kThreads * BS::STRIDE + 2 * NBM * kSMax + NBM * kSMax +
+                          kNW * NBM * kSMax) +
+         sizeof(double) * (2 * kNW + kThreads * kSMax) + sizeof(int) * 4 + 64;
 }
 
 // Histories (fit_tuning_helper.py:147-149, :175-176) from the published partials, summed
@@ -597,10 +650,36 @@ int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const floa
   if (kern.lds > 64 * 1024)
     PMG_HIP(hipFuncSetAttribute((const void*)kern.fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)kern.lds));
-  hipLaunchKernelGGL(kern.fn, dim3(G), dim3(kThreads), kern.lds, st, p);
+  static long long* prof_buf = nullptr;   // debug: per-phase stamps (PMG_ADAM_PROF set)
+  const bool prof = getenv("PMG_ADAM_PROF") != nullptr;
+  if (prof) {
+    if (!prof_buf) PMG_HIP(hipMalloc(&prof_buf, 64 * 8 * sizeof(long long)));
+    PMG_HIP(hipMemsetAsync(prof_buf, 0, 64 * 8 * sizeof(long long), st));
+    p.prof = prof_buf;
+  } else {
+    p.prof = nullptr;
+  }
+  hipLaunchKernelGGL(kern.fn, dim3(G), dim3(kThreadsAll), kern.lds, st, p);
   PMG_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_adam_hist, dim3(64), dim3(64), 0, st, p);
   PMG_LAUNCH_CHECK();
+  if (prof) {
+    long long h[64 * 8];
+    PMG_HIP(hipMemcpyAsync(h, prof_buf, sizeof(h), hipMemcpyDeviceToHost, st));
+    PMG_HIP(hipStreamSynchronize(st));
+    double acc[5] = {0, 0, 0, 0, 0};
+    int n = 0;
+    for (int k = 8; k + 1 < 64; ++k) {   // skip the pipeline fill
+      if (h[k * 8 + 4] == 0 || h[(k + 1) * 8] == 0) break;
+      for (int i = 0; i < 4; ++i) acc[i] += (double)(h[k * 8 + i + 1] - h[k * 8 + i]);
+      acc[4] += (double)(h[(k + 1) * 8] - h[k * 8 + 4]);
+      ++n;
+    }
+    if (n > 0)
+      fprintf(stderr, "[pmg adam prof] bodies=%d ticks/body: rows %.0f | bar1 %.0f | update %.0f | "
+              "sums+bar2+publish %.0f | loop %.0f\n", n, acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n,
+              acc[4] / n);
+  }
   return PMG_OK;
 }
 

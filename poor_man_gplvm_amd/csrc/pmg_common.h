@@ -133,12 +133,28 @@ __device__ __forceinline__ float half_max32(float v) {
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
-// f64 reductions via shuffles (used off the critical path)
-__device__ __forceinline__ double wave_sum_f64(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// f64 DPP: both 32-bit halves moved by the same DPP control
+template <int CTRL, int ROWMASK = 0xf, int BANKMASK = 0xf>
+__device__ __forceinline__ double dppd(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROWMASK, BANKMASK, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROWMASK, BANKMASK, false);
+  return __hiloint2double(hi, lo);
 }
+
+// f64 wave sum, same DPP stage pattern as wave_sum (no LDS round trips), result in
+// every lane (readlane of lane 63)
+__device__ __forceinline__ double wave_sum_f64(double v) {
+  v += dppd<0xB1>(v);
+  v += dppd<0x4E>(v);
+  v += dppd<0x141>(v);
+  v += dppd<0x140>(v);
+  v += dppd<0x142, 0xa>(v);
+  v += dppd<0x143, 0xc>(v);
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), 63);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
+  return __hiloint2double(hi, lo);
+}
+// f64 reductions via shuffles (used off the critical path)
 __device__ __forceinline__ double wave_max_f64(double v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
