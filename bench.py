@@ -32,7 +32,8 @@ CONFIGS = {
     "c5": (256, 50000, 256),
 }
 PEAK_HBM_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
-PEAK_FP32_MFMA_TFLOPS = 157.3    # dense FP32 matrix (spec)
+PEAK_FP32_TFLOPS = 157.3         # dense FP32 matrix / packed vector (spec)
+PEAK_BF16_MFMA_TFLOPS = 2500.0   # dense bf16 MFMA (spec, no sparsity)
 PEAK_I8_MFMA_TOPS = 5000.0       # dense int8 MFMA (= fp8 rate, spec)
 
 
@@ -167,22 +168,39 @@ def main():
     adam_iters = float(np.mean(s[args.warmup:, 0])) if args.steps else 0.0
     repairs = eng.repairs()
 
-    # roofline of the dominant kernel (largest mean time per EM iteration)
-    Lc = L
+    # per-kernel rooflines (SURVEY.md 8(d) algorithmic units per launch); the top-level
+    # `roofline` is the dominant kernel (largest mean time per EM iteration)
     nblk = (L + 31) // 32
-    bytes_fwd = T * Lc * 4 + T * nblk * 4 + T * 8 + T * 2 * Lc * 4 + T * 8
-    bytes_bwd = T * Lc * 4 + T * nblk * 4 + T * 2 * Lc * 4 + T * Lc * 4
-    flops_ss = 2.0 * T * L * (N + 1)
-    ops_em = 2.0 * T * L * N
-    roof = {
-        "forward_filter": ("hbm", bytes_fwd / 1e9, PEAK_HBM_GBS, "GB/s"),
-        "backward_smoother": ("hbm", bytes_bwd / 1e9, PEAK_HBM_GBS, "GB/s"),
-        "suffstats": ("mfma", flops_ss / 1e12, PEAK_FP32_MFMA_TFLOPS, "TFLOP/s"),
-        "emission": ("mfma", ops_em / 1e12, PEAK_I8_MFMA_TOPS, "TFLOP/s"),
+    NB = B.shape[1]
+    units = {
+        # section: (kernel, bound, algorithmic units per launch, unit scale, peak, unit)
+        "forward_filter": ("k_forward", "hbm", 12.0 * T * L + 4.0 * T * nblk + 16.0 * T, 1e9, PEAK_HBM_GBS, "GB/s"),
+        "backward_smoother": ("k_backward", "hbm", 16.0 * T * L + 4.0 * T * nblk, 1e9, PEAK_HBM_GBS, "GB/s"),
+        "suffstats": ("k_ptb3", "mfma", 2.0 * T * L * N, 1e12, PEAK_BF16_MFMA_TFLOPS, "TFLOP/s"),
+        "emission": ("k_emission_i8", "mfma", 2.0 * T * L * N, 1e12, PEAK_I8_MFMA_TOPS, "TFLOP/s"),
+        "mstep_adam": ("k_adam", "mfma", 4.0 * L * NB * N * adam_iters, 1e12, PEAK_FP32_TFLOPS, "TFLOP/s"),
     }
-    dom = max((k for k in summ if k in roof), key=lambda k: summ[k][1])
-    bound, units_per_launch, peak, unit = roof[dom]
-    achieved = units_per_launch / (summ[dom][1] / 1e3)
+    pmc = {}
+    pmc_path = os.path.join(ROOT, "profiles", f"r01_pmc_{args.config}.json")
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as fh:
+            pmc = json.load(fh).get("kernels", {})
+    rooflines = {}
+    for sec, (kname, bound, units_per_launch, scale, peak, unit) in units.items():
+        if sec not in summ:
+            continue
+        t_ms = summ[sec][1]
+        achieved = units_per_launch / scale / (t_ms / 1e3)
+        tr = pmc.get(kname, {}).get("hbm_bytes_per_launch")
+        rooflines[sec] = {"kernel": kname, "bound": bound, "achieved": achieved, "peak": peak, "unit": unit,
+                          "frac": achieved / peak, "traffic": tr, "ms": round(t_ms, 4),
+                          "algorithmic_per_launch": units_per_launch}
+    dom = max(rooflines, key=lambda k: rooflines[k]["ms"])
+    roof_dom = dict(rooflines[dom])
+    roof_dom.pop("ms")
+    roof_dom.pop("algorithmic_per_launch")
+    t_fb = summ["forward_filter"][1] + summ["backward_smoother"][1]
+    B_fb = 28.0 * T * L
     value = world * args.steps / elapsed
     out = {
         "metric": "EM iters/sec at N=512, T=1e5, B=512; fwd-bwd achieved HBM GB/s",
@@ -200,10 +218,11 @@ def main():
         "config": {"workload": f"{args.config}: PoissonGPLVMJump1D.fit_em N={N} T={T} L={L} "
                                f"nb={B.shape[1]} (one EM iteration per step; ranks = independent restarts)",
                    "n_neuron": N, "n_time": T, "n_latent_bin": L, "parallelism": f"restarts x{world}"},
-        "roofline": {"kernel": dom, "bound": bound, "achieved": achieved, "peak": peak, "unit": unit,
-                     "frac": achieved / peak, "traffic": None},
+        "roofline": roof_dom,
+        "rooflines": rooflines,
         "kernels_ms": {k: round(v[1], 4) for k, v in summ.items()},
-        "fwd_bwd_GBps": (bytes_fwd + bytes_bwd) / 1e9 / ((summ["forward_filter"][1] + summ["backward_smoother"][1]) / 1e3),
+        "fwd_bwd_GBps": B_fb / 1e9 / (t_fb / 1e3),
+        "fwd_bwd_frac_hbm": B_fb / 1e9 / (t_fb / 1e3) / PEAK_HBM_GBS,
         "adam_iters_mean": adam_iters,
         "chunk": eng.C,
         "repairs_last": repairs,

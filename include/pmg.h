@@ -141,6 +141,17 @@ int pmg_backward_smoother(const float* delta, const float* phi, const float* alp
                           const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                           int32_t warmup, double tol, float* P, float* gamma, float* rho,
                           void* workspace, size_t workspace_bytes, void* stream);
+/* The same two calls split in phases (1 = the chunk-parallel main pass,   */
+/* 2 = boundary verification, repair rounds and, forward, the logZ sum;    */
+/* 3 = both = the calls above).  Lets a caller time the main kernel alone. */
+int pmg_forward_filter_phase(const float* delta, const float* phi, const double* m, int64_t T,
+                             const pmg_transition* tr, double likelihood_scale, int32_t chunk,
+                             int32_t warmup, double tol, float* alpha, double* logc, double* logz,
+                             void* workspace, size_t workspace_bytes, void* stream, int32_t phase);
+int pmg_backward_smoother_phase(const float* delta, const float* phi, const float* alpha, int64_t T,
+                                const pmg_transition* tr, double likelihood_scale, int32_t chunk,
+                                int32_t warmup, double tol, float* P, float* gamma, float* rho,
+                                void* workspace, size_t workspace_bytes, void* stream, int32_t phase);
 /* number of chunks repaired by the last forward / backward call on this  */
 /* workspace (device int32 pair at a fixed offset; host reads it lazily). */
 size_t pmg_fwdbwd_repair_counter_offset(int64_t T, int32_t L, int32_t chunk);

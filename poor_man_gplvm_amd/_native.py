@@ -25,6 +25,7 @@ EXPORTED_SYMBOLS = (
     "pmg_emission_workspace_size", "pmg_emission_poisson", "pmg_emission_poisson_f64",
     "pmg_emission_rowref", "pmg_loglik_materialize", "pmg_fwdbwd_workspace_size",
     "pmg_forward_filter", "pmg_backward_smoother", "pmg_fwdbwd_repair_counter_offset",
+    "pmg_forward_filter_phase", "pmg_backward_smoother_phase",
     "pmg_suffstats_workspace_size", "pmg_suffstats", "pmg_exp", "pmg_log",
     "pmg_spikes_bf16t", "pmg_suffstats_bf16_workspace_size", "pmg_suffstats_bf16",
     "pmg_mstep_workspace_size", "pmg_mstep_adam", "pmg_joint_workspace_size",
@@ -70,6 +71,10 @@ _SIGS = {
     "pmg_fwdbwd_workspace_size": ([_I64, _I32, _I32], _SZ),
     "pmg_forward_filter": ([_P, _P, _P, _I64, ctypes.POINTER(Transition), _D, _I32, _I32, _D,
                             _P, _P, _P, _P, _SZ, _P], _I32),
+    "pmg_forward_filter_phase": ([_P, _P, _P, _I64, ctypes.POINTER(Transition), _D, _I32, _I32, _D,
+                                  _P, _P, _P, _P, _SZ, _P, _I32], _I32),
+    "pmg_backward_smoother_phase": ([_P, _P, _P, _I64, ctypes.POINTER(Transition), _D, _I32, _I32, _D,
+                                     _P, _P, _P, _P, _SZ, _P, _I32], _I32),
     "pmg_backward_smoother": ([_P, _P, _P, _I64, ctypes.POINTER(Transition), _D, _I32, _I32, _D,
                                _P, _P, _P, _P, _SZ, _P], _I32),
     "pmg_fwdbwd_repair_counter_offset": ([_I64, _I32, _I32], _SZ),

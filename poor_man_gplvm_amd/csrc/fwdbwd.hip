@@ -927,10 +927,11 @@ size_t pmg_fwdbwd_repair_counter_offset(int64_t T, int32_t L, int32_t chunk) {
   return 0;  // repairs[0] (forward), repairs[1] (backward) at the workspace start
 }
 
-int pmg_forward_filter(const float* delta, const float* phi, const double* m, int64_t T,
-                       const pmg_transition* tr, double likelihood_scale, int32_t chunk,
-                       int32_t warmup, double tol, float* alpha, double* logc, double* logz,
-                       void* workspace, size_t workspace_bytes, void* stream) {
+// phase: 1 = speculative chunk-parallel pass, 2 = verify / repair / logZ, 3 = both
+static int forward_impl(const float* delta, const float* phi, const double* m, int64_t T,
+                        const pmg_transition* tr, double likelihood_scale, int32_t chunk,
+                        int32_t warmup, double tol, float* alpha, double* logc, double* logz,
+                        void* workspace, size_t workspace_bytes, void* stream, int phase) {
   FBParams p;
   int rc = fill_params(p, tr, T, chunk, warmup, likelihood_scale, tol);
   if (rc) return rc;
@@ -953,34 +954,55 @@ int pmg_forward_filter(const float* delta, const float* phi, const double* m, in
   fb_kernel_t kf = k_forward_table(J, WP), kfix = k_forward_fix_table(J, WP),
               kr = k_forward_repair_table(J, WP);
   PMG_REQUIRE(kf && kfix && kr, "pmg_forward_filter: no kernel for J=%d WP=%d", J, WP);
-  PMG_HIP(hipMemsetAsync(w.repairs, 0, sizeof(int), st));
-  hipLaunchKernelGGL(kf, dim3(p.M), dim3(64), 0, st, p);
-  PMG_LAUNCH_CHECK();
-  if (p.M > 1) {
-    const int nver = p.M - 1;
-    const bool no_repair = getenv("PMG_DEBUG_NO_REPAIR") != nullptr;
-    for (int round = 0; round <= kFixRounds; ++round) {
-      hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4), dim3(256), 0, st, w.s_in,
-                         (const float*)w.s_out, 1, p.M - 1, -1, 2 * p.Lpad, p.tol, w.flags);
-      PMG_LAUNCH_CHECK();
-      if (no_repair) break;
-      if (round < kFixRounds) {
-        hipLaunchKernelGGL(kfix, dim3(p.M), dim3(64), 0, st, p);
-      } else {
-        hipLaunchKernelGGL(kr, dim3(1), dim3(64 * repair_nw_rt(J)), 0, st, p);
-      }
-      PMG_LAUNCH_CHECK();
-    }
+  if (phase & 1) {
+    PMG_HIP(hipMemsetAsync(w.repairs, 0, sizeof(int), st));
+    hipLaunchKernelGGL(kf, dim3(p.M), dim3(64), 0, st, p);
+    PMG_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(k_sum_f64, dim3(1), dim3(256), 0, st, (const double*)w.chunk_logz, p.M, logz);
-  PMG_LAUNCH_CHECK();
+  if (phase & 2) {
+    if (p.M > 1) {
+      const int nver = p.M - 1;
+      const bool no_repair = getenv("PMG_DEBUG_NO_REPAIR") != nullptr;
+      for (int round = 0; round <= kFixRounds; ++round) {
+        hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4), dim3(256), 0, st, w.s_in,
+                           (const float*)w.s_out, 1, p.M - 1, -1, 2 * p.Lpad, p.tol, w.flags);
+        PMG_LAUNCH_CHECK();
+        if (no_repair) break;
+        if (round < kFixRounds) {
+          hipLaunchKernelGGL(kfix, dim3(p.M), dim3(64), 0, st, p);
+        } else {
+          hipLaunchKernelGGL(kr, dim3(1), dim3(64 * repair_nw_rt(J)), 0, st, p);
+        }
+        PMG_LAUNCH_CHECK();
+      }
+    }
+    hipLaunchKernelGGL(k_sum_f64, dim3(1), dim3(256), 0, st, (const double*)w.chunk_logz, p.M, logz);
+    PMG_LAUNCH_CHECK();
+  }
   return PMG_OK;
 }
 
-int pmg_backward_smoother(const float* delta, const float* phi, const float* alpha, int64_t T,
-                          const pmg_transition* tr, double likelihood_scale, int32_t chunk,
-                          int32_t warmup, double tol, float* P, float* gamma, float* rho,
-                          void* workspace, size_t workspace_bytes, void* stream) {
+int pmg_forward_filter(const float* delta, const float* phi, const double* m, int64_t T,
+                       const pmg_transition* tr, double likelihood_scale, int32_t chunk,
+                       int32_t warmup, double tol, float* alpha, double* logc, double* logz,
+                       void* workspace, size_t workspace_bytes, void* stream) {
+  return forward_impl(delta, phi, m, T, tr, likelihood_scale, chunk, warmup, tol, alpha, logc, logz,
+                      workspace, workspace_bytes, stream, 3);
+}
+
+int pmg_forward_filter_phase(const float* delta, const float* phi, const double* m, int64_t T,
+                             const pmg_transition* tr, double likelihood_scale, int32_t chunk,
+                             int32_t warmup, double tol, float* alpha, double* logc, double* logz,
+                             void* workspace, size_t workspace_bytes, void* stream, int32_t phase) {
+  PMG_REQUIRE(phase >= 1 && phase <= 3, "pmg_forward_filter_phase: phase %d", phase);
+  return forward_impl(delta, phi, m, T, tr, likelihood_scale, chunk, warmup, tol, alpha, logc, logz,
+                      workspace, workspace_bytes, stream, phase);
+}
+
+static int backward_impl(const float* delta, const float* phi, const float* alpha, int64_t T,
+                         const pmg_transition* tr, double likelihood_scale, int32_t chunk,
+                         int32_t warmup, double tol, float* P, float* gamma, float* rho,
+                         void* workspace, size_t workspace_bytes, void* stream, int phase) {
   FBParams p;
   int rc = fill_params(p, tr, T, chunk, warmup, likelihood_scale, tol);
   if (rc) return rc;
@@ -1003,10 +1025,12 @@ int pmg_backward_smoother(const float* delta, const float* phi, const float* alp
   fb_kernel_t kb = k_backward_table(J, WP), kfix = k_backward_fix_table(J, WP),
               kr = k_backward_repair_table(J, WP);
   PMG_REQUIRE(kb && kfix && kr, "pmg_backward_smoother: no kernel for J=%d WP=%d", J, WP);
-  PMG_HIP(hipMemsetAsync(w.repairs + 1, 0, sizeof(int), st));
-  hipLaunchKernelGGL(kb, dim3(p.M), dim3(64), 0, st, p);
-  PMG_LAUNCH_CHECK();
-  if (p.M > 1) {
+  if (phase & 1) {
+    PMG_HIP(hipMemsetAsync(w.repairs + 1, 0, sizeof(int), st));
+    hipLaunchKernelGGL(kb, dim3(p.M), dim3(64), 0, st, p);
+    PMG_LAUNCH_CHECK();
+  }
+  if ((phase & 2) && p.M > 1) {
     const int nver = p.M - 1;
     const bool no_repair = getenv("PMG_DEBUG_NO_REPAIR") != nullptr;
     for (int round = 0; round <= kFixRounds; ++round) {
@@ -1023,6 +1047,23 @@ int pmg_backward_smoother(const float* delta, const float* phi, const float* alp
     }
   }
   return PMG_OK;
+}
+
+int pmg_backward_smoother(const float* delta, const float* phi, const float* alpha, int64_t T,
+                          const pmg_transition* tr, double likelihood_scale, int32_t chunk,
+                          int32_t warmup, double tol, float* P, float* gamma, float* rho,
+                          void* workspace, size_t workspace_bytes, void* stream) {
+  return backward_impl(delta, phi, alpha, T, tr, likelihood_scale, chunk, warmup, tol, P, gamma, rho,
+                       workspace, workspace_bytes, stream, 3);
+}
+
+int pmg_backward_smoother_phase(const float* delta, const float* phi, const float* alpha, int64_t T,
+                                const pmg_transition* tr, double likelihood_scale, int32_t chunk,
+                                int32_t warmup, double tol, float* P, float* gamma, float* rho,
+                                void* workspace, size_t workspace_bytes, void* stream, int32_t phase) {
+  PMG_REQUIRE(phase >= 1 && phase <= 3, "pmg_backward_smoother_phase: phase %d", phase);
+  return backward_impl(delta, phi, alpha, T, tr, likelihood_scale, chunk, warmup, tol, P, gamma, rho,
+                       workspace, workspace_bytes, stream, phase);
 }
 
 }  // extern "C"

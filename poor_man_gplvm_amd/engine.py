@@ -346,22 +346,25 @@ class DeviceEM:
     def forward(self, likelihood_scale, logz_out):
         self._adapt_warmup()
         sc = self.scan
-        with self._t('forward_filter'):
-          nat.check(self.lib.pmg_forward_filter(nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.mref), self.T,
-                                              ctypes.byref(self._tr_c), float(likelihood_scale), self.C,
-                                              int(self.warm[0]), float(sc.tol), nat.ptr(self.alpha),
-                                              nat.ptr(self.logc), nat.ptr(logz_out), nat.ptr(self.ws_fb),
-                                              self.ws_fb.numel(), nat.stream_handle()), "pmg_forward_filter")
+        args = (nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.mref), self.T, ctypes.byref(self._tr_c),
+                float(likelihood_scale), self.C, int(self.warm[0]), float(sc.tol), nat.ptr(self.alpha),
+                nat.ptr(self.logc), nat.ptr(logz_out), nat.ptr(self.ws_fb), self.ws_fb.numel(),
+                nat.stream_handle())
+        with self._t('forward_filter'):          # main chunk-parallel pass (k_forward)
+            nat.check(self.lib.pmg_forward_filter_phase(*args, 1), "pmg_forward_filter")
+        with self._t('forward_repair'):          # verify / repair rounds / logZ
+            nat.check(self.lib.pmg_forward_filter_phase(*args, 2), "pmg_forward_filter")
 
     def backward(self, likelihood_scale, P=True, gamma=None, rho=None):
         sc = self.scan
-        with self._t('backward_smoother'):
-          nat.check(self.lib.pmg_backward_smoother(nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.alpha),
-                                                 self.T, ctypes.byref(self._tr_c), float(likelihood_scale),
-                                                 self.C, int(self.warm[1]), float(sc.tol),
-                                                 nat.ptr(self.P) if P else None, nat.ptr(gamma), nat.ptr(rho),
-                                                 nat.ptr(self.ws_fb), self.ws_fb.numel(), nat.stream_handle()),
-                  "pmg_backward_smoother")
+        args = (nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.alpha), self.T, ctypes.byref(self._tr_c),
+                float(likelihood_scale), self.C, int(self.warm[1]), float(sc.tol),
+                nat.ptr(self.P) if P else None, nat.ptr(gamma), nat.ptr(rho), nat.ptr(self.ws_fb),
+                self.ws_fb.numel(), nat.stream_handle())
+        with self._t('backward_smoother'):       # main chunk-parallel pass (k_backward)
+            nat.check(self.lib.pmg_backward_smoother_phase(*args, 1), "pmg_backward_smoother")
+        with self._t('backward_repair'):         # verify / repair rounds
+            nat.check(self.lib.pmg_backward_smoother_phase(*args, 2), "pmg_backward_smoother")
 
     def e_step(self, likelihood_scale, logz_out, gamma=None, rho=None):
         self.emission(likelihood_scale)
