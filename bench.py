@@ -106,6 +106,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--warm-steps", type=int, default=48)
+    ap.add_argument("--warm-fb", type=str, default="", help="fixed forward,backward warm-up (no adaptation)")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
 
@@ -124,11 +125,13 @@ def main():
     N, T, L = CONFIGS[args.config]
     y, B, W0, lp0 = synth(N, T, L, rank=rank)
     dev = torch.device("cuda", local)
-    scan = ScanConfig(chunk=args.chunk or None, warmup=args.warm_steps)
+    scan = ScanConfig(chunk=args.chunk or None, warmup=args.warm_steps, adaptive=not args.warm_fb)
     sp = SpikeData(y)
     eng = DeviceEM(sp, L, basis=B, scan=scan)
     eng.set_transition(banded_transition(L, 1.0, 0.01, 0.01))
     eng.set_log_posterior(lp0)
+    if args.warm_fb:
+        eng.warm = [int(v) for v in args.warm_fb.split(",")]
     adam = AdamConfig(lr=0.01, maxiter=1000, tol=1e-6, prior_std=1.0)
     W = torch.as_tensor(W0.astype(np.float64), device=dev).contiguous()
     mu, nu = torch.zeros_like(W), torch.zeros_like(W)

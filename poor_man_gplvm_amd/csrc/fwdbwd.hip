@@ -206,26 +206,40 @@ struct BlockTeam {
 // Hilbert projective distance between two non-negative (2, Lpad) states held in
 // memory; components below 1e-30 of the max on both sides are ignored, a
 // component significant (> 1e-20) on one side only counts as a failure.
-__device__ float hilbert_dist(const float* __restrict__ x, const float* __restrict__ y, int n) {
+__device__ float hilbert_dist(const float* __restrict__ x, const float* __restrict__ y, int n,
+                              const float* __restrict__ w = nullptr, int L = 0, int Lpad = 0) {
   const int lane = threadIdx.x & 63;
+  // optional weights w in the (2, L) alpha-row layout for state index i = d*Lpad + j
+  auto wt = [&](int i) -> float {
+    if (!w) return 1.f;
+    const int d = i >= Lpad ? 1 : 0, j = i - d * Lpad;
+    return j < L ? w[d * L + j] : 0.f;
+  };
   float xm = 0.f, ym = 0.f;
   for (int i = lane; i < n; i += 64) {
-    xm = fmaxf(xm, x[i]);
-    ym = fmaxf(ym, y[i]);
+    const float wi = wt(i);
+    xm = fmaxf(xm, x[i] * wi);
+    ym = fmaxf(ym, y[i] * wi);
   }
   xm = wave_max_shfl(xm);
   ym = wave_max_shfl(ym);
   if (!(xm > 0.f) || !(ym > 0.f)) return INFINITY;
   const float ix = 1.f / xm, iy = 1.f / ym;
+  // unweighted (state space): ratios of components above 1e-30 of the max, a component
+  // above 1e-20 on one side only fails.  Weighted (posterior space, |posterior| <= 1):
+  // components below 1e-14 move no output by more than 1e-14 absolute (parity atol is
+  // 1e-12); above it the ratio spread bounds the relative error.
+  const float lo_thr = w ? 1e-14f : 1e-30f, hi_thr = w ? 1e-12f : 1e-20f;
   float lo = INFINITY, hi = -INFINITY;
   int bad = 0;
   for (int i = lane; i < n; i += 64) {
-    const float a = x[i] * ix, b = y[i] * iy;
-    if (a > 1e-30f && b > 1e-30f) {
+    const float wi = wt(i);
+    const float a = x[i] * wi * ix, b = y[i] * wi * iy;
+    if (a > lo_thr && b > lo_thr) {
       const float r = __logf(a) - __logf(b);
       lo = fminf(lo, r);
       hi = fmaxf(hi, r);
-    } else if (fmaxf(a, b) > 1e-20f) {
+    } else if (fmaxf(a, b) > hi_thr) {
       bad = 1;
     }
   }
@@ -496,16 +510,23 @@ __global__ void __launch_bounds__(64 * repair_nw<J>()) k_forward_repair(FBParams
 }
 
 // boundary verification: flags[c] = hilbert(x[c], y[c + off]) > tol; a failing
-// boundary also snapshots y[c + off] into x[c] (the restart state of the repair)
+// boundary also snapshots y[c + off] into x[c] (the restart state of the repair).
+// Backward (w != nullptr): both betas are weighted by alpha at the boundary time
+// t_e = (c+1) C, i.e. the POSTERIOR at t_e is compared.  An error of beta_{t_e}(j)
+// reaches gamma_t(i), t < t_e, only through the joint P(x_t = i, x_{t_e} = j) <=
+// gamma_{t_e}(j), so components with negligible posterior cannot move any output
+// above ~1e-18 probability, while they are exactly the ones the chain forgets slowly.
 __global__ void __launch_bounds__(256) k_verify(float* __restrict__ x, const float* __restrict__ y,
                                                 int first, int last, int off, int SZ, float tol,
-                                                int* __restrict__ flags) {
-  const int w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  const int c = first + w;
+                                                int* __restrict__ flags, const float* __restrict__ w,
+                                                int C, int L, int Lpad) {
+  const int wv = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int c = first + wv;
   if (c > last) return;
   const float* yc = y + (size_t)(c + off) * SZ;
   float* xc = x + (size_t)c * SZ;
-  const float d = hilbert_dist(xc, yc, SZ);
+  const float* wc = w ? w + (size_t)(c + 1) * C * 2 * L : nullptr;
+  const float d = hilbert_dist(xc, yc, SZ, wc, L, Lpad);
   const bool bad = !(d <= tol);
   if ((threadIdx.x & 63) == 0) flags[c] = bad ? 1 : 0;
   if (bad)
@@ -965,7 +986,8 @@ static int forward_impl(const float* delta, const float* phi, const double* m, i
       const bool no_repair = getenv("PMG_DEBUG_NO_REPAIR") != nullptr;
       for (int round = 0; round <= kFixRounds; ++round) {
         hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4), dim3(256), 0, st, w.s_in,
-                           (const float*)w.s_out, 1, p.M - 1, -1, 2 * p.Lpad, p.tol, w.flags);
+                           (const float*)w.s_out, 1, p.M - 1, -1, 2 * p.Lpad, p.tol, w.flags,
+                           (const float*)nullptr, 0, 0, 0);
         PMG_LAUNCH_CHECK();
         if (no_repair) break;
         if (round < kFixRounds) {
@@ -1035,7 +1057,8 @@ static int backward_impl(const float* delta, const float* phi, const float* alph
     const bool no_repair = getenv("PMG_DEBUG_NO_REPAIR") != nullptr;
     for (int round = 0; round <= kFixRounds; ++round) {
       hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4), dim3(256), 0, st, w.b_in,
-                         (const float*)w.b_first, 0, p.M - 2, 1, 2 * p.Lpad, p.tol, w.flags);
+                         (const float*)w.b_first, 0, p.M - 2, 1, 2 * p.Lpad, p.tol, w.flags,
+                         alpha, p.C, p.L, p.Lpad);
       PMG_LAUNCH_CHECK();
       if (no_repair) break;
       if (round < kFixRounds) {
