@@ -1,513 +1,9 @@
-// Time-parallel forward filter / backward smoother over the joint
-// (dynamics x latent) state of the jump GPLVM, gfx950.
-//
-// Reference (log-domain, strictly sequential lax.scan):
-//   filter_one_step   decoder.py:151-172   prior = LSE_i(LSE_d(post+logA)+logK); post = prior+s*ll - c
-//   smooth_one_step   decoder.py:200-226   acausal_t = LSE_{d',j}(logK+logA+(acausal_{t+1}-prior_{t+1})+post_t)
-//   chunk driver      decoder.py:258-332   carries (post[-1], logZ) forward, (acausal[0], joint) backward
-//
-// MI355X design:
-//   * linear space with per-step normalisation (exact up to fp32 rounding; states
-//     below ~1e-38 of the total flush to 0 -- probability-space outputs unchanged);
-//   * the continuous kernel is a row-normalised Toeplitz band K0[i,j] = g[|i-j|]/Z_i
-//     (exactly zero beyond |i-j| = band in the reference's f32), applied
-//     as a 1-D convolution through a per-wave LDS line; the jump kernel is rank-1
-//     (a wave reduction); the 2x2 dynamics mix is elementwise;
-//   * one wave per time chunk; each chunk starts from a uniform guess `warmup`
-//     steps early (HMM forgetting), then every chunk boundary is verified in the
-//     Hilbert projective metric (max-min of log ratios, a contraction of positive
-//     linear maps, so a boundary error <= tol bounds every later output's relative
-//     error by tol) and chunks that fail are recomputed exactly from their
-//     predecessor's state by a single-wave repair pass (rare; sequential only over
-//     consecutive failures);
-//   * the smoother uses the equivalent alpha-beta form gamma_t ~ alpha_t * beta_t
-//     with beta_{T-1} = 1 (the reference's RTS seed acausal_{T-1} = post_{T-1}), so
-//     the backward pass needs only alpha_t and the emission -- no stored priors.
-//
-// Emission input: e[t,l] = exp(s*delta[t,l] + phi[t,l/32]) = exp(s*(ll[t,l] - m[t])).
-#include <stdlib.h>
-
-#include "pmg_common.h"
+// Time-parallel forward filter / backward smoother: host dispatch, boundary
+// verification and the C ABI.  The device code is in fb_kernels.h; its template
+// instances are compiled per J in fb_inst_j*.hip.
+#include "fb_kernels.h"
 
 namespace pmg {
-
-constexpr int kMaxBand = 32;
-constexpr int kFixRounds = 2;  // parallel repair rounds before the sequential fallback
-
-struct FBParams {
-  const float* delta;
-  const float* phi;
-  const double* m;
-  int64_t T;
-  int L;
-  int nblk;
-  const float* invz;
-  float g[kMaxBand + 1];
-  float A00, A01, A10, A11;
-  float invL;
-  float s;
-  double s_d;
-  int C, B, M;
-  float tol;
-  // forward
-  float* alpha;
-  double* logc;
-  double* chunk_logz;
-  float* s_in;
-  float* s_out;
-  // backward
-  const float* alpha_in;
-  float* P;
-  float* gamma;
-  float* rho;
-  float* b_in;
-  float* b_first;
-  int* flags;
-  int* repairs;
-  int Lpad;  // 64*J
-};
-
-// ---------------------------------------------------------------------------
-// per-lane helpers (lane owns latents j0 .. j0+J-1, j0 = lane*J)
-// ---------------------------------------------------------------------------
-template <int J>
-__device__ __forceinline__ void load_row(const float* __restrict__ row, int L, int j0, float v[J]) {
-  if ((L & 3) == 0 && (J & 3) == 0 && j0 + J <= L) {
-#pragma unroll
-    for (int j = 0; j < J; j += 4) {
-      float4 q = *reinterpret_cast<const float4*>(row + j0 + j);
-      v[j] = q.x; v[j + 1] = q.y; v[j + 2] = q.z; v[j + 3] = q.w;
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < J; ++j) v[j] = (j0 + j < L) ? row[j0 + j] : 0.f;
-  }
-}
-
-template <int J>
-__device__ __forceinline__ void store_row(float* __restrict__ row, int L, int j0, const float v[J]) {
-  if ((L & 3) == 0 && (J & 3) == 0 && j0 + J <= L) {
-#pragma unroll
-    for (int j = 0; j < J; j += 4)
-      *reinterpret_cast<float4*>(row + j0 + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
-  } else {
-#pragma unroll
-    for (int j = 0; j < J; ++j)
-      if (j0 + j < L) row[j0 + j] = v[j];
-  }
-}
-
-// raw emission operands for one time step
-template <int J>
-struct EmRaw {
-  float d[J];
-  float ph;
-};
-
-template <int J>
-__device__ __forceinline__ void em_load(const FBParams& p, int64_t t, int j0, EmRaw<J>& r) {
-  load_row<J>(p.delta + t * p.L, p.L, j0, r.d);
-  const int b = j0 >> 5;
-  r.ph = (b < p.nblk) ? p.phi[t * p.nblk + b] : 0.f;
-}
-
-template <int J>
-__device__ __forceinline__ void em_exp(const FBParams& p, int j0, const EmRaw<J>& r, float e[J]) {
-#pragma unroll
-  for (int j = 0; j < J; ++j) e[j] = (j0 + j < p.L) ? exp_acc(fmaf(p.s, r.d[j], r.ph)) : 0.f;
-}
-
-// out[j] = sum_{k=-WP..WP} g[|k|] * in[j+k]  over the whole latent line (zero halo)
-template <int J, int WP>
-__device__ __forceinline__ void band_conv(const FBParams& p, float* lds, int j0, const float in[J],
-                                          float out[J]) {
-#pragma unroll
-  for (int j = 0; j < J; ++j) lds[WP + j0 + j] = in[j];
-  __syncthreads();
-  float win[J + 2 * WP];
-#pragma unroll
-  for (int k = 0; k < J + 2 * WP; ++k) win[k] = lds[j0 + k];
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    float acc = p.g[0] * win[j + WP];
-#pragma unroll
-    for (int k = 1; k <= WP; ++k) acc = fmaf(p.g[k], win[j + WP - k] + win[j + WP + k], acc);
-    out[j] = acc;
-  }
-  __syncthreads();
-}
-
-
-// ---------------------------------------------------------------------------
-// Teams: the threads that carry ONE chain.  The chunk-parallel kernels use one wave
-// per chunk (DPP reductions, no block barriers); the sequential repair of a long
-// cascade uses NW waves on the same chain (wave DPP + LDS partials behind a block
-// barrier; the scratch is double-buffered so one barrier per reduction suffices).
-// Thread t owns latents j0 = t*J .. t*J+J-1 in both cases.
-// ---------------------------------------------------------------------------
-struct WaveTeam {
-  static constexpr int NW = 1;
-  __device__ explicit WaveTeam(float*) {}
-  __device__ void sum2(float& a, float& b) { wave_sum2(a, b); }
-  __device__ float sum(float a) { return wave_sum(a); }
-  __device__ float vmax(float a) { return wave_max_shfl(a); }
-  __device__ float vmin(float a) { return wave_min_shfl(a); }
-  __device__ bool any(bool b) { return __ballot(b) != 0ull; }
-};
-
-template <int NW_>
-struct BlockTeam {
-  static constexpr int NW = NW_;
-  float* red;  // LDS scratch, 2 x 2 x NW floats
-  int buf = 0;
-  __device__ explicit BlockTeam(float* r) : red(r) {}
-  __device__ float* slot() {
-    float* r = red + buf * 2 * NW;
-    buf ^= 1;
-    return r;
-  }
-  __device__ void sum2(float& a, float& b) {
-    wave_sum2(a, b);
-    float* r = slot();
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-      r[w] = a;
-      r[NW + w] = b;
-    }
-    __syncthreads();
-    float A = 0.f, B = 0.f;
-#pragma unroll
-    for (int i = 0; i < NW; ++i) {
-      A += r[i];
-      B += r[NW + i];
-    }
-    a = A;
-    b = B;
-  }
-  __device__ float sum(float a) {
-    float b = 0.f;
-    sum2(a, b);
-    return a;
-  }
-  __device__ float vmax(float a) {
-    a = wave_max_shfl(a);
-    float* r = slot();
-    if ((threadIdx.x & 63) == 0) r[threadIdx.x >> 6] = a;
-    __syncthreads();
-    float m = r[0];
-#pragma unroll
-    for (int i = 1; i < NW; ++i) m = fmaxf(m, r[i]);
-    return m;
-  }
-  __device__ float vmin(float a) { return -vmax(-a); }
-  __device__ bool any(bool b) { return vmax(__ballot(b) ? 1.f : 0.f) > 0.f; }
-};
-
-// Hilbert projective distance between two non-negative (2, Lpad) states held in
-// memory; components below 1e-30 of the max on both sides are ignored, a
-// component significant (> 1e-20) on one side only counts as a failure.
-__device__ float hilbert_dist(const float* __restrict__ x, const float* __restrict__ y, int n,
-                              const float* __restrict__ w = nullptr, int L = 0, int Lpad = 0) {
-  const int lane = threadIdx.x & 63;
-  // optional weights w in the (2, L) alpha-row layout for state index i = d*Lpad + j
-  auto wt = [&](int i) -> float {
-    if (!w) return 1.f;
-    const int d = i >= Lpad ? 1 : 0, j = i - d * Lpad;
-    return j < L ? w[d * L + j] : 0.f;
-  };
-  float xm = 0.f, ym = 0.f;
-  for (int i = lane; i < n; i += 64) {
-    const float wi = wt(i);
-    xm = fmaxf(xm, x[i] * wi);
-    ym = fmaxf(ym, y[i] * wi);
-  }
-  xm = wave_max_shfl(xm);
-  ym = wave_max_shfl(ym);
-  if (!(xm > 0.f) || !(ym > 0.f)) return INFINITY;
-  const float ix = 1.f / xm, iy = 1.f / ym;
-  // unweighted (state space): ratios of components above 1e-30 of the max, a component
-  // above 1e-20 on one side only fails.  Weighted (posterior space, |posterior| <= 1):
-  // components below 1e-14 move no output by more than 1e-14 absolute (parity atol is
-  // 1e-12); above it the ratio spread bounds the relative error.
-  const float lo_thr = w ? 1e-14f : 1e-30f, hi_thr = w ? 1e-12f : 1e-20f;
-  float lo = INFINITY, hi = -INFINITY;
-  int bad = 0;
-  for (int i = lane; i < n; i += 64) {
-    const float wi = wt(i);
-    const float a = x[i] * wi * ix, b = y[i] * wi * iy;
-    if (a > lo_thr && b > lo_thr) {
-      const float r = __logf(a) - __logf(b);
-      lo = fminf(lo, r);
-      hi = fmaxf(hi, r);
-    } else if (fmaxf(a, b) > hi_thr) {
-      bad = 1;
-    }
-  }
-  lo = wave_min_shfl(lo);
-  hi = wave_max_shfl(hi);
-  if (__ballot(bad)) return INFINITY;
-  if (hi < lo) return 0.f;
-  return hi - lo;
-}
-
-// same metric, x held in registers with the (2, Lpad) lane layout, y in memory
-template <int J, class Team>
-__device__ float hilbert_reg(Team& tm, const float x0[J], const float x1[J], const float* __restrict__ y,
-                             int Lpad, int j0) {
-  float xm = 0.f, ym = 0.f;
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    xm = fmaxf(xm, fmaxf(x0[j], x1[j]));
-    ym = fmaxf(ym, fmaxf(y[j0 + j], y[Lpad + j0 + j]));
-  }
-  xm = tm.vmax(xm);
-  ym = tm.vmax(ym);
-  if (!(xm > 0.f) || !(ym > 0.f)) return INFINITY;
-  const float ix = 1.f / xm, iy = 1.f / ym;
-  float lo = INFINITY, hi = -INFINITY;
-  int bad = 0;
-#pragma unroll
-  for (int j = 0; j < 2 * J; ++j) {
-    const float a = (j < J ? x0[j] : x1[j - J]) * ix;
-    const float b = (j < J ? y[j0 + j] : y[Lpad + j0 + j - J]) * iy;
-    if (a > 1e-30f && b > 1e-30f) {
-      const float r = __logf(a) - __logf(b);
-      lo = fminf(lo, r);
-      hi = fmaxf(hi, r);
-    } else if (fmaxf(a, b) > 1e-20f) {
-      bad = 1;
-    }
-  }
-  lo = tm.vmin(lo);
-  hi = tm.vmax(hi);
-  if (tm.any(bad != 0)) return INFINITY;
-  if (hi < lo) return 0.f;
-  return hi - lo;
-}
-
-// ---------------------------------------------------------------------------
-// forward
-// ---------------------------------------------------------------------------
-template <int J, int WP, class Team = WaveTeam>
-struct Fwd {
-  float p0[J], p1[J];
-  float P0, P1;  // sum of p0, p1 (wave-uniform)
-
-  __device__ void init_uniform(const FBParams& p, int j0) {
-    const float u = 0.5f * p.invL;
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      p0[j] = (j0 + j < p.L) ? u : 0.f;
-      p1[j] = p0[j];
-    }
-    P0 = 0.5f;
-    P1 = 0.5f;
-  }
-  __device__ void load_state(Team& tm, const FBParams& p, const float* src, int j0) {
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      p0[j] = src[j0 + j];
-      p1[j] = src[p.Lpad + j0 + j];
-    }
-    float a = 0.f, b = 0.f;
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      a += p0[j];
-      b += p1[j];
-    }
-    tm.sum2(a, b);
-    const float inv = 1.f / (a + b);
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      p0[j] *= inv;
-      p1[j] *= inv;
-    }
-    P0 = a * inv;
-    P1 = b * inv;
-  }
-  __device__ void save_state(const FBParams& p, float* dst, int j0) const {
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      dst[j0 + j] = p0[j];
-      dst[p.Lpad + j0 + j] = p1[j];
-    }
-  }
-  // one filter step with emission e; returns the normaliser S
-  __device__ float step(Team& tm, const FBParams& p, float* lds, int j0, const float invz[J],
-                        const float e[J]) {
-    float a0[J];
-#pragma unroll
-    for (int j = 0; j < J; ++j) a0[j] = fmaf(p0[j], p.A00, p1[j] * p.A10) * invz[j];
-    const float jump = fmaf(p.A01, P0, p.A11 * P1) * p.invL;
-    float pr0[J];
-    band_conv<J, WP>(p, lds, j0, a0, pr0);
-    float U0 = 0.f, U1 = 0.f;
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      p0[j] = pr0[j] * e[j];
-      p1[j] = jump * e[j];
-      U0 += p0[j];
-      U1 += p1[j];
-    }
-    tm.sum2(U0, U1);
-    const float S = U0 + U1;
-    const float inv = 1.f / S;
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      p0[j] *= inv;
-      p1[j] *= inv;
-    }
-    P0 = U0 * inv;
-    P1 = U1 * inv;
-    return S;
-  }
-};
-
-// run forward from t0 (state initialised) to t_e; writes outputs for t >= t_c and the
-// state at t_c-1 into s_in_dst (if given)
-template <int J, int WP, class Team, int PF = 1>
-__device__ double fwd_run(Team& tm, const FBParams& p, Fwd<J, WP, Team>& st, float* lds, int j0,
-                          const float invz[J], int64_t t0, int64_t t_c, int64_t t_e, float* s_in_dst) {
-  double logz = 0.0;
-  if (t0 >= t_e) return 0.0;
-  // emission rows PF steps ahead (the sequential repair chain is latency-bound; the
-  // chunk-parallel kernels hide latency across waves and use PF = 1)
-  EmRaw<J> ring[PF];
-#pragma unroll
-  for (int q = 0; q < PF; ++q)
-    if (t0 + q < t_e) em_load<J>(p, t0 + q, j0, ring[q]);
-  for (int64_t tb = t0; tb < t_e; tb += PF) {
-#pragma unroll
-    for (int q = 0; q < PF; ++q) {
-      const int64_t t = tb + q;
-      if (t < t_e) {
-        float e[J];
-        em_exp<J>(p, j0, ring[q], e);
-        if (t + PF < t_e) em_load<J>(p, t + PF, j0, ring[q]);
-        const float S = st.step(tm, p, lds, j0, invz, e);
-        if (t >= t_c) {
-          float* arow = p.alpha + t * 2 * (int64_t)p.L;
-          store_row<J>(arow, p.L, j0, st.p0);
-          store_row<J>(arow + p.L, p.L, j0, st.p1);
-          const double lc = (double)__logf(S) + p.s_d * p.m[t];
-          if (threadIdx.x == 0) p.logc[t] = lc;
-          logz += lc;
-        } else if (t == t_c - 1 && s_in_dst) {
-          st.save_state(p, s_in_dst, j0);
-        }
-      }
-    }
-  }
-  return logz;
-}
-
-#define PMG_FB_PROLOGUE_T(JJ, NWW)                                      \
-  __shared__ __attribute__((aligned(16))) float lds[64 * (NWW) * (JJ) + 2 * WP + 4 * (NWW)]; \
-  float* team_red = lds + 64 * (NWW) * (JJ) + 2 * WP;                   \
-  const int lane = threadIdx.x & 63;                                    \
-  (void)lane;                                                           \
-  const int j0 = threadIdx.x * (JJ);                                    \
-  for (int k = threadIdx.x; k < 64 * (NWW) * (JJ) + 2 * WP; k += 64 * (NWW)) lds[k] = 0.f; \
-  __syncthreads();                                                      \
-  float invz[JJ];                                                       \
-  _Pragma("unroll") for (int j = 0; j < (JJ); ++j) invz[j] = (j0 + j < p.L) ? p.invz[j0 + j] : 0.f; \
-  const size_t SZ = (size_t)2 * p.Lpad;                                 \
-  (void)SZ;                                                             \
-  (void)team_red;
-
-#define PMG_FB_PROLOGUE                                                 \
-  __shared__ __attribute__((aligned(16))) float lds[64 * J + 2 * WP];  \
-  const int lane = threadIdx.x & 63;                                    \
-  const int j0 = lane * J;                                              \
-  WaveTeam tm(nullptr);                                                 \
-  for (int k = lane; k < 64 * J + 2 * WP; k += 64) lds[k] = 0.f;        \
-  __syncthreads();                                                      \
-  float invz[J];                                                        \
-  _Pragma("unroll") for (int j = 0; j < J; ++j) invz[j] = (j0 + j < p.L) ? p.invz[j0 + j] : 0.f; \
-  const size_t SZ = (size_t)2 * p.Lpad;                                 \
-  (void)SZ;
-
-// speculative pass: chunk c starts `B` steps early from a uniform guess
-template <int J, int WP>
-__global__ void __launch_bounds__(64) k_forward(FBParams p) {
-  const int c = blockIdx.x;
-  if (c >= p.M) return;
-  PMG_FB_PROLOGUE
-  const int64_t t_c = (int64_t)c * p.C;
-  const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
-  int64_t t0 = (c == 0) ? 0 : t_c - p.B;
-  if (t0 < 0) t0 = 0;
-  Fwd<J, WP> st;
-  st.init_uniform(p, j0);
-  float* sin = p.s_in + (size_t)c * SZ;
-  if (c > 0 && t0 == t_c) st.save_state(p, sin, j0);  // no warm-up: the guess itself
-  const double lz = fwd_run(tm, p, st, lds, j0, invz, t0, t_c, t_e, c > 0 ? sin : nullptr);
-  st.save_state(p, p.s_out + (size_t)c * SZ, j0);
-  if (lane == 0) p.chunk_logz[c] = lz;
-}
-
-// parallel repair round: every flagged chunk restarts from its snapshot s_in[c]
-template <int J, int WP>
-__global__ void __launch_bounds__(64) k_forward_fix(FBParams p) {
-  const int c = blockIdx.x;
-  if (c >= p.M || c == 0 || p.flags[c] == 0) return;
-  PMG_FB_PROLOGUE
-  const int64_t t_c = (int64_t)c * p.C;
-  const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
-  Fwd<J, WP> st;
-  st.load_state(tm, p, p.s_in + (size_t)c * SZ, j0);
-  const double lz = fwd_run(tm, p, st, lds, j0, invz, t_c, t_c, t_e, nullptr);
-  st.save_state(p, p.s_out + (size_t)c * SZ, j0);
-  if (lane == 0) {
-    p.chunk_logz[c] = lz;
-    atomicAdd(&p.repairs[0], 1);
-  }
-}
-
-// sequential fallback for whatever is still flagged after the parallel rounds.  A long
-// cascade (slowly forgetting chain, e.g. the flat tuning of the first EM iterations)
-// is latency-critical, so NW waves carry the one chain (J/NW latents per thread).
-template <int J> constexpr int repair_nw() { return J >= 8 ? 8 : J; }
-
-template <int J, int WP>
-__global__ void __launch_bounds__(64 * repair_nw<J>()) k_forward_repair(FBParams p) {
-  constexpr int NW = repair_nw<J>(), JB = J / NW;
-  PMG_FB_PROLOGUE_T(JB, NW)
-  BlockTeam<NW> tm(team_red);
-  int repairs = 0;
-  bool changed = false;
-  int c = 1;
-  Fwd<JB, WP, BlockTeam<NW>> st;
-  while (c < p.M) {
-    if (!changed) {  // jump to the next flagged chunk, 64 flags at a time (every wave alike)
-      int found = -1;
-      for (int base = c; base < p.M && found < 0; base += 64) {
-        const int idx = base + lane;
-        const bool f = idx < p.M && p.flags[idx] != 0;
-        const unsigned long long bal = __ballot(f);
-        if (bal) found = base + (int)__builtin_ctzll(bal);
-      }
-      if (found < 0) break;
-      c = found;
-      st.load_state(tm, p, p.s_out + (size_t)(c - 1) * SZ, j0);
-    }
-    const int64_t t_c = (int64_t)c * p.C;
-    const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
-    st.save_state(p, p.s_in + (size_t)c * SZ, j0);
-    const double lz = fwd_run<JB, WP, BlockTeam<NW>, 16 / JB>(tm, p, st, lds, j0, invz, t_c, t_c, t_e, (float*)nullptr);
-    float* sout = p.s_out + (size_t)c * SZ;
-    const float d = hilbert_reg<JB>(tm, st.p0, st.p1, sout, p.Lpad, j0);
-    changed = !(d <= p.tol);
-    __syncthreads();  // every wave has read sout before it is overwritten
-    st.save_state(p, sout, j0);
-    if (threadIdx.x == 0) p.chunk_logz[c] = lz;
-    __threadfence();
-    __syncthreads();
-    ++repairs;
-    ++c;
-  }
-  if (threadIdx.x == 0) p.repairs[0] += repairs;
-}
 
 // boundary verification: flags[c] = hilbert(x[c], y[c + off]) > tol; a failing
 // boundary also snapshots y[c + off] into x[c] (the restart state of the repair).
@@ -544,265 +40,6 @@ __global__ void k_sum_f64(const double* __restrict__ x, int n, double* __restric
     __syncthreads();
   }
   if (threadIdx.x == 0) out[0] = sm[0];
-}
-
-// ---------------------------------------------------------------------------
-// backward (beta recursion).  Every step back uses the same arithmetic
-//   v = e_t * beta_t / sum(e_t * beta_t),  beta_{t-1} = Trans(v)
-// on the warm-up and on the output path, so two chunks that have converged to
-// the same beta produce bit-identical continuations (as the forward does).
-// ---------------------------------------------------------------------------
-template <int J, int WP, class Team = WaveTeam>
-struct Bwd {
-  float b0[J], b1[J];  // beta at the current time
-
-  __device__ void init_ones(const FBParams& p, int j0) {
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      b0[j] = (j0 + j < p.L) ? 1.f : 0.f;
-      b1[j] = b0[j];
-    }
-  }
-  __device__ void load_state(const FBParams& p, const float* src, int j0) {
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      b0[j] = src[j0 + j];
-      b1[j] = src[p.Lpad + j0 + j];
-    }
-  }
-  __device__ void save_state(const FBParams& p, float* dst, int j0) const {
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      dst[j0 + j] = b0[j];
-      dst[p.Lpad + j0 + j] = b1[j];
-    }
-  }
-  // v = e*beta scaled by 1/(V0+V1) (returned in v0/v1); beta <- Trans(v)
-  __device__ void step_back(const FBParams& p, float* lds, int j0, const float invz[J],
-                            const float e[J], float V0, float V1, float v0[J], float v1[J]) {
-    const float sc = 1.f / (V0 + V1);
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      v0[j] = e[j] * b0[j] * sc;
-      v1[j] = e[j] * b1[j] * sc;
-    }
-    float w0[J];
-    band_conv<J, WP>(p, lds, j0, v0, w0);
-    const float w1 = V1 * sc * p.invL;
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      const float c0 = w0[j] * invz[j];
-      const float real = (j0 + j < p.L) ? 1.f : 0.f;
-      b0[j] = fmaf(p.A00, c0, p.A01 * w1) * real;
-      b1[j] = fmaf(p.A10, c0, p.A11 * w1) * real;
-    }
-  }
-};
-
-// one plain backward step at time t (beta_t -> beta_{t-1}); v kept in (v0, v1)
-template <int J, int WP, class Team>
-__device__ __forceinline__ void bwd_plain(Team& tm, const FBParams& p, Bwd<J, WP, Team>& st, float* lds,
-                                          int j0, const float invz[J], int64_t t, float v0[J], float v1[J]) {
-  EmRaw<J> r;
-  em_load<J>(p, t, j0, r);
-  float e[J];
-  em_exp<J>(p, j0, r, e);
-  float V0 = 0.f, V1 = 0.f;
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    V0 += e[j] * st.b0[j];
-    V1 += e[j] * st.b1[j];
-  }
-  tm.sum2(V0, V1);
-  st.step_back(p, lds, j0, invz, e, V0, V1, v0, v1);
-}
-
-// output steps t = t_e-1 .. t_c.  On entry st holds beta_{t_e-1} and (vp0, vp1) the v that
-// produced it (has_prev false at the sequence end).  Writes beta_{t_c} to bf (registers).
-template <int J>
-struct BwdRow {
-  EmRaw<J> em;
-  float a0[J], a1[J];
-};
-
-template <int J>
-__device__ __forceinline__ void bwd_row_load(const FBParams& p, int64_t t, int j0, BwdRow<J>& r) {
-  em_load<J>(p, t, j0, r.em);
-  const float* arow = p.alpha_in + t * 2 * (int64_t)p.L;
-  load_row<J>(arow, p.L, j0, r.a0);
-  load_row<J>(arow + p.L, p.L, j0, r.a1);
-}
-
-template <int J, int WP, class Team, int PF = 1>
-__device__ void bwd_out(Team& tm, const FBParams& p, Bwd<J, WP, Team>& st, float* lds, int j0,
-                        const float invz[J], int64_t t_c, int64_t t_e, float vp0[J], float vp1[J],
-                        bool has_prev, float bf0[J], float bf1[J]) {
-  const int64_t L = p.L;
-  BwdRow<J> ring[PF];
-#pragma unroll
-  for (int q = 0; q < PF; ++q)
-    if (t_e - 1 - q >= t_c) bwd_row_load<J>(p, t_e - 1 - q, j0, ring[q]);
-  for (int64_t tb = t_e - 1; tb >= t_c; tb -= PF) {
-#pragma unroll
-    for (int q = 0; q < PF; ++q) {
-      const int64_t t = tb - q;
-      if (t >= t_c) {
-        float a0[J], a1[J], e[J];
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-          a0[j] = ring[q].a0[j];
-          a1[j] = ring[q].a1[j];
-        }
-        em_exp<J>(p, j0, ring[q].em, e);
-        if (t - PF >= t_c) bwd_row_load<J>(p, t - PF, j0, ring[q]);
-        float G = 0.f, V0 = 0.f, V1 = 0.f;
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-          a0[j] *= st.b0[j];
-          a1[j] *= st.b1[j];
-          G += a0[j] + a1[j];
-          V0 += e[j] * st.b0[j];
-          V1 += e[j] * st.b1[j];
-        }
-        tm.sum2(V0, V1);
-        G = tm.sum(G);
-        const float iG = 1.f / G;
-        float pp[J];
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-          a0[j] *= iG;
-          a1[j] *= iG;
-          pp[j] = a0[j] + a1[j];
-        }
-        if (p.P) store_row<J>(p.P + t * L, p.L, j0, pp);
-        if (p.gamma) {
-          store_row<J>(p.gamma + t * 2 * L, p.L, j0, a0);
-          store_row<J>(p.gamma + t * 2 * L + L, p.L, j0, a1);
-        }
-        if (p.rho && has_prev && t + 1 < p.T) {  // rho_{t+1} = v_{t+1} / sum(alpha_t * beta_t)
-          float r0[J], r1[J];
-#pragma unroll
-          for (int j = 0; j < J; ++j) {
-            r0[j] = vp0[j] * iG;
-            r1[j] = vp1[j] * iG;
-          }
-          store_row<J>(p.rho + (t + 1) * 2 * L, p.L, j0, r0);
-          store_row<J>(p.rho + (t + 1) * 2 * L + L, p.L, j0, r1);
-        }
-        if (t == t_c) {
-#pragma unroll
-          for (int j = 0; j < J; ++j) {
-            bf0[j] = st.b0[j];
-            bf1[j] = st.b1[j];
-          }
-        } else {
-          st.step_back(p, lds, j0, invz, e, V0, V1, vp0, vp1);
-          has_prev = true;
-        }
-      }
-    }
-  }
-}
-
-template <int J, int WP>
-__global__ void __launch_bounds__(64) k_backward(FBParams p) {
-  const int c = blockIdx.x;
-  if (c >= p.M) return;
-  PMG_FB_PROLOGUE
-  const int64_t t_c = (int64_t)c * p.C;
-  const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
-  Bwd<J, WP> st;
-  st.init_ones(p, j0);
-  float vp0[J], vp1[J];
-#pragma unroll
-  for (int j = 0; j < J; ++j) vp0[j] = vp1[j] = 0.f;
-  bool has_prev = false;
-  if (c < p.M - 1) {
-    int64_t t_w = t_e + p.B;  // beta guess (ones) at t_w, exact when t_w is the last bin
-    if (t_w > p.T - 1) t_w = p.T - 1;
-    for (int64_t t = t_w; t > t_e; --t) bwd_plain(tm, p, st, lds, j0, invz, t, vp0, vp1);
-    st.save_state(p, p.b_in + (size_t)c * SZ, j0);                 // beta_{t_e}
-    bwd_plain(tm, p, st, lds, j0, invz, t_e, vp0, vp1);          // -> beta_{t_e-1}
-    has_prev = true;
-  }
-  float bf0[J], bf1[J];
-  bwd_out(tm, p, st, lds, j0, invz, t_c, t_e, vp0, vp1, has_prev, bf0, bf1);
-  float* bf = p.b_first + (size_t)c * SZ;
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    bf[j0 + j] = bf0[j];
-    bf[p.Lpad + j0 + j] = bf1[j];
-  }
-}
-
-// parallel repair round: flagged chunk c restarts from its snapshot b_in[c] = beta_{t_e}
-template <int J, int WP>
-__global__ void __launch_bounds__(64) k_backward_fix(FBParams p) {
-  const int c = blockIdx.x;
-  if (c >= p.M - 1 || p.flags[c] == 0) return;
-  PMG_FB_PROLOGUE
-  const int64_t t_c = (int64_t)c * p.C;
-  const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
-  Bwd<J, WP> st;
-  st.load_state(p, p.b_in + (size_t)c * SZ, j0);
-  float vp0[J], vp1[J];
-  bwd_plain(tm, p, st, lds, j0, invz, t_e, vp0, vp1);
-  float bf0[J], bf1[J];
-  bwd_out(tm, p, st, lds, j0, invz, t_c, t_e, vp0, vp1, true, bf0, bf1);
-  float* bf = p.b_first + (size_t)c * SZ;
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    bf[j0 + j] = bf0[j];
-    bf[p.Lpad + j0 + j] = bf1[j];
-  }
-  if (lane == 0) atomicAdd(&p.repairs[1], 1);
-}
-
-// sequential fallback (descending chunks), NW waves on the one chain
-template <int J, int WP>
-__global__ void __launch_bounds__(64 * repair_nw<J>()) k_backward_repair(FBParams p) {
-  constexpr int NW = repair_nw<J>(), JB = J / NW;
-  PMG_FB_PROLOGUE_T(JB, NW)
-  BlockTeam<NW> tm(team_red);
-  int repairs = 0;
-  bool changed = false;
-  int c = p.M - 2;
-  while (c >= 0) {
-    if (!changed) {
-      int found = -1;
-      for (int top = c; top >= 0 && found < 0; top -= 64) {
-        const int idx = top - lane;
-        const bool f = idx >= 0 && p.flags[idx] != 0;
-        const unsigned long long bal = __ballot(f);
-        if (bal) found = top - (int)__builtin_ctzll(bal);
-      }
-      if (found < 0) break;
-      c = found;
-    }
-    const int64_t t_c = (int64_t)c * p.C;
-    const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
-    Bwd<JB, WP, BlockTeam<NW>> st;
-    st.load_state(p, p.b_first + (size_t)(c + 1) * SZ, j0);
-    st.save_state(p, p.b_in + (size_t)c * SZ, j0);
-    float vp0[JB], vp1[JB];
-    bwd_plain(tm, p, st, lds, j0, invz, t_e, vp0, vp1);
-    float bf0[JB], bf1[JB];
-    bwd_out<JB, WP, BlockTeam<NW>, 16 / JB>(tm, p, st, lds, j0, invz, t_c, t_e, vp0, vp1, true, bf0, bf1);
-    float* bf = p.b_first + (size_t)c * SZ;
-    const float d = hilbert_reg<JB>(tm, bf0, bf1, bf, p.Lpad, j0);
-    changed = !(d <= p.tol);
-    __syncthreads();  // every wave has read bf before it is overwritten
-#pragma unroll
-    for (int j = 0; j < JB; ++j) {
-      bf[j0 + j] = bf0[j];
-      bf[p.Lpad + j0 + j] = bf1[j];
-    }
-    __threadfence();
-    __syncthreads();
-    ++repairs;
-    --c;
-  }
-  if (threadIdx.x == 0) p.repairs[1] += repairs;
 }
 
 // ---------------------------------------------------------------------------
@@ -851,53 +88,19 @@ static int pick_WP(int band) {
   return -1;
 }
 
-typedef void (*fb_kernel_t)(FBParams);
-
 static int repair_nw_rt(int J) { return J >= 8 ? 8 : J; }
 
-#define PMG_FB_TABLE(NAME)                                                                 \
-  static fb_kernel_t NAME##_table(int J, int WP) {                                         \
-    switch (J * 100 + WP) {                                                                \
-      case 105: return NAME<1, 5>;                                                    \
-      case 109: return NAME<1, 9>;                                                    \
-      case 113: return NAME<1, 13>;                                                   \
-      case 117: return NAME<1, 17>;                                                   \
-      case 125: return NAME<1, 25>;                                                   \
-      case 132: return NAME<1, 32>;                                                   \
-      case 205: return NAME<2, 5>;                                                    \
-      case 209: return NAME<2, 9>;                                                    \
-      case 213: return NAME<2, 13>;                                                   \
-      case 217: return NAME<2, 17>;                                                   \
-      case 225: return NAME<2, 25>;                                                   \
-      case 232: return NAME<2, 32>;                                                   \
-      case 405: return NAME<4, 5>;                                                    \
-      case 409: return NAME<4, 9>;                                                    \
-      case 413: return NAME<4, 13>;                                                   \
-      case 417: return NAME<4, 17>;                                                   \
-      case 425: return NAME<4, 25>;                                                   \
-      case 432: return NAME<4, 32>;                                                   \
-      case 805: return NAME<8, 5>;                                                    \
-      case 809: return NAME<8, 9>;                                                    \
-      case 813: return NAME<8, 13>;                                                   \
-      case 817: return NAME<8, 17>;                                                   \
-      case 825: return NAME<8, 25>;                                                   \
-      case 832: return NAME<8, 32>;                                                   \
-      case 1605: return NAME<16, 5>;                                                  \
-      case 1609: return NAME<16, 9>;                                                  \
-      case 1613: return NAME<16, 13>;                                                 \
-      case 1617: return NAME<16, 17>;                                                 \
-      case 1625: return NAME<16, 25>;                                                 \
-      case 1632: return NAME<16, 32>;                                                 \
-      default: return nullptr;                                                             \
-    }                                                                                      \
+// kernel sets are instantiated per latents-per-lane J in fb_inst_j*.hip (parallel builds)
+static bool fb_set(int J, int WP, FBKernelSet* k) {
+  switch (J) {
+    case 1: return fb_set_j1(WP, k);
+    case 2: return fb_set_j2(WP, k);
+    case 4: return fb_set_j4(WP, k);
+    case 8: return fb_set_j8(WP, k);
+    case 16: return fb_set_j16(WP, k);
+    default: return false;
   }
-
-PMG_FB_TABLE(k_forward)
-PMG_FB_TABLE(k_forward_repair)
-PMG_FB_TABLE(k_forward_fix)
-PMG_FB_TABLE(k_backward_fix)
-PMG_FB_TABLE(k_backward)
-PMG_FB_TABLE(k_backward_repair)
+}
 
 static int fill_params(FBParams& p, const pmg_transition* tr, int64_t T, int C, int B,
                        double s, double tol) {
@@ -972,8 +175,10 @@ static int forward_impl(const float* delta, const float* phi, const double* m, i
   p.flags = w.flags;
   p.repairs = w.repairs;
   const int J = p.Lpad / 64, WP = pick_WP(tr->band);
-  fb_kernel_t kf = k_forward_table(J, WP), kfix = k_forward_fix_table(J, WP),
-              kr = k_forward_repair_table(J, WP);
+  FBKernelSet ks;
+  const bool have = fb_set(J, WP, &ks);
+  fb_kernel_t kf = have ? ks.forward : nullptr, kfix = have ? ks.forward_fix : nullptr,
+              kr = have ? ks.forward_repair : nullptr;
   PMG_REQUIRE(kf && kfix && kr, "pmg_forward_filter: no kernel for J=%d WP=%d", J, WP);
   if (phase & 1) {
     PMG_HIP(hipMemsetAsync(w.repairs, 0, sizeof(int), st));
@@ -1044,8 +249,10 @@ static int backward_impl(const float* delta, const float* phi, const float* alph
   p.flags = w.flags;
   p.repairs = w.repairs;
   const int J = p.Lpad / 64, WP = pick_WP(tr->band);
-  fb_kernel_t kb = k_backward_table(J, WP), kfix = k_backward_fix_table(J, WP),
-              kr = k_backward_repair_table(J, WP);
+  FBKernelSet ks;
+  const bool have = fb_set(J, WP, &ks);
+  fb_kernel_t kb = !have ? nullptr : (rho || gamma || !P) ? ks.backward_full : ks.backward,
+              kfix = have ? ks.backward_fix : nullptr, kr = have ? ks.backward_repair : nullptr;
   PMG_REQUIRE(kb && kfix && kr, "pmg_backward_smoother: no kernel for J=%d WP=%d", J, WP);
   if (phase & 1) {
     PMG_HIP(hipMemsetAsync(w.repairs + 1, 0, sizeof(int), st));

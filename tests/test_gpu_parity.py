@@ -104,6 +104,9 @@ SCAN_CASES = [
     (24, 300, 700, 1.0, 0.01, 0.01, 100, 16, 1.0),      # L between 256 and 512
     (30, 512, 1200, 1.0, 0.01, 0.01, 16, 0, 1.0),       # sequential repair, 8-wave team
     (16, 1024, 300, 1.0, 0.01, 0.01, 16, 0, 1.0),       # sequential repair, 2 latents/thread
+    (40, 512, 3000, 1.0, 0.01, 0.01, 64, 64, 1.0),      # C3 lane layout (8 latents/lane), chunk-parallel
+    (40, 1024, 1500, 1.0, 0.01, 0.01, 64, 64, 1.0),     # 16 latents/lane, chunk-parallel
+    (40, 512, 2000, 3.0, 0.01, 0.01, 50, 48, 1.0),      # band 25 at 8 latents/lane (4 halo lanes)
 ]
 
 
