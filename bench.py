@@ -30,6 +30,7 @@ CONFIGS = {
     "c2": (128, 10000, 256),
     "c3": (512, 100000, 512),
     "c5": (256, 50000, 256),
+    "c4": (1024, 1000000, 1024),
 }
 PEAK_HBM_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
 PEAK_FP32_TFLOPS = 157.3         # dense FP32 matrix / packed vector (spec)
@@ -60,6 +61,56 @@ def synth(N, T, L, ls=10.0, seed=0, rank=0):
     lp0 = np.log(p).astype(np.float32)
     W0 = np.random.default_rng(123).normal(size=W.shape).astype(np.float32)
     return y, B, W0, lp0
+
+
+class LazyRows:
+    """(T, K) array whose row blocks are generated on demand: rows [a, b) of block
+    size `block` come from fn(block_index) -> (rows, K), seeded per block, so every
+    rank of a time-sharded run materialises only its own (extended) slice."""
+
+    def __init__(self, T, K, fn, block=10000):
+        self.shape = (T, K)
+        self.fn, self.block = fn, block
+
+    def __getitem__(self, sl):
+        a, b, _ = sl.indices(self.shape[0])
+        parts = []
+        for k in range(a // self.block, (b - 1) // self.block + 1):
+            blk = self.fn(k)
+            lo, hi = max(a, k * self.block) - k * self.block, min(b, (k + 1) * self.block) - k * self.block
+            parts.append(blk[lo:hi])
+        return np.concatenate(parts, 0)
+
+
+def synth_long(N, T, L, ls=10.0, seed=0, block=10000):
+    """synth() for long recordings (C4): the latent path is sampled whole (cheap), the
+    spikes and the posterior init per 10k-step block with per-block seeds."""
+    from poor_man_gplvm_amd.gp_kernel import generate_basis, create_transition_prob_1d
+    B = generate_basis(ls, L)
+    W = np.random.default_rng(seed).normal(size=(B.shape[1], N))
+    tun = np.logaddexp(B.astype(np.float64) @ W, 0.0)
+    K, _, A, _ = create_transition_prob_1d(L, 1.0, 0.01, 0.01)
+    rng = np.random.default_rng(seed + 1)
+    cK = np.cumsum(K, axis=2)
+    u = rng.random((T, 2))
+    lat = np.empty(T, np.int64)
+    d, l = 0, L // 2
+    for t in range(T):
+        d = 1 if u[t, 0] < A[d, 1] else 0
+        l = int(min(np.searchsorted(cK[d, l], u[t, 1] * cK[d, l, -1], side="right"), L - 1))
+        lat[t] = l
+
+    def spikes(k):
+        sl = lat[k * block:(k + 1) * block]
+        return np.random.default_rng([seed + 2, k]).poisson(tun[sl]).astype(np.float32)
+
+    def post0(k):
+        n = min(block, T - k * block)
+        uu = np.random.default_rng([seed + 3, k]).random((n, L)) * 0.1
+        return np.log(uu / uu.sum(1, keepdims=True)).astype(np.float32)
+
+    W0 = np.random.default_rng(123).normal(size=W.shape).astype(np.float32)
+    return LazyRows(T, N, spikes, block), B, W0, LazyRows(T, L, post0, block)
 
 
 def cpu_baseline(N, T, L, adam_iters, t_sample=128, adam_sample=10):
@@ -97,6 +148,148 @@ def cpu_baseline(N, T, L, adam_iters, t_sample=128, adam_sample=10):
                        f"iterations (the GPU run's mean): {total:.1f} s per EM iteration")}
 
 
+def compute_rooflines(summ, T, L, N, NB, adam_iters, config):
+    """Per-kernel rooflines (SURVEY.md 8(d) algorithmic units per launch) from the
+    KernelTimer summary; the top-level `roofline` is the dominant kernel (largest mean
+    time per EM iteration).  T = time steps one launch processes."""
+    nblk = (L + 31) // 32
+    units = {
+        # section: (kernel, bound, algorithmic units per launch, unit scale, peak, unit)
+        "forward_filter": ("k_forward", "hbm", 12.0 * T * L + 4.0 * T * nblk + 16.0 * T, 1e9, PEAK_HBM_GBS, "GB/s"),
+        "backward_smoother": ("k_backward", "hbm", 16.0 * T * L + 4.0 * T * nblk, 1e9, PEAK_HBM_GBS, "GB/s"),
+        "suffstats": ("k_ptb3", "mfma", 2.0 * T * L * N, 1e12, PEAK_BF16_MFMA_TFLOPS, "TFLOP/s"),
+        "emission": ("k_emission_i8", "mfma", 2.0 * T * L * N, 1e12, PEAK_I8_MFMA_TOPS, "TFLOP/s"),
+        "mstep_adam": ("k_adam", "mfma", 4.0 * L * NB * N * adam_iters, 1e12, PEAK_FP32_TFLOPS, "TFLOP/s"),
+    }
+    pmc = {}
+    pmc_path = os.path.join(ROOT, "profiles", f"r01_pmc_{config}.json")
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as fh:
+            pmc = json.load(fh).get("kernels", {})
+    rooflines = {}
+    for sec, (kname, bound, units_per_launch, scale, peak, unit) in units.items():
+        if sec not in summ:
+            continue
+        t_ms = summ[sec][1]
+        achieved = units_per_launch / scale / (t_ms / 1e3)
+        tr = pmc.get(kname, {}).get("hbm_bytes_per_launch")
+        rooflines[sec] = {"kernel": kname, "bound": bound, "achieved": achieved, "peak": peak, "unit": unit,
+                          "frac": achieved / peak, "traffic": tr, "ms": round(t_ms, 4),
+                          "algorithmic_per_launch": units_per_launch}
+    dom = max(rooflines, key=lambda k: rooflines[k]["ms"])
+    roof_dom = dict(rooflines[dom])
+    roof_dom.pop("ms")
+    roof_dom.pop("algorithmic_per_launch")
+    return rooflines, roof_dom
+
+
+def bench_timeshard(args):
+    """One EM iteration of ONE recording time-sharded over the ranks (timeshard.py):
+    value = EM iterations/s of the whole job (total T fixed: strong scaling)."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from poor_man_gplvm_amd.engine import AdamConfig, ScanConfig, KernelTimer
+    from poor_man_gplvm_amd.gp_kernel import banded_transition
+    from poor_man_gplvm_amd.timeshard import DistComm, LocalComm, TimeShardedEM, shard_layout
+
+    N, T, L = CONFIGS[args.config]
+    t_syn = time.perf_counter()
+    y, B, W0, lp0 = synth_long(N, T, L) if T > 200000 else synth(N, T, L)
+    t_syn = time.perf_counter() - t_syn
+    comm = DistComm() if world > 1 else LocalComm(args.virtual)
+    scan = ScanConfig(chunk=args.chunk or None, warmup=args.warm_steps, adaptive=not args.warm_fb)
+    lays = shard_layout(T, comm.world, chunk=args.chunk or None, halo=args.halo, scan=scan)
+    eng = TimeShardedEM(y, B, banded_transition(L, 1.0, 0.01, 0.01), comm, lays, scan)
+    for s in eng.shards:
+        s.set_log_posterior(np.asarray(lp0[s.lay.ext_start:s.lay.ext_stop]))
+        if args.warm_fb:
+            s.warm = [int(v) for v in args.warm_fb.split(",")]
+    dev = eng.dev
+    adam = AdamConfig(lr=0.01, maxiter=1000, tol=1e-6, prior_std=1.0)
+    n = len(eng.shards)
+    Ws = [torch.as_tensor(W0.astype(np.float64), device=dev).contiguous() for _ in range(n)]
+    mus = [torch.zeros_like(Ws[0]) for _ in range(n)]
+    nus = [torch.zeros_like(Ws[0]) for _ in range(n)]
+    cnts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(n)]
+    n_all = args.warmup + args.steps
+    stats = torch.zeros((n_all, 4), dtype=torch.float64, device=dev)
+    lh = torch.zeros((n_all, adam.maxiter), dtype=torch.float64, device=dev)
+    eh = torch.zeros_like(lh)
+    logz = torch.zeros(n_all, dtype=torch.float64, device=dev)
+    rounds = []
+
+    def em_iter(i):
+        eng.m_step(Ws, mus, nus, cnts, adam, stats[i], lh[i], eh[i])
+        eng.e_step(1.0, logz[i:i + 1])
+        rounds.append(tuple(eng.carry_rounds))
+
+    for i in range(args.warmup):
+        em_iter(i)
+    torch.cuda.synchronize()
+    timer = KernelTimer()
+    eng.set_timer(timer)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.warmup, n_all):
+        em_iter(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        te = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        elapsed = float(te.item())
+    summ = timer.summary()
+    # per-launch figures: a timed section covers every local shard once per EM iteration
+    summ = {k: (c, ms / n) for k, (c, ms) in summ.items()}
+    st = stats.cpu().numpy()
+    adam_iters = float(np.mean(st[args.warmup:, 0])) if args.steps else 0.0
+    T_ext = max(s.T for s in eng.shards)
+    rooflines, roof_dom = compute_rooflines(summ, T_ext, L, N, B.shape[1], adam_iters, args.config)
+    t_fb = summ["forward_filter"][1] + summ["backward_smoother"][1]
+    out = {
+        "metric": "EM iters/sec at N=512, T=1e5, B=512; fwd-bwd achieved HBM GB/s",
+        "value": args.steps / elapsed,
+        "unit": "EM iters/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32 state / int8-exact emission / f64 stats",
+        "data": "synthetic (spikes sampled from the model; per-10k-block seeds for long recordings)",
+        "config": {"workload": f"{args.config}: ONE PoissonGPLVMJump1D.fit_em N={N} T={T} L={L} nb={B.shape[1]}, "
+                               f"time-sharded over {comm.world} shard(s) ({n} per process), halo {args.halo}; "
+                               f"one EM iteration per step",
+                   "n_neuron": N, "n_time": T, "n_latent_bin": L,
+                   "parallelism": f"time shards x{comm.world} (RCCL all-reduce of y_w/t_w + carry send/recv)"},
+        "roofline": roof_dom,
+        "rooflines": rooflines,
+        "kernels_ms": {k: round(v[1], 4) for k, v in summ.items()},
+        "fwd_bwd_GBps_per_shard": 28.0 * T_ext * L / 1e9 / (t_fb / 1e3),
+        "adam_iters_mean": adam_iters,
+        "chunk": lays[0].chunk,
+        "carry_rounds_timed": rounds[args.warmup:],
+        "repairs_last": [list(s.repairs()) for s in eng.shards],
+        "synth_s": round(t_syn, 1),
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -108,7 +301,14 @@ def main():
     ap.add_argument("--warm-steps", type=int, default=48)
     ap.add_argument("--warm-fb", type=str, default="", help="fixed forward,backward warm-up (no adaptation)")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--shard", default="restarts", choices=["restarts", "time"],
+                    help="multi-GPU axis: independent restarts (weak scaling) or time shards of one "
+                         "recording (strong scaling, RCCL suff-stat all-reduce + carry hand-off)")
+    ap.add_argument("--virtual", type=int, default=1, help="time shards per process (single-GPU rehearsal)")
+    ap.add_argument("--halo", type=int, default=512, help="time-shard halo (steps)")
     args = ap.parse_args()
+    if args.shard == "time":
+        return bench_timeshard(args)
 
     import torch
     import torch.distributed as dist
@@ -171,37 +371,7 @@ def main():
     adam_iters = float(np.mean(s[args.warmup:, 0])) if args.steps else 0.0
     repairs = eng.repairs()
 
-    # per-kernel rooflines (SURVEY.md 8(d) algorithmic units per launch); the top-level
-    # `roofline` is the dominant kernel (largest mean time per EM iteration)
-    nblk = (L + 31) // 32
-    NB = B.shape[1]
-    units = {
-        # section: (kernel, bound, algorithmic units per launch, unit scale, peak, unit)
-        "forward_filter": ("k_forward", "hbm", 12.0 * T * L + 4.0 * T * nblk + 16.0 * T, 1e9, PEAK_HBM_GBS, "GB/s"),
-        "backward_smoother": ("k_backward", "hbm", 16.0 * T * L + 4.0 * T * nblk, 1e9, PEAK_HBM_GBS, "GB/s"),
-        "suffstats": ("k_ptb3", "mfma", 2.0 * T * L * N, 1e12, PEAK_BF16_MFMA_TFLOPS, "TFLOP/s"),
-        "emission": ("k_emission_i8", "mfma", 2.0 * T * L * N, 1e12, PEAK_I8_MFMA_TOPS, "TFLOP/s"),
-        "mstep_adam": ("k_adam", "mfma", 4.0 * L * NB * N * adam_iters, 1e12, PEAK_FP32_TFLOPS, "TFLOP/s"),
-    }
-    pmc = {}
-    pmc_path = os.path.join(ROOT, "profiles", f"r01_pmc_{args.config}.json")
-    if os.path.exists(pmc_path):
-        with open(pmc_path) as fh:
-            pmc = json.load(fh).get("kernels", {})
-    rooflines = {}
-    for sec, (kname, bound, units_per_launch, scale, peak, unit) in units.items():
-        if sec not in summ:
-            continue
-        t_ms = summ[sec][1]
-        achieved = units_per_launch / scale / (t_ms / 1e3)
-        tr = pmc.get(kname, {}).get("hbm_bytes_per_launch")
-        rooflines[sec] = {"kernel": kname, "bound": bound, "achieved": achieved, "peak": peak, "unit": unit,
-                          "frac": achieved / peak, "traffic": tr, "ms": round(t_ms, 4),
-                          "algorithmic_per_launch": units_per_launch}
-    dom = max(rooflines, key=lambda k: rooflines[k]["ms"])
-    roof_dom = dict(rooflines[dom])
-    roof_dom.pop("ms")
-    roof_dom.pop("algorithmic_per_launch")
+    rooflines, roof_dom = compute_rooflines(summ, T, L, N, B.shape[1], adam_iters, args.config)
     t_fb = summ["forward_filter"][1] + summ["backward_smoother"][1]
     B_fb = 28.0 * T * L
     value = world * args.steps / elapsed

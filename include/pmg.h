@@ -156,6 +156,27 @@ int pmg_backward_smoother_phase(const float* delta, const float* phi, const floa
 /* workspace (device int32 pair at a fixed offset; host reads it lazily). */
 size_t pmg_fwdbwd_repair_counter_offset(int64_t T, int32_t L, int32_t chunk);
 
+/* Chunk-boundary states of the two scans inside a pmg_fwdbwd workspace, so that a  */
+/* caller can stitch scans that run on different devices (time shards: the carries */
+/* of the chunk loop, decoder.py:283-304 forward / :313-326 backward, handed from  */
+/* one shard to the next).  Each state is 2 x Lpad f32 (d = 0 row at [0, L), d = 1  */
+/* row at [Lpad, Lpad + L), Lpad = pmg_fwdbwd_lpad(L)), unnormalised (the scans and */
+/* the boundary check are scale-free).  For chunk c of a workspace sized for         */
+/* (T, L, chunk):                                                                   */
+/*   FWD_IN    restart state of chunk c (filter state at c*chunk - 1)               */
+/*   FWD_OUT   filter state at the last step of chunk c                              */
+/*   BWD_IN    restart beta at the first step after chunk c                          */
+/*   BWD_FIRST beta at the first step of chunk c                                     */
+/* Writing FWD_OUT[c-1] (BWD_FIRST[c+1]) and re-running phase 2 of the forward        */
+/* (backward) call re-verifies chunk c against the new carry and repairs it and its */
+/* successors exactly as for an interior boundary.  Returns NULL on a bad argument. */
+#define PMG_STATE_FWD_IN 0
+#define PMG_STATE_FWD_OUT 1
+#define PMG_STATE_BWD_IN 2
+#define PMG_STATE_BWD_FIRST 3
+int32_t pmg_fwdbwd_lpad(int32_t L);
+float* pmg_fwdbwd_state(void* workspace, int64_t T, int32_t L, int32_t chunk, int32_t which, int64_t c);
+
 /* ------------------------------------------------------------------ */
 /* Sufficient statistics -- fit_tuning_helper.get_statistics             */
 /* (fit_tuning_helper.py:28-42): y_w = P^T y (L,N), t_w = sum_t P (L).    */
@@ -200,6 +221,18 @@ int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const floa
                    const double* yw, const double* tw, int32_t L, int32_t NB, int32_t N,
                    const pmg_adam_cfg* cfg, double* stats, double* loss_hist, double* err_hist,
                    void* workspace, size_t workspace_bytes, void* stream);
+
+/* Same loop and outputs for shapes the persistent kernel does not hold          */
+/* (L > 512 or NB > 128, e.g. BASELINE C4: L = 1024, NB = 154): per body an f64    */
+/* LDS-tiled F = B W + gradient-factor kernel, an f64 B^T G + optax-update kernel  */
+/* and a one-workgroup decision kernel (fixed-order sums); bodies are enqueued in */
+/* batches of 16 and the host reads the decision word once per batch (this call   */
+/* synchronises the stream).  Workspace: pmg_mstep_tiled_workspace_size.           */
+size_t pmg_mstep_tiled_workspace_size(int32_t L, int32_t NB, int32_t N);
+int pmg_mstep_adam_tiled(double* W, double* mu, double* nu, int64_t* count, const float* basis,
+                         const double* yw, const double* tw, int32_t L, int32_t NB, int32_t N,
+                         const pmg_adam_cfg* cfg, double* stats, double* loss_hist, double* err_hist,
+                         void* workspace, size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------ */
 /* Pairwise joint (decode only) -- the logaddexp accumulation of         */

@@ -17,6 +17,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "csrc", "libpmg_hip.so")
 
 PMG_MAX_BAND = 32
+# pmg_fwdbwd_state slots (include/pmg.h)
+STATE_FWD_IN, STATE_FWD_OUT, STATE_BWD_IN, STATE_BWD_FIRST = 0, 1, 2, 3
 ABI_VERSION = 1
 
 # every symbol the header declares (checked by tests/test_capi_symbols.py)
@@ -29,7 +31,8 @@ EXPORTED_SYMBOLS = (
     "pmg_suffstats_workspace_size", "pmg_suffstats", "pmg_exp", "pmg_log",
     "pmg_spikes_bf16t", "pmg_suffstats_bf16_workspace_size", "pmg_suffstats_bf16",
     "pmg_mstep_workspace_size", "pmg_mstep_adam", "pmg_joint_workspace_size",
-    "pmg_joint_accumulate",
+    "pmg_joint_accumulate", "pmg_fwdbwd_lpad", "pmg_fwdbwd_state",
+    "pmg_mstep_tiled_workspace_size", "pmg_mstep_adam_tiled",
 )
 
 
@@ -78,6 +81,8 @@ _SIGS = {
     "pmg_backward_smoother": ([_P, _P, _P, _I64, ctypes.POINTER(Transition), _D, _I32, _I32, _D,
                                _P, _P, _P, _P, _SZ, _P], _I32),
     "pmg_fwdbwd_repair_counter_offset": ([_I64, _I32, _I32], _SZ),
+    "pmg_fwdbwd_lpad": ([_I32], _I32),
+    "pmg_fwdbwd_state": ([_P, _I64, _I32, _I32, _I32, _I64], _P),
     "pmg_suffstats_workspace_size": ([_I64, _I32, _I32], _SZ),
     "pmg_suffstats": ([_P, _P, _I64, _I32, _I32, _I32, _P, _P, _P, _SZ, _P], _I32),
     "pmg_spikes_bf16t": ([_P, _I64, _I32, _P, _I64, _P], _I32),
@@ -88,6 +93,9 @@ _SIGS = {
     "pmg_mstep_workspace_size": ([_I32, _I32], _SZ),
     "pmg_mstep_adam": ([_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, ctypes.POINTER(AdamCfg),
                         _P, _P, _P, _P, _SZ, _P], _I32),
+    "pmg_mstep_tiled_workspace_size": ([_I32, _I32, _I32], _SZ),
+    "pmg_mstep_adam_tiled": ([_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, ctypes.POINTER(AdamCfg),
+                              _P, _P, _P, _P, _SZ, _P], _I32),
     "pmg_joint_workspace_size": ([_I64, _I32], _SZ),
     "pmg_joint_accumulate": ([_P, _P, _I64, _I32, _P, _P, _SZ, _P], _I32),
 }

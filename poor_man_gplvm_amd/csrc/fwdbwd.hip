@@ -151,6 +151,28 @@ size_t pmg_fwdbwd_repair_counter_offset(int64_t T, int32_t L, int32_t chunk) {
   return 0;  // repairs[0] (forward), repairs[1] (backward) at the workspace start
 }
 
+int32_t pmg_fwdbwd_lpad(int32_t L) {
+  const int J = pick_J(L);
+  return J < 0 ? 0 : 64 * J;
+}
+
+float* pmg_fwdbwd_state(void* workspace, int64_t T, int32_t L, int32_t chunk, int32_t which, int64_t c) {
+  const int J = pick_J(L);
+  if (!workspace || J < 0 || chunk <= 0 || T <= 0) return nullptr;
+  const int64_t M = (T + chunk - 1) / chunk;
+  if (c < 0 || c >= M) return nullptr;
+  FBWork w = carve_fb(workspace, T, 64 * J, chunk);
+  float* base = nullptr;
+  switch (which) {
+    case PMG_STATE_FWD_IN: base = w.s_in; break;
+    case PMG_STATE_FWD_OUT: base = w.s_out; break;
+    case PMG_STATE_BWD_IN: base = w.b_in; break;
+    case PMG_STATE_BWD_FIRST: base = w.b_first; break;
+    default: return nullptr;
+  }
+  return base + (size_t)c * 2 * (64 * J);
+}
+
 // phase: 1 = speculative chunk-parallel pass, 2 = verify / repair / logZ, 3 = both
 static int forward_impl(const float* delta, const float* phi, const double* m, int64_t T,
                         const pmg_transition* tr, double likelihood_scale, int32_t chunk,

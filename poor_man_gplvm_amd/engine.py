@@ -268,19 +268,27 @@ class DeviceEM:
                                              nat.ptr(self.ws_ss), self.ws_ss.numel(), sh), "pmg_suffstats")
         self.adam(W, mu, nu, count, cfg, stats_out, lh_out, eh_out)
 
+    # shapes the persistent one-launch Adam kernel holds (a latent row per thread, the
+    # basis row in registers + LDS); larger ones use the tiled per-body kernels
+    PERSISTENT_MAX_L, PERSISTENT_MAX_NB = 512, 128
+
     def adam(self, W, mu, nu, count, cfg: AdamConfig, stats_out, lh_out, eh_out):
         if self.basis is None:
             raise ValueError("no basis")
-        need = int(self.lib.pmg_mstep_workspace_size(self.N, int(cfg.maxiter)))
+        tiled = self.L > self.PERSISTENT_MAX_L or self.NB > self.PERSISTENT_MAX_NB
+        need = int(self.lib.pmg_mstep_tiled_workspace_size(self.L, self.NB, self.N) if tiled
+                   else self.lib.pmg_mstep_workspace_size(self.N, int(cfg.maxiter)))
         if self.ws_ad is None or self.ws_ad.numel() < need:
             self.ws_ad = torch.empty(need, dtype=torch.uint8, device=self.dev)
         c = cfg.to_c()
+        fn = self.lib.pmg_mstep_adam_tiled if tiled else self.lib.pmg_mstep_adam
         with self._t('mstep_adam'):
-          nat.check(self.lib.pmg_mstep_adam(nat.ptr(W), nat.ptr(mu), nat.ptr(nu), nat.ptr(count),
-                                          nat.ptr(self.basis), nat.ptr(self.yw), nat.ptr(self.tw),
-                                          self.L, self.NB, self.N, ctypes.byref(c), nat.ptr(stats_out),
-                                          nat.ptr(lh_out), nat.ptr(eh_out), nat.ptr(self.ws_ad),
-                                          self.ws_ad.numel(), nat.stream_handle()), "pmg_mstep_adam")
+          nat.check(fn(nat.ptr(W), nat.ptr(mu), nat.ptr(nu), nat.ptr(count),
+                       nat.ptr(self.basis), nat.ptr(self.yw), nat.ptr(self.tw),
+                       self.L, self.NB, self.N, ctypes.byref(c), nat.ptr(stats_out),
+                       nat.ptr(lh_out), nat.ptr(eh_out), nat.ptr(self.ws_ad),
+                       self.ws_ad.numel(), nat.stream_handle()),
+                    "pmg_mstep_adam_tiled" if tiled else "pmg_mstep_adam")
 
     def compute_tuning(self, W):
         with self._t('tuning_softplus'):

@@ -211,12 +211,19 @@ def test_suffstats_nonint_spikes_use_f32_path():
     assert SpikeData(y).ybt is None
 
 
-@pytest.mark.parametrize("N,L,maxiter,tol", [(30, 100, 40, 0.0), (30, 100, 1000, 1e-6), (128, 256, 60, 0.0),
-                                             (7, 48, 1, 1e-6)])
-def test_adam_vs_oracle(N, L, maxiter, tol):
+@pytest.mark.parametrize("N,L,maxiter,tol,tiled", [(30, 100, 40, 0.0, False), (30, 100, 1000, 1e-6, False),
+                                                   (128, 256, 60, 0.0, False), (7, 48, 1, 1e-6, False),
+                                                   (30, 100, 40, 0.0, True), (30, 100, 1000, 1e-6, True),
+                                                   (7, 48, 1, 1e-6, True), (7, 48, 2, 1e-6, True),
+                                                   (64, 1024, 30, 0.0, True), (40, 700, 1000, 1e-6, True)])
+def test_adam_vs_oracle(N, L, maxiter, tol, tiled):
+    """tiled: pmg_mstep_adam_tiled (forced for small shapes; L > 512 / NB > 128 always)."""
     from poor_man_gplvm_amd.engine import AdamConfig
     d = make(N, L, 500)
     sp, eng = _engine(d, L)
+    if tiled:
+        eng.PERSISTENT_MAX_L = 0
+    assert eng.L <= 512 or tiled
     P = np.exp(d['lp0'].astype(np.float64))
     yw, tw = O.get_statistics(d['lp0'].astype(np.float64), d['y'])
     eng.yw.copy_(torch.as_tensor(yw, device='cuda'))

@@ -1,0 +1,164 @@
+"""GPU parity of the time-sharded EM (poor_man_gplvm_amd/timeshard.py): shards of one
+spike train with halo warm-up and carry rounds must reproduce the unsharded answer.
+
+Bars (as tests/test_gpu_parity.py): against the float64 golden fixtures the same
+tolerances as the single-GPU EM; against the single-GPU engine on larger inputs the
+scan tolerance after one EM iteration (Hilbert boundary tol 1e-6 -> probabilities
+within rel 2e-5 where P > 1e-12; 1e-5 absolute after two), logZ rel 1e-7 (suff-stat sums are re-associated over shards), identical
+Adam iteration counts.
+Virtual shards (LocalComm) run every shard on cuda:0 in one process; the gloo case
+runs two real ranks (both on cuda:0) through DistComm with host-staged exchange.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from tests.synth import make
+from tests.test_gpu_parity import HERE, RT, argmax_match, close_prob
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _dev():
+    torch.cuda.set_device(0)
+
+
+def _sharded_fixture(name, world, chunk, halo):
+    import poor_man_gplvm_amd as P
+    from poor_man_gplvm_amd.timeshard import run_em_timesharded
+    f = np.load(os.path.join(HERE, 'golden', name))
+    L = f['basis'].shape[0]
+    res, info = run_em_timesharded(f['y'].astype(np.float32), f['W0'], f['basis'], f['lp0'],
+                                   n_iter=int(f['n_iter']), transition=P.banded_transition(L, float(f['mv'])),
+                                   world=world, chunk=chunk, halo=halo,
+                                   adam=P.AdamConfig(maxiter=int(f['maxiter']), tol=float(f['tol'])))
+    return f, res, info
+
+
+@pytest.mark.parametrize("world,chunk,halo", [(1, None, 512), (2, 16, 64), (3, 16, 16), (5, 8, 8)])
+def test_timesharded_one_iteration_golden(world, chunk, halo):
+    f, res, info = _sharded_fixture('em_c1_one.npz', world, chunk, halo)
+    np.testing.assert_allclose(res['tuning'], f['tuning'], rtol=RT)
+    close_prob(res['posterior_latent_marg'], f['posterior'].astype(np.float64).sum(1))
+    argmax_match(res['posterior_latent_marg'], f['posterior'].sum(1))
+    np.testing.assert_allclose(res['log_marginal_l'], f['log_marginal_l'], rtol=1e-7)
+    assert res['m_step_res_l']['n_iter'] == list(f['m_n_iter'])
+    assert res['posterior'].shape == f['posterior'].shape
+
+
+def test_timesharded_fixed_iterations_golden():
+    """Three EM iterations over 4 shards (same bar as test_fit_em_fixed_iterations_golden)."""
+    f, res, info = _sharded_fixture('em_c1_fixed.npz', 4, 16, 32)
+    np.testing.assert_allclose(res['tuning'], f['tuning'], rtol=RT)
+    exact = f['posterior'].astype(np.float64).sum(1)
+    ours = np.asarray(res['posterior_latent_marg'], np.float64)
+    ref_noise = np.abs(f['mimic32_posterior_latent'].astype(np.float64) - exact).max()
+    dev = np.abs(ours - exact).max()
+    assert dev < 1e-5 and dev < 0.1 * ref_noise, (dev, ref_noise)
+    argmax_match(res['posterior_latent_marg'], f['posterior'].sum(1))
+    np.testing.assert_allclose(res['log_marginal_l'], f['log_marginal_l'], rtol=1e-7)
+    assert res['m_step_res_l']['n_iter'] == list(f['m_n_iter'])
+
+
+def _vs_single(world, halo, chunk, n_iter=2, N=48, L=128, T=12000, flat=False):
+    import poor_man_gplvm_amd as P
+    from poor_man_gplvm_amd.timeshard import run_em_timesharded
+    d = make(N, L, T)
+    W0 = d['W0'] * (0.05 if flat else 1.0)    # nearly flat tuning: slow forgetting, long cascades
+    tr = P.banded_transition(L, 1.0)
+    ad = P.AdamConfig(maxiter=40, tol=0.0)
+    sc = P.ScanConfig(chunk=chunk, warmup=16, adaptive=False)
+    ref, _ = P.run_em(d['y'], W0, d['B'], d['lp0'], n_iter=n_iter, transition=tr, adam=ad, scan=sc)
+    res, info = run_em_timesharded(d['y'], W0, d['B'], d['lp0'], n_iter=n_iter, transition=tr, world=world,
+                                   adam=ad, scan=sc, halo=halo, chunk=chunk)
+    assert res['m_step_res_l']['n_iter'] == ref['m_step_res_l']['n_iter']
+    np.testing.assert_allclose(res['log_marginal_l'], ref['log_marginal_l'], rtol=1e-7)
+    np.testing.assert_allclose(res['tuning'], ref['tuning'], rtol=1e-5)
+    a, b = res['posterior_latent_marg'].astype(np.float64), ref['posterior_latent_marg'].astype(np.float64)
+    if n_iter == 1:     # same M-step up to f64 re-association: the scan tolerance
+        m = np.maximum(a, b) > 1e-12
+        assert np.max(np.abs(a[m] - b[m]) / np.maximum(a[m], b[m])) < 2e-5
+    else:               # later iterations amplify tuning rounding (test_fit_em_fixed_iterations_golden)
+        assert np.max(np.abs(a - b)) < 1e-5
+    argmax_match(a, b)
+    return info
+
+
+@pytest.mark.parametrize("n_iter", [1, 2])
+def test_timesharded_vs_single_gpu(n_iter):
+    info = _vs_single(world=4, halo=512, chunk=32, n_iter=n_iter)
+    assert all(r[0] >= 1 for r in info['carry_rounds'])
+
+
+def test_timesharded_flat_tuning_cascade():
+    """Nearly flat tuning (as test_gpu_parity.test_flat_tuning_cascade) and a one-chunk
+    halo: nothing forgets, every boundary fails, so the carry rounds must hand the
+    exact state through every shard in turn; the E-step must still match the oracle."""
+    from oracle import gplvm_oracle as O
+    from poor_man_gplvm_amd.engine import ScanConfig
+    from poor_man_gplvm_amd.gp_kernel import banded_transition
+    from poor_man_gplvm_amd.timeshard import LocalComm, TimeShardedEM, shard_layout
+    N, L, T, R = 24, 256, 3000, 4
+    d = make(N, L, T)
+    rng = np.random.default_rng(11)
+    tun = (d['tuning'].mean(0, keepdims=True) * (1.0 + 1e-3 * rng.standard_normal((L, N)))).astype(np.float64)
+    lays = shard_layout(T, R, chunk=32, halo=32)
+    eng = TimeShardedEM(d['y'], d['B'], banded_transition(L, 1.0), LocalComm(R), lays,
+                        ScanConfig(chunk=32, warmup=16, adaptive=False))
+    for s in eng.shards:
+        s.set_tuning(tun)
+    logz = torch.zeros(1, dtype=torch.float64, device='cuda')
+    gam = [torch.empty((s.T, 2, L), dtype=torch.float32, device='cuda') for s in eng.shards]
+    eng.e_step(1.0, logz, gamma=gam)
+    assert min(eng.carry_rounds) >= 2, eng.carry_rounds
+    g = np.concatenate([x[s.own].cpu().numpy() for s, x in zip(eng.shards, gam)], 0)
+    P = np.concatenate([s.P[s.own].cpu().numpy() for s in eng.shards], 0)
+    K, logK, A, logA = O.create_transition_prob_1d(L, 1.0)
+    lpa, lz, lca, cs, _, _ = O.smooth_all_step_combined_ma_chunk(d['y'], tun, logK, logA, with_joint=False)
+    close_prob(g, np.exp(lpa))
+    close_prob(P, np.exp(lpa).sum(1))
+    alpha = np.concatenate([s.alpha[s.own].cpu().numpy() for s in eng.shards], 0)
+    close_prob(alpha, np.exp(lca))
+    assert abs(logz.item() - lz) <= 1e-7 * abs(lz)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _gloo_worker(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import poor_man_gplvm_amd as P
+    from poor_man_gplvm_amd.timeshard import DistComm, run_em_timesharded
+    f = np.load(os.path.join(HERE, 'golden', 'em_c1_one.npz'))
+    L = f['basis'].shape[0]
+    res, info = run_em_timesharded(f['y'].astype(np.float32), f['W0'], f['basis'], f['lp0'],
+                                   n_iter=int(f['n_iter']), transition=P.banded_transition(L, float(f['mv'])),
+                                   comm=DistComm(), chunk=16, halo=32,
+                                   adam=P.AdamConfig(maxiter=int(f['maxiter']), tol=float(f['tol'])))
+    out[rank] = None if res is None else (res['posterior_latent_marg'], res['tuning'], res['log_marginal_l'])
+    dist.destroy_process_group()
+
+
+def test_timesharded_gloo_two_ranks():
+    import torch.multiprocessing as mp
+    f = np.load(os.path.join(HERE, 'golden', 'em_c1_one.npz'))
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_gloo_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    assert out[1] is None
+    plm, tun, lz = out[0]
+    np.testing.assert_allclose(tun, f['tuning'], rtol=RT)
+    close_prob(plm, f['posterior'].astype(np.float64).sum(1))
+    np.testing.assert_allclose(lz, f['log_marginal_l'], rtol=1e-7)
