@@ -248,9 +248,7 @@ def bench_timeshard(args):
         te = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
         elapsed = float(te.item())
-    summ = timer.summary()
-    # per-launch figures: a timed section covers every local shard once per EM iteration
-    summ = {k: (c, ms / n) for k, (c, ms) in summ.items()}
+    summ = timer.summary()      # mean per call; every local shard makes its own calls
     st = stats.cpu().numpy()
     adam_iters = float(np.mean(st[args.warmup:, 0])) if args.steps else 0.0
     T_ext = max(s.T for s in eng.shards)

@@ -7,14 +7,15 @@
 // decided on the device from fixed-order f64 sums (bit-identical on every rank of a
 // time-sharded fit, which runs this loop replicated).
 //
-// One body = three launches on the caller's stream:
-//   k_at_rows  F = B W (f64 LDS-tiled GEMM, 64 latents x 64 neurons per workgroup),
-//              f = softplus(F), G = (y_w/(f+1e-20) - t_w) sigmoid(F) -> G (L,N) f64,
-//              per-workgroup partial of sum[xlogy(y_w, f+1e-20) - f t_w]
-//   k_at_grad  g = -B^T G + W/sd^2 (16 basis x 64 neurons per workgroup), partials of
-//              |g|^2 and of the log prior at the evaluated W, then the optax update of
-//              (W, mu, nu) in place (skipped on the initial evaluation)
-//   k_at_ctrl  one workgroup: fixed-order sums -> loss, |g|; histories; stop decision
+// One body = four launches on the caller's stream:
+//   k_at_rows    F = B W (f64 LDS-tiled GEMM, 32 latents x 32 neurons per workgroup),
+//                f = softplus(F), G = (y_w/(f+1e-20) - t_w) sigmoid(F) -> G (L,N) f64,
+//                per-workgroup partial of sum[xlogy(y_w, f+1e-20) - f t_w]
+//   k_at_grad    partial B^T G over 8 slices of L (16 basis x 64 neurons per workgroup)
+//   k_at_update  g = -B^T G + W/sd^2 (slices summed in order), partials of |g|^2 and
+//                of the log prior at the evaluated W, then the optax update of
+//                (W, mu, nu) in place (skipped on the initial evaluation)
+//   k_at_ctrl    one workgroup: fixed-order sums -> loss, |g|; histories; stop decision
 // Every kernel returns immediately once the decision is "stop", so the host enqueues
 // bodies in batches of kBatch and reads the decision word once per batch.
 #include <math.h>
@@ -24,8 +25,12 @@
 namespace pmg {
 
 constexpr int kAtBatch = 16;
-constexpr int kRowTM = 64, kRowTN = 64, kRowTK = 16;   // k_at_rows tile
-constexpr int kGradTK = 16, kGradTN = 64, kGradTL = 64; // k_at_grad tile
+// Small tiles on purpose: at C4 one body is ~160 M f64 FMAs per GEMM, too little to
+// hide a global-load round trip inside a workgroup, so latency is hidden ACROSS
+// workgroups (4-5 resident per CU); LDS reads are mostly broadcasts (cheap).
+constexpr int kRowTM = 32, kRowTN = 32, kRowTK = 16;    // k_at_rows tile (4 outputs / thread)
+constexpr int kGradTK = 16, kGradTN = 64, kGradTL = 32; // k_at_grad tile (4 outputs / thread)
+constexpr int kGradSplit = 8;                           // split of the L reduction
 
 struct AtCtrl {
   int active;   // 1 while the loop runs (the decision for the NEXT body)
@@ -50,6 +55,7 @@ struct AtParams {
   double* err_hist;
   AtCtrl* ctrl;
   double* G;      // (L, N)
+  double* gsplit; // [kGradSplit][NB][N] partial B^T G
   double* lpart;  // [gridRows]
   double* epart;  // [gridGrad]
   double* ppart;  // [gridGrad]
@@ -58,11 +64,12 @@ struct AtParams {
 
 __device__ __forceinline__ double at_sigmoid(double x) { return 1.0 / (1.0 + exp(-x)); }
 
-// fixed-order block sum of one double per thread (256 threads)
-__device__ __forceinline__ double block_sum256(double v, double* sm) {
+// fixed-order block sum of one double per thread (NT threads)
+template <int NT = 256>
+__device__ __forceinline__ double block_sum(double v, double* sm) {
   sm[threadIdx.x] = v;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
+  for (int o = NT / 2; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) sm[threadIdx.x] += sm[threadIdx.x + o];
     __syncthreads();
   }
@@ -78,11 +85,7 @@ __global__ void __launch_bounds__(256) k_at_rows(AtParams p) {
   __shared__ double sm[256];
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int n0 = blockIdx.x * kRowTN, l0 = blockIdx.y * kRowTM;
-  double acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
+  double acc[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
   for (int k0 = 0; k0 < p.NB; k0 += kRowTK) {
     for (int e = threadIdx.x; e < kRowTK * kRowTM; e += 256) {
       const int l = e / kRowTK, k = e % kRowTK;   // consecutive threads walk k (contiguous in B)
@@ -97,58 +100,59 @@ __global__ void __launch_bounds__(256) k_at_rows(AtParams p) {
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < kRowTK; ++k) {
-      double b[4], w[4];
-#pragma unroll
-      for (int a = 0; a < 4; ++a) b[a] = sB[k][ty + 16 * a];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) w[c] = sW[k][tx + 16 * c];
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) acc[a][c] = fma(b[a], w[c], acc[a][c]);
+      const double b0 = sB[k][ty], b1 = sB[k][ty + 16];
+      const double w0 = sW[k][tx], w1 = sW[k][tx + 16];
+      acc[0][0] = fma(b0, w0, acc[0][0]);
+      acc[0][1] = fma(b0, w1, acc[0][1]);
+      acc[1][0] = fma(b1, w0, acc[1][0]);
+      acc[1][1] = fma(b1, w1, acc[1][1]);
     }
     __syncthreads();
   }
   double part = 0.0;
 #pragma unroll
-  for (int a = 0; a < 4; ++a) {
+  for (int a = 0; a < 2; ++a) {
     const int l = l0 + ty + 16 * a;
     if (l >= p.L) continue;
     const double twl = p.tw[l];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < 2; ++c) {
       const int n = n0 + tx + 16 * c;
       if (n >= p.N) continue;
       const double F = acc[a][c];
-      const double f = softplus_d(F);
+      const double ex = exp(-fabs(F));                 // shared by softplus and sigmoid
+      const double f = fmax(F, 0.0) + log1p(ex);        // jax softplus = logaddexp(F, 0)
+      const double sg = F >= 0.0 ? 1.0 / (1.0 + ex) : ex / (1.0 + ex);
       const double fe = f + 1e-20;
       const double y = p.yw[(size_t)l * p.N + n];
-      p.G[(size_t)l * p.N + n] = (y / fe - twl) * at_sigmoid(F);
+      p.G[(size_t)l * p.N + n] = (y / fe - twl) * sg;
       part += (y == 0.0 ? 0.0 : y * log(fe)) - f * twl;
     }
   }
-  const double s = block_sum256(part, sm);
+  const double s = block_sum(part, sm);
   if (threadIdx.x == 0) p.lpart[blockIdx.y * gridDim.x + blockIdx.x] = s;
 }
 
-__global__ void __launch_bounds__(256) k_at_grad(AtParams p, int update) {
+// partial B^T G over one L-slice (blockIdx.z): 16 basis rows x 64 neurons per workgroup
+__global__ void __launch_bounds__(256) k_at_grad(AtParams p) {
   if (!p.ctrl->active) return;
   __shared__ double sG[kGradTL][kGradTN];
   __shared__ double sB[kGradTL][kGradTK + 1];
-  __shared__ double sm[256];
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;   // ty: basis row, tx: 4 neurons
   const int n0 = blockIdx.x * kGradTN, k0 = blockIdx.y * kGradTK;
+  const int span = (p.L + kGradSplit - 1) / kGradSplit;
+  const int la = blockIdx.z * span, lb = min(p.L, la + span);
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int l0 = 0; l0 < p.L; l0 += kGradTL) {
+  for (int l0 = la; l0 < lb; l0 += kGradTL) {
     for (int e = threadIdx.x; e < kGradTL * kGradTN; e += 256) {
       const int l = e / kGradTN, n = e % kGradTN;
       const int gl = l0 + l, gn = n0 + n;
-      sG[l][n] = (gl < p.L && gn < p.N) ? p.G[(size_t)gl * p.N + gn] : 0.0;
+      sG[l][n] = (gl < lb && gn < p.N) ? p.G[(size_t)gl * p.N + gn] : 0.0;
     }
     for (int e = threadIdx.x; e < kGradTL * kGradTK; e += 256) {
       const int l = e / kGradTK, k = e % kGradTK;
       const int gl = l0 + l, gk = k0 + k;
-      sB[l][k] = (gl < p.L && gk < p.NB) ? (double)p.basis[(size_t)gl * p.NB + gk] : 0.0;
+      sB[l][k] = (gl < lb && gk < p.NB) ? (double)p.basis[(size_t)gl * p.NB + gk] : 0.0;
     }
     __syncthreads();
 #pragma unroll 8
@@ -160,22 +164,36 @@ __global__ void __launch_bounds__(256) k_at_grad(AtParams p, int update) {
     __syncthreads();
   }
   const int k = k0 + ty;
-  const double sd = p.prior_std, isd2 = 1.0 / (sd * sd);
-  const double lp_const = -log(sd) - 0.5 * log(2.0 * M_PI);
-  const int64_t cnt = *p.count + 1;
-  const double bc1 = 1.0 - pow(p.b1, (double)cnt), bc2 = 1.0 - pow(p.b2, (double)cnt);
-  double e2 = 0.0, lpr = 0.0;
+  if (k >= p.NB) return;
+  double* out = p.gsplit + ((size_t)blockIdx.z * p.NB + k) * p.N;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const int n = n0 + tx + 16 * c;
-    if (k >= p.NB || n >= p.N) continue;
-    const size_t o = (size_t)k * p.N + n;
+    if (n < p.N) out[n] = acc[c];
+  }
+}
+
+// g = -sum_z gsplit[z] + W/sd^2 (fixed order), |g|^2 and log-prior partials at the
+// evaluated W, then the optax 0.2.2 update of (W, mu, nu) in place when `update`
+__global__ void __launch_bounds__(256) k_at_update(AtParams p, int update) {
+  if (!p.ctrl->active) return;
+  __shared__ double sm[256];
+  const size_t tot = (size_t)p.NB * p.N;
+  const size_t o = (size_t)blockIdx.x * 256 + threadIdx.x;
+  double e2 = 0.0, lpr = 0.0;
+  if (o < tot) {
+    double gs = 0.0;
+#pragma unroll
+    for (int z = 0; z < kGradSplit; ++z) gs += p.gsplit[(size_t)z * tot + o];
+    const double sd = p.prior_std, isd2 = 1.0 / (sd * sd);
     const double w = p.W[o];
-    const double g = -acc[c] + w * isd2;
-    e2 += g * g;
-    const double z = w / sd;
-    lpr += -0.5 * z * z + lp_const;
+    const double g = -gs + w * isd2;
+    e2 = g * g;
+    const double zz = w / sd;
+    lpr = -0.5 * zz * zz - log(sd) - 0.5 * log(2.0 * M_PI);
     if (update) {
+      const int64_t cnt = *p.count + 1;
+      const double bc1 = 1.0 - pow(p.b1, (double)cnt), bc2 = 1.0 - pow(p.b2, (double)cnt);
       const double m = (1.0 - p.b1) * g + p.b1 * p.mu[o];
       const double v = (1.0 - p.b2) * g * g + p.b2 * p.nu[o];
       p.mu[o] = m;
@@ -183,12 +201,11 @@ __global__ void __launch_bounds__(256) k_at_grad(AtParams p, int update) {
       p.W[o] = w + (-p.lr) * ((m / bc1) / (sqrt(v / bc2 + p.eps_root) + p.eps));
     }
   }
-  const double se = block_sum256(e2, sm);
-  const double sp = block_sum256(lpr, sm);
+  const double se = block_sum(e2, sm);
+  const double sp = block_sum(lpr, sm);
   if (threadIdx.x == 0) {
-    const int b = blockIdx.y * gridDim.x + blockIdx.x;
-    p.epart[b] = se;
-    p.ppart[b] = sp;
+    p.epart[blockIdx.x] = se;
+    p.ppart[blockIdx.x] = sp;
   }
 }
 
@@ -208,9 +225,9 @@ __global__ void __launch_bounds__(256) k_at_ctrl(AtParams p, int mode) {
     b += p.ppart[q];
     e += p.epart[q];
   }
-  const double ll = block_sum256(a, sm);
-  const double lpr = block_sum256(b, sm);
-  const double e2 = block_sum256(e, sm);
+  const double ll = block_sum(a, sm);
+  const double lpr = block_sum(b, sm);
+  const double e2 = block_sum(e, sm);
   if (threadIdx.x != 0) return;
   const double loss = -ll - lpr;
   const double err = sqrt(e2);
@@ -241,16 +258,18 @@ __global__ void __launch_bounds__(256) k_at_ctrl(AtParams p, int mode) {
 
 static size_t at_ws(int L, int NB, int N, AtParams* p, void* base) {
   const int gr = ((N + kRowTN - 1) / kRowTN) * ((L + kRowTM - 1) / kRowTM);
-  const int gg = ((N + kGradTN - 1) / kGradTN) * ((NB + kGradTK - 1) / kGradTK);
+  const int gg = (int)(((size_t)NB * N + 255) / 256);
   Carver c(base);
   AtCtrl* ctrl = c.take<AtCtrl>(1);
   double* G = c.take<double>((size_t)L * N);
+  double* gs = c.take<double>((size_t)kGradSplit * NB * N);
   double* lp = c.take<double>(gr);
   double* ep = c.take<double>(gg);
   double* pp = c.take<double>(gg);
   if (p) {
     p->ctrl = ctrl;
     p->G = G;
+    p->gsplit = gs;
     p->lpart = lp;
     p->epart = ep;
     p->ppart = pp;
@@ -309,11 +328,13 @@ int pmg_mstep_adam_tiled(double* W, double* mu, double* nu, int64_t* count, cons
   PMG_HIP(hipMemsetAsync(err_hist, 0, sizeof(double) * (size_t)p.maxiter, st));
   PMG_HIP(hipMemsetAsync(stats, 0, 4 * sizeof(double), st));
   const dim3 grow((N + kRowTN - 1) / kRowTN, (L + kRowTM - 1) / kRowTM);
-  const dim3 ggrad((N + kGradTN - 1) / kGradTN, (NB + kGradTK - 1) / kGradTK);
+  const dim3 ggrad((N + kGradTN - 1) / kGradTN, (NB + kGradTK - 1) / kGradTK, kGradSplit);
+  const dim3 gupd((unsigned)(((size_t)NB * N + 255) / 256));
   hipLaunchKernelGGL(k_at_start, dim3(1), dim3(1), 0, st, p.ctrl);
   PMG_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_at_rows, grow, dim3(256), 0, st, p);
-  hipLaunchKernelGGL(k_at_grad, ggrad, dim3(256), 0, st, p, 0);
+  hipLaunchKernelGGL(k_at_grad, ggrad, dim3(256), 0, st, p);
+  hipLaunchKernelGGL(k_at_update, gupd, dim3(256), 0, st, p, 0);
   hipLaunchKernelGGL(k_at_ctrl, dim3(1), dim3(256), 0, st, p, 0);
   PMG_LAUNCH_CHECK();
   int active = 1;
@@ -321,7 +342,8 @@ int pmg_mstep_adam_tiled(double* W, double* mu, double* nu, int64_t* count, cons
     const int nb = (p.maxiter - 1 - done) < kAtBatch ? (p.maxiter - 1 - done) : kAtBatch;
     for (int b = 0; b < nb; ++b) {
       hipLaunchKernelGGL(k_at_rows, grow, dim3(256), 0, st, p);
-      hipLaunchKernelGGL(k_at_grad, ggrad, dim3(256), 0, st, p, 1);
+      hipLaunchKernelGGL(k_at_grad, ggrad, dim3(256), 0, st, p);
+      hipLaunchKernelGGL(k_at_update, gupd, dim3(256), 0, st, p, 1);
       hipLaunchKernelGGL(k_at_ctrl, dim3(1), dim3(256), 0, st, p, 1);
     }
     PMG_LAUNCH_CHECK();
