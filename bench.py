@@ -396,6 +396,7 @@ def main():
         "fwd_bwd_frac_hbm": B_fb / 1e9 / (t_fb / 1e3) / PEAK_HBM_GBS,
         "adam_iters_mean": adam_iters,
         "chunk": eng.C,
+        "chunk_bwd": eng.Cb,
         "repairs_last": repairs,
         "scan_warmup_fwd_bwd": list(eng.warm),
     }

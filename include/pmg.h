@@ -98,6 +98,20 @@ int pmg_emission_rowref(const double* rblk, int64_t T, int32_t nblk, double like
 int pmg_loglik_materialize(const float* delta, const double* rblk, int64_t T, int32_t L,
                            float* ll, void* stream);
 
+/* Naive-Bayes decoding (no temporal prior) -- decoder.get_naive_bayes_ma_chunk   */
+/* (decoder.py:106-149) / get_naive_bayes_ma (:88-102).                           */
+/* Per-time dt emission, get_loglikelihood_ma_all_changing_dt (decoder.py:73-85):  */
+/* lam = tuning*dt_t[t] + 1e-20, one log per (t, l, n) as in the reference, f64;   */
+/* outputs split as pmg_emission_poisson (delta, rblk).  dt_t (T) f64.            */
+int pmg_emission_poisson_dt(const float* y, const double* gconst, const double* tuning64,
+                            const float* ma_neuron, int32_t ma_is_2d, const uint8_t* ma_latent,
+                            const double* dt_t, int64_t T, int32_t L, int32_t N, float* delta,
+                            double* rblk, void* stream);
+/* Row normalisation of decoder.py:97-100: log_marginal_l[t] = logsumexp_l ll[t,l]  */
+/* (f64), log_post (T,L) f32 = ll - log_marginal_l[t]; ll given as (delta, rblk).    */
+int pmg_naive_bayes_normalize(const float* delta, const double* rblk, int64_t T, int32_t L,
+                              float* log_post, double* log_marginal_l, void* stream);
+
 /* ------------------------------------------------------------------ */
 /* Transition description (gp_kernel.create_transition_prob_1d,         */
 /* gp_kernel.py:42-89): continuous kernel K0[i,j] = g[|i-j|]*invz[i]     */

@@ -33,6 +33,7 @@ EXPORTED_SYMBOLS = (
     "pmg_mstep_workspace_size", "pmg_mstep_adam", "pmg_joint_workspace_size",
     "pmg_joint_accumulate", "pmg_fwdbwd_lpad", "pmg_fwdbwd_state",
     "pmg_mstep_tiled_workspace_size", "pmg_mstep_adam_tiled",
+    "pmg_emission_poisson_dt", "pmg_naive_bayes_normalize",
 )
 
 
@@ -69,6 +70,8 @@ _SIGS = {
     "pmg_emission_workspace_size": ([_I64, _I32, _I32], _SZ),
     "pmg_emission_poisson": ([_P, _P, _P, _P, _P, _D, _I64, _I32, _I32, _I32, _P, _P, _P, _SZ, _P], _I32),
     "pmg_emission_poisson_f64": ([_P, _P, _P, _P, _I32, _P, _D, _I64, _I32, _I32, _P, _P, _P, _SZ, _P], _I32),
+    "pmg_emission_poisson_dt": ([_P, _P, _P, _P, _I32, _P, _P, _I64, _I32, _I32, _P, _P, _P], _I32),
+    "pmg_naive_bayes_normalize": ([_P, _P, _I64, _I32, _P, _P, _P], _I32),
     "pmg_emission_rowref": ([_P, _I64, _I32, _D, _P, _P, _P], _I32),
     "pmg_loglik_materialize": ([_P, _P, _I64, _I32, _P, _P], _I32),
     "pmg_fwdbwd_workspace_size": ([_I64, _I32, _I32], _SZ),

@@ -248,6 +248,56 @@ class PoissonGPLVMJump1D:
         res.update(compute_transition_posterior_prob(r['log_accumulated_joint']))
         return res
 
+    def decode_latent_naive_bayes(self, y, tuning=None, hyperparam={}, ma_neuron=None, ma_latent=None,
+                                  likelihood_scale=1., n_time_per_chunk=10000, dt_l=1., t_l=None):
+        """core.py:788-792 -> core.py:499-524 -> decoder.get_naive_bayes_ma_chunk
+        (decoder.py:106-149): per-time-bin posterior without temporal prior.
+        A constant dt uses the exact int8 emission; a per-time dt_l the f64 per-bin
+        kernel (pmg_emission_poisson_dt); the logsumexp normalisation is
+        pmg_naive_bayes_normalize.  likelihood_scale and n_time_per_chunk are accepted
+        and unused, as in the reference."""
+        if _is_tsd(y):
+            t_l = y.t
+            y = y.d
+        if tuning is None:
+            tuning = self.tuning
+        if ma_neuron is None:
+            ma_neuron = self.ma_neuron_default
+        if ma_latent is None:
+            ma_latent = self.ma_latent_default
+        y = np.asarray(y)
+        T = y.shape[0]
+        dt = np.broadcast_to(np.asarray(dt_l, np.float64), (T,))
+        ma = None if ma_neuron is None else np.asarray(ma_neuron, np.float32)
+        sp = SpikeData(y, ma)
+        eng = DeviceEM(sp, self.n_latent_bin, scan=self.scan_config)
+        eng.set_ma_latent(ma_latent)
+        eng.set_tuning(np.asarray(tuning))
+        dev, L = eng.dev, self.n_latent_bin
+        lib, sh = eng.lib, nat.stream_handle()
+        if np.all(dt == dt[0]):
+            eng._emission_call(sp, sh, float(dt[0]))
+        else:
+            dtt = torch.as_tensor(np.array(dt, dtype=np.float64), device=dev)
+            nat.check(lib.pmg_emission_poisson_dt(nat.ptr(sp.y), nat.ptr(sp.gconst), nat.ptr(eng.tuning64),
+                                                  nat.ptr(sp.ma), int(sp.ma_2d), nat.ptr(eng.ma_latent),
+                                                  nat.ptr(dtt), T, L, sp.N, nat.ptr(eng.delta), nat.ptr(eng.rblk),
+                                                  sh), "pmg_emission_poisson_dt")
+        log_post = torch.empty((T, L), dtype=torch.float32, device=dev)
+        lml = torch.empty(T, dtype=torch.float64, device=dev)
+        nat.check(lib.pmg_naive_bayes_normalize(nat.ptr(eng.delta), nat.ptr(eng.rblk), T, L, nat.ptr(log_post),
+                                                nat.ptr(lml), sh), "pmg_naive_bayes_normalize")
+        lp = _np(log_post)
+        lml_h = _np(lml)
+        posterior_latent = np.exp(lp)
+        if t_l is not None and nap is not None:
+            posterior_latent = nap.TsdFrame(d=posterior_latent, t=t_l)
+        return {'log_posterior_latent': lp,
+                'log_marginal_l': lml_h.astype(np.float32),
+                'log_marginal_total': float(lml_h.sum()),
+                'posterior_latent': posterior_latent,
+                'll_per_pos_l': _np(eng.loglik())}
+
     # ------------------------------------------------------------------ EM
     def fit_em(self, y, hyperparam={}, key=0, n_iter=20, log_posterior_init=None, ma_neuron=None,
                ma_latent=None, n_time_per_chunk=10000, dt=1., likelihood_scale=1., save_every=None,

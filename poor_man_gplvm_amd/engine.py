@@ -56,11 +56,22 @@ class ScanConfig:
                                  # repair, halve it after two E-steps with <=0.1%
     max_warmup: int = 1024
     min_warmup: int = 16
+    chunk_bwd: int | None = None  # backward chunk (None: = chunk if set, else 2x the default)
 
     def chunk_for(self, T):
         if self.chunk:
             return int(self.chunk)
         return max(32, int(math.ceil(T / 2048)))
+
+    def chunk_bwd_for(self, T):
+        """The backward pass runs at ~1 wave per SIMD with twice the forward chunk: its
+        per-step work is larger and its warm-up is then amortised over more output
+        steps (C3 sweep, profiles/r01_c3_chunk_sweep.txt)."""
+        if self.chunk_bwd:
+            return int(self.chunk_bwd)
+        if self.chunk:
+            return int(self.chunk)
+        return 2 * self.chunk_for(T)
 
 
 def default_device():
@@ -175,6 +186,7 @@ class DeviceEM:
         self.T, self.N, self.L = spikes.T, spikes.N, int(L)
         self.scan = scan or ScanConfig()
         self.C = self.scan.chunk_for(self.T)
+        self.Cb = self.scan.chunk_bwd_for(self.T)
         self.nblk = _ru(self.L, 32) // 32
         T, L, N, dev = self.T, self.L, self.N, self.dev
         f32, f64 = torch.float32, torch.float64
@@ -197,7 +209,8 @@ class DeviceEM:
         self.yw = torch.empty((L, N), dtype=f64, device=dev)
         self.tw = torch.empty(L, dtype=f64, device=dev)
         self.ws_em = torch.empty(int(self.lib.pmg_emission_workspace_size(T, L, N)), dtype=torch.uint8, device=dev)
-        self.ws_fb = torch.empty(int(self.lib.pmg_fwdbwd_workspace_size(T, L, self.C)), dtype=torch.uint8, device=dev)
+        self.ws_fb = torch.empty(int(self.lib.pmg_fwdbwd_workspace_size(T, L, min(self.C, self.Cb))),
+                                 dtype=torch.uint8, device=dev)
         ss_bytes = (self.lib.pmg_suffstats_bf16_workspace_size(T, L, N) if spikes.ybt is not None
                     else self.lib.pmg_suffstats_workspace_size(T, L, spikes.Np))
         self.ws_ss = torch.empty(int(ss_bytes), dtype=torch.uint8, device=dev)
@@ -332,8 +345,9 @@ class DeviceEM:
         host sync (pinned async copy + event query)."""
         if not self.scan.adaptive or self._rep_evt is None or not self._rep_evt.query():
             return
-        M = (self.T + self.C - 1) // self.C
+        Ms = ((self.T + self.C - 1) // self.C, (self.T + self.Cb - 1) // self.Cb)
         for i, r in enumerate(int(v) for v in self._rep_host.tolist()):
+            M = Ms[i]
             if r > max(1, M // 100):
                 self.warm[i] = min(self.scan.max_warmup, 2 * self.warm[i])
                 self._clean[i] = 0
@@ -366,7 +380,7 @@ class DeviceEM:
     def backward(self, likelihood_scale, P=True, gamma=None, rho=None):
         sc = self.scan
         args = (nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.alpha), self.T, ctypes.byref(self._tr_c),
-                float(likelihood_scale), self.C, int(self.warm[1]), float(sc.tol),
+                float(likelihood_scale), self.Cb, int(self.warm[1]), float(sc.tol),
                 nat.ptr(self.P) if P else None, nat.ptr(gamma), nat.ptr(rho), nat.ptr(self.ws_fb),
                 self.ws_fb.numel(), nat.stream_handle())
         with self._t('backward_smoother'):       # main chunk-parallel pass (k_backward)

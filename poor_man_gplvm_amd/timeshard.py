@@ -226,10 +226,11 @@ class ShardEM(DeviceEM):
             if ma.ndim == 2:
                 ma = ma[lay.ext_start:lay.ext_stop]
         sp = SpikeData(y_ext, ma, device=device)
+        # one chunk grid for both passes: the carry slots sit on the shard's chunk boundaries
         sc = ScanConfig(chunk=lay.chunk, warmup=scan.warmup, tol=scan.tol, adaptive=scan.adaptive,
-                        max_warmup=scan.max_warmup, min_warmup=scan.min_warmup)
+                        max_warmup=scan.max_warmup, min_warmup=scan.min_warmup, chunk_bwd=lay.chunk)
         super().__init__(sp, L, basis=basis, scan=sc)
-        assert self.C == lay.chunk
+        assert self.C == lay.chunk and self.Cb == lay.chunk
         self.Lpad = int(self.lib.pmg_fwdbwd_lpad(self.L))
         To, hl = lay.T_own, lay.left
         self.own = slice(hl, hl + To)

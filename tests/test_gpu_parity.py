@@ -338,3 +338,37 @@ def test_decode_latent_golden(name):
     np.testing.assert_allclose(r['log_likelihood_all'], f['log_likelihood_all'], rtol=2e-7, atol=1e-5)
     for k in ['p_transition_latent', 'p_transition_dynamics', 'p_joint_dynamics', 'p_joint_latent']:
         np.testing.assert_allclose(r[k], f[k], rtol=1e-4, atol=1e-7)
+
+
+# ----------------------------------------------------------------------------- naive Bayes
+@pytest.mark.parametrize("case", ["dt1", "dt_const", "dt_per_t", "masked", "masked_dt_per_t"])
+def test_decode_latent_naive_bayes_vs_oracle(case):
+    """decode_latent_naive_bayes (core.py:499-524 -> decoder.py:73-149): constant dt on
+    the int8 emission, per-time dt on the f64 per-bin kernel; probabilities within
+    rel 1e-5 (atol 1e-12), per-bin log marginals rel 1e-7, ll as test_emission."""
+    import poor_man_gplvm_amd as P
+    N, L, T = 40, 100, 700
+    d = make(N, L, T)
+    rng = np.random.default_rng(5)
+    dt = 1.0
+    ma = ml = None
+    if case == "dt_const":
+        dt = 0.37
+    if case in ("dt_per_t", "masked_dt_per_t"):
+        dt = rng.uniform(0.3, 1.7, size=T)
+    if case.startswith("masked"):
+        ma = (rng.random((T, N)) > 0.2).astype(np.float32)
+        ml = (rng.random(L) > 0.3).astype(np.float32)
+    m = P.PoissonGPLVMJump1D(N, n_latent_bin=L, tuning_lengthscale=10.)
+    res = m.decode_latent_naive_bayes(d['y'], tuning=d['tuning'], ma_neuron=ma, ma_latent=ml, dt_l=dt)
+    assert list(res) == ['log_posterior_latent', 'log_marginal_l', 'log_marginal_total', 'posterior_latent',
+                         'll_per_pos_l']
+    lp, lml, lmt, ll = O.naive_bayes_chunk(d['y'], d['tuning'], ma, ml, dt)
+    keep = np.ones(L, bool) if ml is None else ml.astype(bool)
+    close_prob(res['posterior_latent'][:, keep], np.exp(lp)[:, keep])
+    argmax_match(res['posterior_latent'], np.exp(lp))
+    np.testing.assert_allclose(res['log_marginal_l'], lml, rtol=1e-7, atol=1e-4)
+    assert abs(res['log_marginal_total'] - lmt) <= 1e-9 * abs(lmt)
+    np.testing.assert_allclose(res['ll_per_pos_l'], ll, rtol=2e-7, atol=1e-5)
+    if ml is not None:
+        assert np.all(res['posterior_latent'][:, ~keep] == 0.0)
