@@ -279,17 +279,29 @@ struct BlockTeam {
 __device__ __forceinline__ float hilbert_dist(const float* __restrict__ x, const float* __restrict__ y, int n,
                               const float* __restrict__ w = nullptr, int L = 0, int Lpad = 0) {
   const int lane = threadIdx.x & 63;
-  // optional weights w in the (2, L) alpha-row layout for state index i = d*Lpad + j
-  auto wt = [&](int i) -> float {
-    if (!w) return 1.f;
-    const int d = i >= Lpad ? 1 : 0, j = i - d * Lpad;
-    return j < L ? w[d * L + j] : 0.f;
-  };
+  // every operand is fetched up front (n = 2*Lpad <= 2048: at most 32 per lane) so the
+  // wave pays one memory round trip, not one per strided pass
+  constexpr int kMaxPer = 2 * 1024 / 64;
+  float xv[kMaxPer], yv[kMaxPer];
+#pragma unroll
+  for (int q = 0; q < kMaxPer; ++q) {
+    const int i = lane + 64 * q;
+    float wi = 0.f;
+    if (i < n) {
+      wi = 1.f;
+      if (w) {  // optional weights w in the (2, L) alpha-row layout for state index i = d*Lpad + j
+        const int d = i >= Lpad ? 1 : 0, j = i - d * Lpad;
+        wi = j < L ? w[d * L + j] : 0.f;
+      }
+    }
+    xv[q] = i < n ? x[i] * wi : 0.f;
+    yv[q] = i < n ? y[i] * wi : 0.f;
+  }
   float xm = 0.f, ym = 0.f;
-  for (int i = lane; i < n; i += 64) {
-    const float wi = wt(i);
-    xm = fmaxf(xm, x[i] * wi);
-    ym = fmaxf(ym, y[i] * wi);
+#pragma unroll
+  for (int q = 0; q < kMaxPer; ++q) {
+    xm = fmaxf(xm, xv[q]);
+    ym = fmaxf(ym, yv[q]);
   }
   xm = wave_max_shfl(xm);
   ym = wave_max_shfl(ym);
@@ -302,9 +314,9 @@ __device__ __forceinline__ float hilbert_dist(const float* __restrict__ x, const
   const float lo_thr = w ? 1e-14f : 1e-30f, hi_thr = w ? 1e-12f : 1e-20f;
   float lo = INFINITY, hi = -INFINITY;
   int bad = 0;
-  for (int i = lane; i < n; i += 64) {
-    const float wi = wt(i);
-    const float a = x[i] * wi * ix, b = y[i] * wi * iy;
+#pragma unroll
+  for (int q = 0; q < kMaxPer; ++q) {
+    const float a = xv[q] * ix, b = yv[q] * iy;
     if (a > lo_thr && b > lo_thr) {
       const float r = __logf(a) - __logf(b);
       lo = fminf(lo, r);

@@ -12,13 +12,20 @@ namespace pmg {
 // reaches gamma_t(i), t < t_e, only through the joint P(x_t = i, x_{t_e} = j) <=
 // gamma_{t_e}(j), so components with negligible posterior cannot move any output
 // above ~1e-18 probability, while they are exactly the ones the chain forgets slowly.
+// prev (nullable): the flags of the previous round.  A boundary that passed before can
+// only fail again if the chunk whose output it compares against (c + off) was
+// recomputed in that round, so every other boundary is skipped without a load.
 __global__ void __launch_bounds__(256) k_verify(float* __restrict__ x, const float* __restrict__ y,
                                                 int first, int last, int off, int SZ, float tol,
                                                 int* __restrict__ flags, const float* __restrict__ w,
-                                                int C, int L, int Lpad) {
+                                                int C, int L, int Lpad, const int* __restrict__ prev) {
   const int wv = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int c = first + wv;
   if (c > last) return;
+  if (prev && prev[c + off] == 0) {
+    if ((threadIdx.x & 63) == 0) flags[c] = 0;
+    return;
+  }
   const float* yc = y + (size_t)(c + off) * SZ;
   float* xc = x + (size_t)c * SZ;
   const float* wc = w ? w + (size_t)(c + 1) * C * 2 * L : nullptr;
@@ -49,11 +56,12 @@ struct FBWork {
   float *s_in, *s_out, *b_in, *b_first;
   double* chunk_logz;
   int* flags;
+  int* flags_b;   // the other verify round's flags (double-buffered)
   int* repairs;
 };
 
 // workspace layout (the Python diagnostics mirror it): repairs[64] | s_in | s_out |
-// b_in | b_first (M x 2 x Lpad f32 each) | chunk_logz[M] | flags[M]
+// b_in | b_first (M x 2 x Lpad f32 each) | chunk_logz[M] | flags[M] | flags_b[M]
 static FBWork carve_fb(void* ws, int64_t T, int Lpad, int C, size_t* total = nullptr) {
   const int64_t M = (T + C - 1) / C;
   Carver c(ws);
@@ -65,6 +73,7 @@ static FBWork carve_fb(void* ws, int64_t T, int Lpad, int C, size_t* total = nul
   w.b_first = c.take<float>((size_t)M * 2 * Lpad);
   w.chunk_logz = c.take<double>(M);
   w.flags = c.take<int>(M);
+  w.flags_b = c.take<int>(M);
   if (total) *total = c.off + 256;
   return w;
 }
@@ -212,9 +221,12 @@ static int forward_impl(const float* delta, const float* phi, const double* m, i
       const int nver = p.M - 1;
       const bool no_repair = getenv("PMG_DEBUG_NO_REPAIR") != nullptr;
       for (int round = 0; round <= kFixRounds; ++round) {
+        int* cur = (round & 1) ? w.flags_b : w.flags;
+        const int* prev = round == 0 ? nullptr : ((round & 1) ? w.flags : w.flags_b);
+        p.flags = cur;
         hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4), dim3(256), 0, st, w.s_in,
-                           (const float*)w.s_out, 1, p.M - 1, -1, 2 * p.Lpad, p.tol, w.flags,
-                           (const float*)nullptr, 0, 0, 0);
+                           (const float*)w.s_out, 1, p.M - 1, -1, 2 * p.Lpad, p.tol, cur,
+                           (const float*)nullptr, 0, 0, 0, prev);
         PMG_LAUNCH_CHECK();
         if (no_repair) break;
         if (round < kFixRounds) {
@@ -285,9 +297,12 @@ static int backward_impl(const float* delta, const float* phi, const float* alph
     const int nver = p.M - 1;
     const bool no_repair = getenv("PMG_DEBUG_NO_REPAIR") != nullptr;
     for (int round = 0; round <= kFixRounds; ++round) {
+      int* cur = (round & 1) ? w.flags_b : w.flags;
+      const int* prev = round == 0 ? nullptr : ((round & 1) ? w.flags : w.flags_b);
+      p.flags = cur;
       hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4), dim3(256), 0, st, w.b_in,
-                         (const float*)w.b_first, 0, p.M - 2, 1, 2 * p.Lpad, p.tol, w.flags,
-                         alpha, p.C, p.L, p.Lpad);
+                         (const float*)w.b_first, 0, p.M - 2, 1, 2 * p.Lpad, p.tol, cur,
+                         alpha, p.C, p.L, p.Lpad, prev);
       PMG_LAUNCH_CHECK();
       if (no_repair) break;
       if (round < kFixRounds) {
