@@ -470,6 +470,54 @@ def naive_bayes_chunk(y, tuning, ma_neuron=None, ma_latent=None, dt_l=1.0, n_tim
 
 
 # ----------------------------------------------------------------------------
+# latent-only model (decoder_latentonly.py, core.py:76-375 / :919-1019)
+# ----------------------------------------------------------------------------
+def create_transition_prob_latent_1d(n_latent, movement_variance=1.0):
+    """gp_kernel.py:92-118: row-normalised RBF over latent bins (the same kernel as
+    the jump model's continuous dynamics, create_transition_prob_1d logK[0])."""
+    K, logK, _, _ = create_transition_prob_1d(n_latent, movement_variance)
+    return K[0], logK[0]
+
+
+def smooth_latent_only(y, tuning, logK, ma_neuron=None, ma_latent=None, likelihood_scale=1.0):
+    """decoder_latentonly.py:34-226 in one chunk (the chunk carries are exact, so the
+    result does not depend on n_time_per_chunk): filter from log(1/L)
+    (:58-80), RTS smoother seeded with the last filter posterior and a -1e40 joint
+    (:126-154).  Returns (acausal (T,L), logZ, causal (T,L), log c_t (T), joint (L,L),
+    ll (T,L))."""
+    ll = loglikelihood_poisson_all(y, tuning, ma_neuron, ma_latent)
+    T, L = ll.shape
+    post = np.log(np.ones(L, _F) / L)
+    logz = 0.0
+    causal = np.empty((T, L), _F)
+    prior = np.empty((T, L), _F)
+    cs = np.empty(T, _F)
+    for t in range(T):
+        pr = logsumexp(post[:, None] + logK, axis=0)                        # :45-48
+        u = pr + likelihood_scale * ll[t]
+        c = logsumexp(u)
+        post = u - c
+        logz += c
+        causal[t], prior[t], cs[t] = post, pr, c
+    acausal = np.empty((T, L), _F)
+    acausal[T - 1] = causal[T - 1]
+    joint = np.full((L, L), -1e40, _F)
+    for t in range(T - 2, -1, -1):
+        inside = logK + (acausal[t + 1] - prior[t + 1])[None, :] + causal[t][:, None]   # :109-112
+        acausal[t] = logsumexp(inside, axis=1)
+        joint = np.logaddexp(joint, inside)
+    return acausal, float(logz), causal, cs, joint, ll
+
+
+def compute_transition_posterior_prob_latent(log_joint):
+    """decoder_latentonly.py:227-252."""
+    lj = log_joint - logsumexp(log_joint)
+    lt = lj - logsumexp(lj, axis=1, keepdims=True)
+    return {'p_joint_latent': np.exp(lj), 'p_transition_latent': np.exp(lt),
+            'log_joint_latent': lj, 'log_transition_latent': lt}
+
+
+# ----------------------------------------------------------------------------
 # synthetic data (numpy RNG; the reference's JAX PRNG cannot be reproduced)
 # ----------------------------------------------------------------------------
 def init_latent_posterior_from_uniform(u, random_scale=0.1):

@@ -543,3 +543,141 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
     info = {'opt_state': {'mu': _np(mu), 'nu': _np(nu), 'count': int(_np(cnt)[0])},
             'params64': _np(W), 'repairs': eng.repairs(), 'chunk': eng.C}
     return res, info
+
+
+class PoissonGPLVM1D(PoissonGPLVMJump1D):
+    """Poisson GPLVM with a smooth 1-d latent and no dynamics (core.py:919-1019 over
+    AbstractGPLVM1D, core.py:76-375; decoder_latentonly.py).
+
+    The latent-only chain is the jump engine with the dynamics pinned to
+    A = [[1, 0], [1, 0]] (p_move_to_jump = 0, p_jump_to_move = 1): starting from the
+    uniform (d, l) state, the continuous prior is K^T (1/L) exactly as
+    filter_all_step_latent starts from log(1/L) (decoder_latentonly.py:66-68), the jump
+    state's prior is exactly 0 at every step, and every latent-only quantity (filter,
+    smoother, logZ, one-step marginals, pairwise joint) is the d = 0 block of the jump
+    engine's.  basis_type 'rbf' with smoothness_penalty = 0 (the default objective
+    poisson_m_step_objective); the b-spline smoothness objective is not implemented."""
+
+    def __init__(self, n_neuron, n_latent_bin=100, tuning_lengthscale=5., param_prior_std=1.,
+                 movement_variance=1., explained_variance_threshold_basis=0.999, rng_init_int=123,
+                 w_init_variance=1., w_init_mean=0., basis_type='rbf', custom_tuning_kernel=None,
+                 custom_transition_kernel=None, smoothness_penalty=0., scan_config: ScanConfig | None = None):
+        if basis_type != 'rbf' or smoothness_penalty != 0.:
+            raise NotImplementedError("PoissonGPLVM1D: only basis_type='rbf' with smoothness_penalty=0 "
+                                      "(poisson_m_step_objective) is implemented")
+        super().__init__(n_neuron, n_latent_bin=n_latent_bin, tuning_lengthscale=tuning_lengthscale,
+                         param_prior_std=param_prior_std, movement_variance=movement_variance,
+                         explained_variance_threshold_basis=explained_variance_threshold_basis,
+                         rng_init_int=rng_init_int, w_init_variance=w_init_variance, w_init_mean=w_init_mean,
+                         p_move_to_jump=0.0, p_jump_to_move=1.0, basis_type=basis_type,
+                         custom_tuning_kernel=custom_tuning_kernel,
+                         custom_transition_kernel=custom_transition_kernel,
+                         smoothness_penalty=smoothness_penalty, scan_config=scan_config)
+        del self.possible_dynamics
+
+    def _transition(self, movement_variance, p_move_to_jump=0.0, p_jump_to_move=1.0):
+        return banded_transition(self.n_latent_bin, movement_variance, 0.0, 1.0, self.custom_transition_kernel)
+
+    def init_latent_posterior(self, T, key, random_scale=0.1):
+        """core.py:241-251: (1/L + U(0,1)*scale), row-normalised, log (numpy RNG)."""
+        L = self.n_latent_bin
+        post = np.ones((T, L)) / L + _rng(key).random((T, L)) * random_scale
+        post = post / post.sum(axis=1, keepdims=True)
+        with np.errstate(divide='ignore'):
+            lp = np.log(post)
+        lp = np.where(lp == -np.inf, -1e40, lp)
+        return lp.astype(np.float32), post.astype(np.float32)
+
+    def decode_latent(self, y, tuning=None, hyperparam={}, ma_neuron=None, ma_latent=None,
+                      likelihood_scale=1., n_time_per_chunk=10000, t_l=None):
+        """core.py:136-177 + decoder_latentonly.compute_transition_posterior_prob_latent
+        (decoder_latentonly.py:227-252)."""
+        if _is_tsd(y):
+            t_l = y.t
+            y = y.d
+        if tuning is None:
+            tuning = self.tuning
+        if ma_neuron is None:
+            ma_neuron = self.ma_neuron_default
+        if ma_latent is None:
+            ma_latent = self.ma_latent_default
+        hp = dict(hyperparam)
+        hp['p_move_to_jump'], hp['p_jump_to_move'] = 0.0, 1.0
+        mv = hp.get('movement_variance', self.movement_variance)
+        _, logK, _, logA = create_transition_prob_1d(self.n_latent_bin, mv, 0.0, 1.0, self.custom_transition_kernel)
+        r = self._run_decode(y, tuning, hp, ma_neuron, ma_latent, likelihood_scale, joint=True, logK=logK, logA=logA)
+        posterior_all = r['posterior_all'][:, 0]
+        if t_l is not None and nap is not None:
+            posterior_all = nap.TsdFrame(d=posterior_all, t=t_l)
+        res = {'log_posterior_all': r['log_posterior_all'][:, 0],
+               'log_marginal_final': r['log_marginal_final'],
+               'posterior_all': posterior_all,
+               'log_one_step_predictive_marginals_all': r['log_one_step_predictive_marginals_all'],
+               'log_likelihood_all': r['log_likelihood_all']}
+        res.update(compute_transition_posterior_prob_latent(r['log_accumulated_joint'][0, 0]))
+        return res
+
+    def fit_em(self, y, hyperparam={}, key=0, n_iter=20, log_posterior_init=None, ma_neuron=None,
+               ma_latent=None, n_time_per_chunk=10000, dt=1., likelihood_scale=1., save_every=None,
+               m_step_step_size=0.01, m_step_maxiter=1000, m_step_tol=1e-6,
+               posterior_init_kwargs={'random_scale': 0.1}, verboase=True, **kwargs):
+        """core.py:1000-1019 + AbstractGPLVM1D.fit_em (core.py:259-375): returns its 13 keys."""
+        hp = dict(hyperparam)
+        hp['p_move_to_jump'], hp['p_jump_to_move'] = 0.0, 1.0
+        r = super().fit_em(y, hyperparam=hp, key=key, n_iter=n_iter, log_posterior_init=log_posterior_init,
+                           ma_neuron=ma_neuron, ma_latent=ma_latent, n_time_per_chunk=n_time_per_chunk, dt=dt,
+                           likelihood_scale=likelihood_scale, save_every=save_every,
+                           m_step_step_size=m_step_step_size, m_step_maxiter=m_step_maxiter,
+                           m_step_tol=m_step_tol, posterior_init_kwargs=posterior_init_kwargs, verboase=verboase)
+        del self.log_latent_transition_kernel_l, self.log_dynamics_transition_kernel
+        self.log_latent_transition_kernel = create_transition_prob_1d(
+            self.n_latent_bin, self.movement_variance, 0.0, 1.0, self.custom_transition_kernel)[1][0]
+        posterior = r['posterior'][:, 0]
+        if _is_tsd(y):
+            posterior = nap.TsdFrame(d=posterior, t=y.t)
+        return {'log_posterior_all_saved': [lp[:, 0] for lp in r['log_posterior_all_saved']],
+                'log_posterior_init': r['log_posterior_init'],
+                'params_saved': r['params_saved'],
+                'tuning_saved': r['tuning_saved'],
+                'iter_saved': r['iter_saved'],
+                'params': r['params'],
+                'tuning': r['tuning'],
+                'log_posterior_final': r['log_posterior_final'][:, 0],
+                'log_marginal': r['log_marginal'],
+                'log_marginal_l': r['log_marginal_l'],
+                'log_marginal_saved': r['log_marginal_saved'],
+                'posterior': posterior,
+                'm_step_res_l': r['m_step_res_l']}
+
+    def sample_latent(self, T, key=0, movement_variance=1, init_latent=None):
+        """core.py:209-229 with a numpy RNG: latent from K[prev]."""
+        rng = _rng(key)
+        K, _ = create_transition_prob_1d(self.n_latent_bin, movement_variance, 0.0, 1.0)[:2]
+        cK = np.cumsum(K[0], 1)
+        l = int(rng.integers(self.n_latent_bin)) if init_latent is None else int(init_latent)
+        out = np.empty(T, np.int32)
+        u = rng.random(T)
+        for t in range(T):
+            l = int(min(np.searchsorted(cK[l], u[t] * cK[l, -1], side='right'), self.n_latent_bin - 1))
+            out[t] = l
+        return out
+
+    def sample(self, T, hyperparam={}, key=0, init_latent=None, dt=1., tuning=None):
+        """core.py:231-239."""
+        rng = _rng(key)
+        k1, k2 = int(rng.integers(2 ** 31)), int(rng.integers(2 ** 31))
+        mv = hyperparam.get('movement_variance', self.movement_variance)
+        latent_l = self.sample_latent(T, k1, mv, init_latent)
+        return latent_l, self.sample_y(latent_l, hyperparam, tuning, dt, k2)
+
+
+def compute_transition_posterior_prob_latent(log_accumulated_joint_total):
+    """decoder_latentonly.py:227-252 on the host (f64): normalised joint and
+    row-conditional transition of the latent-only model, keys in jax's sorted order."""
+    from scipy.special import logsumexp
+    lj = np.asarray(log_accumulated_joint_total, np.float64)
+    lj = lj - logsumexp(lj)
+    lt = lj - logsumexp(lj, axis=1, keepdims=True)
+    r = {'p_joint_latent': np.exp(lj), 'p_transition_latent': np.exp(lt),
+         'log_joint_latent': lj, 'log_transition_latent': lt}
+    return {k: r[k].astype(np.float32) for k in sorted(r)}

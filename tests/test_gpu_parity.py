@@ -372,3 +372,69 @@ def test_decode_latent_naive_bayes_vs_oracle(case):
     np.testing.assert_allclose(res['ll_per_pos_l'], ll, rtol=2e-7, atol=1e-5)
     if ml is not None:
         assert np.all(res['posterior_latent'][:, ~keep] == 0.0)
+
+
+# ----------------------------------------------------------------------------- latent-only model
+@pytest.mark.parametrize("masked", [False, True])
+def test_latent_only_decode_vs_oracle(masked):
+    """PoissonGPLVM1D.decode_latent (core.py:136-177, decoder_latentonly.py) vs the f64
+    restatement oracle.smooth_latent_only (pinned by path enumeration)."""
+    import poor_man_gplvm_amd as P
+    N, L, T = 30, 100, 900
+    d = make(N, L, T)
+    ml = None
+    if masked:
+        ml = (np.random.default_rng(2).random(L) > 0.2).astype(np.float32)
+    m = P.PoissonGPLVM1D(N, n_latent_bin=L, tuning_lengthscale=10.)
+    res = m.decode_latent(d['y'], tuning=d['tuning'], ma_latent=ml)
+    assert list(res) == ['log_posterior_all', 'log_marginal_final', 'posterior_all',
+                         'log_one_step_predictive_marginals_all', 'log_likelihood_all', 'log_joint_latent',
+                         'log_transition_latent', 'p_joint_latent', 'p_transition_latent']
+    _, logK = O.create_transition_prob_latent_1d(L, 1.0)
+    lpa, lz, lca, cs, lj, ll = O.smooth_latent_only(d['y'], d['tuning'], logK, ma_latent=ml)
+    close_prob(res['posterior_all'], np.exp(lpa))
+    argmax_match(res['posterior_all'], np.exp(lpa))
+    assert abs(res['log_marginal_final'] - lz) <= 1e-7 * abs(lz)
+    np.testing.assert_allclose(res['log_one_step_predictive_marginals_all'], cs, rtol=1e-6, atol=1e-5)
+    ref = O.compute_transition_posterior_prob_latent(lj)
+    np.testing.assert_allclose(res['p_joint_latent'], ref['p_joint_latent'], rtol=1e-4,
+                               atol=1e-5 * ref['p_joint_latent'].max())
+    # row-conditional transitions: rows the posterior visits (joint row mass > 1e-6);
+    # a nearly unvisited row is a ratio of two tiny f32-rounded sums
+    keep = np.ones(L, bool) if ml is None else ml.astype(bool)
+    rows = keep & (ref['p_joint_latent'].sum(1) > 1e-6)
+    np.testing.assert_allclose(res['p_transition_latent'][np.ix_(rows, keep)],
+                               ref['p_transition_latent'][np.ix_(rows, keep)], rtol=1e-4, atol=1e-6)
+
+
+def test_latent_only_fit_em_one_iteration_vs_oracle():
+    """PoissonGPLVM1D.fit_em (core.py:259-375, :1000-1019): M-step from the injected
+    posterior (the same Adam loop), then the latent-only E-step."""
+    import poor_man_gplvm_amd as P
+    N, L, T = 30, 100, 600
+    d = make(N, L, T)
+    m = P.PoissonGPLVM1D(N, n_latent_bin=L, tuning_lengthscale=10.)
+    m.params = d['W0'][:, :N] if d['W0'].shape[0] == m.n_basis else m.params
+    W0 = np.asarray(m.params, np.float64)
+    B = np.asarray(m.tuning_basis, np.float64)
+    # an informative injected posterior (around the sampled latent path): the model's own
+    # init (1/L + U*0.1, core.py:241-251) is nearly flat, and the E-step after an M-step
+    # from it is ill-conditioned enough that fp32 rounding alone moves P by ~1e-5
+    # (the float32 reference-mimic deviates by 1.2e-5 there)
+    lat = d['latent'][:, 1]
+    post = np.exp(-(np.arange(L)[None, :] - lat[:, None]) ** 2 / 8.0) + 1e-3
+    lp0 = np.log(post / post.sum(1, keepdims=True)).astype(np.float32)
+    res = m.fit_em(d['y'], n_iter=1, log_posterior_init=lp0, m_step_maxiter=40, m_step_tol=0.0)
+    assert list(res) == ['log_posterior_all_saved', 'log_posterior_init', 'params_saved', 'tuning_saved',
+                         'iter_saved', 'params', 'tuning', 'log_posterior_final', 'log_marginal',
+                         'log_marginal_l', 'log_marginal_saved', 'posterior', 'm_step_res_l']
+    mr = O.m_step(W0, d['y'].astype(np.float64), lp0.astype(np.float64), B, 1.0, O.adam_init(W0), maxiter=40, tol=0.0)
+    tun = O.get_tuning_softplus(mr['params'], B)
+    np.testing.assert_allclose(res['tuning'], tun, rtol=RT)
+    _, logK = O.create_transition_prob_latent_1d(L, 1.0)
+    lpa, lz, *_ = O.smooth_latent_only(d['y'], tun, logK)
+    close_prob(res['posterior'], np.exp(lpa))
+    argmax_match(res['posterior'], np.exp(lpa))
+    np.testing.assert_allclose(res['log_marginal_l'], [lz], rtol=1e-7)
+    assert res['m_step_res_l']['n_iter'] == [mr['n_iter']]
+    assert res['posterior'].shape == (T, L) and res['log_posterior_final'].shape == (T, L)

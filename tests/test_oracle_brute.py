@@ -78,3 +78,23 @@ def test_emission_formula():
     exp1 = sum(ma[n] * (xlogy(y[1, n], lam[0, n]) - lam[0, n] - gammaln(y[1, n] + 1)) for n in range(3))
     np.testing.assert_allclose(ll[:, 0], [exp0, exp1], rtol=1e-14)
     assert np.all(ll[:, 1] == -1e20)
+
+
+@pytest.mark.parametrize("L,T,mv,s", [(3, 4, 1.0, 1.0), (4, 3, 0.5, 0.6), (2, 1, 1.0, 1.0), (5, 3, 2.0, 1.3)])
+def test_latent_only_vs_enumeration(L, T, mv, s):
+    """decoder_latentonly restatement (D = 1) vs path enumeration."""
+    rng = np.random.default_rng(L * 10 + T)
+    K, logK = O.create_transition_prob_latent_1d(L, mv)
+    ll = rng.normal(size=(T, L)) * 2.0
+    post, joint, logZ, cs = brute.enumerate_posteriors(ll, K[None], np.ones((1, 1)), s)
+    orig = O.loglikelihood_poisson_all
+    try:
+        O.loglikelihood_poisson_all = lambda yy, tt, mn, ml, dt=1.0: ll
+        lpa, lz, lca, c, lj, _ = O.smooth_latent_only(np.zeros((T, 2)), np.zeros((L, 2)), logK, likelihood_scale=s)
+    finally:
+        O.loglikelihood_poisson_all = orig
+    np.testing.assert_allclose(np.exp(lpa), post[:, 0], atol=1e-12)
+    np.testing.assert_allclose(lz, logZ, rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(c, cs, atol=1e-12)
+    if T > 1:
+        np.testing.assert_allclose(np.exp(lj), joint[0, 0], atol=1e-12)
