@@ -80,14 +80,20 @@ __global__ void __launch_bounds__(256) k_rates_prepare(
 // A[row r][k = 16h .. 16h+15] and B[k = 16h ..][col r]; the same (h, byte) -> k
 // assignment on both operands keeps the K pairing consistent.
 // C/D: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*h.
-constexpr int ET = 128, EL = 64, EKC = 128, EROW = EKC + 16;
+constexpr int ET = 128, EL = 64, EKC = 64, EROW = EKC + 16;
+// EKC = 64: the double-buffered stage (sY 20 KB + sQ 51 KB) lets two workgroups share a
+// CU, so one workgroup's epilogue and first loads overlap the other's MFMAs (at 128 B
+// chunks the 129 KB stage held the CU alone).  Rows of 80 B: 16 consecutive rows still
+// start on distinct bank quads (5 is odd).
+constexpr int ESEG = EKC / 16;                 // 16-byte segments per staged row
+constexpr int EQSEG = kDig * EL * ESEG;        // digit segments per chunk (1280)
 
 __device__ __forceinline__ int xcd_group(int bid, int nwg) {
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-__global__ void __launch_bounds__(512) k_emission_i8(
+__global__ void __launch_bounds__(512, 4) k_emission_i8(
     const int8_t* __restrict__ yq, const int8_t* __restrict__ qd,
     const double* __restrict__ lamsum, const double* __restrict__ gconst,
     const uint8_t* __restrict__ ma_latent, int64_t T, int64_t Tp, int L, int Lp, int Kp, int nLT,
@@ -106,33 +112,37 @@ __global__ void __launch_bounds__(512) k_emission_i8(
   const size_t plane = (size_t)Lp * Kp;
 
   // branch-free staging loads (Kp is a multiple of EKC): rows past Tp / Lp are
-  // clamped -- their outputs are never written.
-  const int sc = (tid & 7) * 16;
-  int64_t ty0 = t0 + (tid >> 3), ty1 = ty0 + 64;
-  ty0 = ty0 < Tp ? ty0 : Tp - 1;
-  ty1 = ty1 < Tp ? ty1 : Tp - 1;
-  const int8_t* yrow0 = yq + ty0 * Kp + sc;
-  const int8_t* yrow1 = yq + ty1 * Kp + sc;
-  int lq = l0 + (tid >> 3);
-  lq = lq < Lp ? lq : Lp - 1;
-  const int8_t* qrow = qd + (size_t)lq * Kp + sc;
+  // clamped -- their outputs are never written.  One spike segment and up to three
+  // digit segments per thread.
+  const int ysr = tid / ESEG, ysc = (tid % ESEG) * 16;
+  int64_t ty = t0 + ysr;
+  ty = ty < Tp ? ty : Tp - 1;
+  const int8_t* yrow = yq + ty * Kp + ysc;
+  const int8_t* qsrc[3];
+  int qdst[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    int sgi = tid + 512 * i;
+    sgi = sgi < EQSEG ? sgi : EQSEG - 1;          // the third slot is partly idle
+    const int d = sgi / (EL * ESEG), rem = sgi % (EL * ESEG);
+    const int row = rem / ESEG, col = (rem % ESEG) * 16;
+    int lq = l0 + row;
+    lq = lq < Lp ? lq : Lp - 1;
+    qsrc[i] = qd + d * plane + (size_t)lq * Kp + col;
+    qdst[i] = (d * EL + row) * EROW + col;
+  }
+  const bool q2 = tid + 1024 < EQSEG;
 #define PMG_EM_LOAD(k0)                                                      \
-  ry0 = *reinterpret_cast<const uint4*>(yrow0 + (k0));                      \
-  ry1 = *reinterpret_cast<const uint4*>(yrow1 + (k0));                      \
-  rq0 = *reinterpret_cast<const uint4*>(qrow + (k0));                       \
-  rq1 = *reinterpret_cast<const uint4*>(qrow + plane + (k0));               \
-  rq2 = *reinterpret_cast<const uint4*>(qrow + 2 * plane + (k0));           \
-  rq3 = *reinterpret_cast<const uint4*>(qrow + 3 * plane + (k0));           \
-  rq4 = *reinterpret_cast<const uint4*>(qrow + 4 * plane + (k0));
+  ry0 = *reinterpret_cast<const uint4*>(yrow + (k0));                       \
+  rq0 = *reinterpret_cast<const uint4*>(qsrc[0] + (k0));                    \
+  rq1 = *reinterpret_cast<const uint4*>(qsrc[1] + (k0));                    \
+  rq2 = *reinterpret_cast<const uint4*>(qsrc[2] + (k0));
 #define PMG_EM_STORE(b)                                                      \
-  *reinterpret_cast<uint4*>(&sY[b][tid >> 3][sc]) = ry0;                    \
-  *reinterpret_cast<uint4*>(&sY[b][64 + (tid >> 3)][sc]) = ry1;             \
-  *reinterpret_cast<uint4*>(&sQ[b][0][tid >> 3][sc]) = rq0;                 \
-  *reinterpret_cast<uint4*>(&sQ[b][1][tid >> 3][sc]) = rq1;                 \
-  *reinterpret_cast<uint4*>(&sQ[b][2][tid >> 3][sc]) = rq2;                 \
-  *reinterpret_cast<uint4*>(&sQ[b][3][tid >> 3][sc]) = rq3;                 \
-  *reinterpret_cast<uint4*>(&sQ[b][4][tid >> 3][sc]) = rq4;
-  uint4 ry0, ry1, rq0, rq1, rq2, rq3, rq4;
+  *reinterpret_cast<uint4*>(&sY[b][ysr][ysc]) = ry0;                        \
+  *reinterpret_cast<uint4*>(&sQ[b][0][0][0] + qdst[0]) = rq0;               \
+  *reinterpret_cast<uint4*>(&sQ[b][0][0][0] + qdst[1]) = rq1;               \
+  if (q2) *reinterpret_cast<uint4*>(&sQ[b][0][0][0] + qdst[2]) = rq2;
+  uint4 ry0, rq0, rq1, rq2;
 
   v16i acc[kDig];
 #pragma unroll
