@@ -231,6 +231,9 @@ typedef struct pmg_adam_cfg {
   int32_t maxiter;
 } pmg_adam_cfg;
 size_t pmg_mstep_workspace_size(int32_t N, int32_t maxiter);
+/* 1 when pmg_mstep_adam holds this (L, NB, N) shape (basis in registers + LDS, */
+/* L <= 512), else 0: the caller then uses pmg_mstep_adam_tiled.               */
+int pmg_mstep_adam_supported(int32_t L, int32_t NB, int32_t N);
 int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const float* basis,
                    const double* yw, const double* tw, int32_t L, int32_t NB, int32_t N,
                    const pmg_adam_cfg* cfg, double* stats, double* loss_hist, double* err_hist,

@@ -45,7 +45,7 @@ __all__ = [
     "get_statistics", "poisson_m_step_objective", "poisson_m_step_grad",
     "adam_init", "adam_update", "adam_run", "m_step", "fit_em", "decode_latent",
     "naive_bayes_chunk", "init_latent_posterior_from_uniform", "sample_latent",
-    "sample_spikes",
+    "sample_spikes", "jump_consensus", "downsampled_lml",
 ]
 
 NEG_MASK = -1e20          # decoder.py:46  masked latent log-likelihood
@@ -548,3 +548,43 @@ def sample_latent(T, L, rng, movement_variance=1.0, p_move_to_jump=0.01, p_jump_
 def sample_spikes(tuning, latent, rng, dt=1.0):
     """core.py:795-800: y ~ Poisson(tuning[latent] * dt)."""
     return rng.poisson(np.asarray(tuning, np.float64)[latent] * dt)
+
+
+def jump_consensus(jump_p, jump_p_all_chain, window_size=5, jump_p_thresh=0.4, consensus_thresh=0.8):
+    """model_selection_helper.py:264-299, as scalar Python loops over chains and
+    window rows (the window is jump_p_all_chain[jti-window_size : jti+window_size],
+    numpy slice rules, negative start included)."""
+    T, n_chain = np.asarray(jump_p_all_chain).shape
+    ok_l, keep = [], []
+    for jti in range(len(jump_p)):
+        if not jump_p[jti] >= jump_p_thresh:
+            continue
+        rows = list(range(T))[jti - window_size:jti + window_size]
+        n_hit = 0
+        for c in range(n_chain):
+            if any(jump_p_all_chain[r][c] > jump_p_thresh for r in rows):
+                n_hit += 1
+        ok = (n_hit / n_chain) >= consensus_thresh
+        ok_l.append(ok)
+        if ok:
+            keep.append(jti)
+    frac = float(np.mean(ok_l)) if ok_l else float('nan')
+    filt = np.zeros(len(jump_p))
+    filt[keep] = 1
+    return frac, filt, np.array(ok_l, dtype=bool)
+
+
+def downsampled_lml(y, tuning, masks, movement_variance=1.0, p_move_to_jump=0.01, p_jump_to_move=0.01,
+                    ma_neuron=None, likelihood_scale=1.0):
+    """model_selection_helper.py:243-260 with the latent masks given explicitly:
+    log_marginal_final of one decode per mask, and their mean / std."""
+    L = tuning.shape[0]
+    _, logK, _, logA = create_transition_prob_1d(L, movement_variance, p_move_to_jump, p_jump_to_move)
+    lml = []
+    for m in masks:
+        _, logz, *_ = smooth_all_step_combined_ma_chunk(np.asarray(y, _F), np.asarray(tuning, _F), logK.astype(_F),
+                                                        logA.astype(_F), ma_neuron, np.asarray(m), likelihood_scale,
+                                                        with_joint=False)
+        lml.append(float(logz))
+    lml = np.array(lml)
+    return lml, lml.mean(), lml.std()

@@ -30,7 +30,7 @@ EXPORTED_SYMBOLS = (
     "pmg_forward_filter_phase", "pmg_backward_smoother_phase",
     "pmg_suffstats_workspace_size", "pmg_suffstats", "pmg_exp", "pmg_log",
     "pmg_spikes_bf16t", "pmg_suffstats_bf16_workspace_size", "pmg_suffstats_bf16",
-    "pmg_mstep_workspace_size", "pmg_mstep_adam", "pmg_joint_workspace_size",
+    "pmg_mstep_workspace_size", "pmg_mstep_adam_supported", "pmg_mstep_adam", "pmg_joint_workspace_size",
     "pmg_joint_accumulate", "pmg_fwdbwd_lpad", "pmg_fwdbwd_state",
     "pmg_mstep_tiled_workspace_size", "pmg_mstep_adam_tiled",
     "pmg_emission_poisson_dt", "pmg_naive_bayes_normalize",
@@ -94,6 +94,7 @@ _SIGS = {
     "pmg_exp": ([_P, _I64, _P, _P], _I32),
     "pmg_log": ([_P, _I64, _P, _P], _I32),
     "pmg_mstep_workspace_size": ([_I32, _I32], _SZ),
+    "pmg_mstep_adam_supported": ([_I32, _I32, _I32], ctypes.c_int),
     "pmg_mstep_adam": ([_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, ctypes.POINTER(AdamCfg),
                         _P, _P, _P, _P, _SZ, _P], _I32),
     "pmg_mstep_tiled_workspace_size": ([_I32, _I32, _I32], _SZ),

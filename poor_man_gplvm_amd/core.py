@@ -180,6 +180,9 @@ class PoissonGPLVMJump1D:
                 res['log_one_step_predictive_marginals_all'], res['log_accumulated_joint'],
                 res['log_likelihood_all'])
 
+    def _check_latent_mask(self, tr, ma_latent):
+        """Hook for models without a jump state (PoissonGPLVM1D)."""
+
     def _run_decode(self, y, tuning, hyperparam, ma_neuron, ma_latent, likelihood_scale, joint=True,
                     logK=None, logA=None):
         mv = hyperparam.get('movement_variance', self.movement_variance)
@@ -187,9 +190,11 @@ class PoissonGPLVMJump1D:
         pjm = hyperparam.get('p_jump_to_move', self.p_jump_to_move)
         y = np.asarray(y)
         ma = None if ma_neuron is None else np.asarray(ma_neuron, np.float32)
+        tr = self._transition(mv, pmj, pjm)
+        self._check_latent_mask(tr, ma_latent)
         sp = SpikeData(y, ma)
         eng = DeviceEM(sp, self.n_latent_bin, scan=self.scan_config)
-        eng.set_transition(self._transition(mv, pmj, pjm))
+        eng.set_transition(tr)
         eng.set_ma_latent(ma_latent)
         eng.set_tuning(np.asarray(tuning))
         dev = eng.dev
@@ -297,6 +302,46 @@ class PoissonGPLVMJump1D:
                 'log_marginal_total': float(lml_h.sum()),
                 'posterior_latent': posterior_latent,
                 'll_per_pos_l': _np(eng.loglik())}
+
+    def log_marginal_masked(self, y, ma_latent_l, tuning=None, hyperparam={}, ma_neuron=None,
+                            likelihood_scale=1.):
+        """log_marginal_final of decode_latent(y, ma_latent=m) for every mask m in
+        ma_latent_l ((R, L) or a list), as an (R,) float64 array.
+
+        This is the inner loop of model_selection_helper.get_downsampled_lml
+        (model_selection_helper.py:243-260), which reads nothing from each decode
+        but log_marginal_final.  So the spikes are uploaded once, the transition and
+        tuning are set once, and each mask runs only the emission and the forward
+        filter (logZ is the filter's Σ_t c_t, decoder.py:151-187).  The backward
+        pass, the joint and the host copies of (T, D, L) tensors are skipped.
+        Every logZ stays on the device until one copy at the end."""
+        if _is_tsd(y):
+            y = y.d
+        if tuning is None:
+            tuning = self.tuning
+        if ma_neuron is None:
+            ma_neuron = self.ma_neuron_default
+        masks = np.asarray(ma_latent_l)
+        if masks.ndim != 2 or masks.shape[1] != self.n_latent_bin:
+            raise ValueError(f"ma_latent_l must have shape (R, {self.n_latent_bin})")
+        if not np.all(masks.any(axis=1)):
+            raise ValueError("every latent mask must keep at least one latent bin")
+        mv = hyperparam.get('movement_variance', self.movement_variance)
+        pmj = hyperparam.get('p_move_to_jump', self.p_move_to_jump)
+        pjm = hyperparam.get('p_jump_to_move', self.p_jump_to_move)
+        ma = None if ma_neuron is None else np.asarray(ma_neuron, np.float32)
+        tr = self._transition(mv, pmj, pjm)
+        for m in masks:
+            self._check_latent_mask(tr, m)
+        eng = DeviceEM(SpikeData(np.asarray(y), ma), self.n_latent_bin, scan=self.scan_config)
+        eng.set_transition(tr)
+        eng.set_tuning(np.asarray(tuning))
+        logz = torch.zeros(len(masks), dtype=torch.float64, device=eng.dev)
+        for r, m in enumerate(masks):
+            eng.set_ma_latent(m)
+            eng.emission(likelihood_scale)
+            eng.forward(likelihood_scale, logz[r:r + 1])
+        return _np(logz).astype(np.float64)
 
     # ------------------------------------------------------------------ EM
     def fit_em(self, y, hyperparam={}, key=0, n_iter=20, log_posterior_init=None, ma_neuron=None,
@@ -578,6 +623,21 @@ class PoissonGPLVM1D(PoissonGPLVMJump1D):
     def _transition(self, movement_variance, p_move_to_jump=0.0, p_jump_to_move=1.0):
         return banded_transition(self.n_latent_bin, movement_variance, 0.0, 1.0, self.custom_transition_kernel)
 
+    def _check_latent_mask(self, tr, ma_latent):
+        """Without a jump state, the only way across a run of masked latent bins is one
+        continuous-kernel step of weight exp(-gap^2/mv^2).  The reference keeps those
+        log-domain terms (logK is dense, gp_kernel.py:42-89); the device band stops at
+        tr.band bins (weights below 1e-30 of the centre, under the fp32 range).  A mask
+        whose kept bins are more than tr.band apart therefore has no faithful banded
+        form: raise instead of returning a different log marginal."""
+        if ma_latent is None:
+            return
+        kept = np.flatnonzero(np.asarray(ma_latent) != 0)
+        if kept.size > 1 and int(np.diff(kept).max()) > tr.band:
+            raise NotImplementedError(
+                f"PoissonGPLVM1D: ma_latent leaves a gap of {int(np.diff(kept).max())} latent bins between kept "
+                f"bins, wider than the continuous-kernel band ({tr.band}) of the device scan")
+
     def init_latent_posterior(self, T, key, random_scale=0.1):
         """core.py:241-251: (1/L + U(0,1)*scale), row-normalised, log (numpy RNG)."""
         L = self.n_latent_bin
@@ -624,6 +684,7 @@ class PoissonGPLVM1D(PoissonGPLVMJump1D):
         """core.py:1000-1019 + AbstractGPLVM1D.fit_em (core.py:259-375): returns its 13 keys."""
         hp = dict(hyperparam)
         hp['p_move_to_jump'], hp['p_jump_to_move'] = 0.0, 1.0
+        self._check_latent_mask(self._transition(hp.get('movement_variance', self.movement_variance)), ma_latent)
         r = super().fit_em(y, hyperparam=hp, key=key, n_iter=n_iter, log_posterior_init=log_posterior_init,
                            ma_neuron=ma_neuron, ma_latent=ma_latent, n_time_per_chunk=n_time_per_chunk, dt=dt,
                            likelihood_scale=likelihood_scale, save_every=save_every,

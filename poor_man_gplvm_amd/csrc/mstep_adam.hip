@@ -583,6 +583,15 @@ size_t pmg_mstep_workspace_size(int32_t N, int32_t maxiter) {
   return adam_ws(G, maxiter > 1 ? maxiter : 1, nullptr, nullptr);
 }
 
+int pmg_mstep_adam_supported(int32_t L, int32_t NB, int32_t N) {
+  if (L <= 0 || L > kThreads || NB <= 0 || N <= 0) return 0;
+  int S, G, ng, LG;
+  adam_geometry(N, L, NB, S, G, ng, LG);
+  if (S > kSMax || NB * S > kThreads) return 0;
+  AdamKernel kern = pick_adam(NB, S);
+  return (kern.fn != nullptr && kern.lds <= 160 * 1024) ? 1 : 0;
+}
+
 int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const float* basis,
                    const double* yw, const double* tw, int32_t L, int32_t NB, int32_t N,
                    const pmg_adam_cfg* cfg, double* stats, double* loss_hist, double* err_hist,

@@ -288,7 +288,8 @@ class DeviceEM:
     def adam(self, W, mu, nu, count, cfg: AdamConfig, stats_out, lh_out, eh_out):
         if self.basis is None:
             raise ValueError("no basis")
-        tiled = self.L > self.PERSISTENT_MAX_L or self.NB > self.PERSISTENT_MAX_NB
+        tiled = (self.L > self.PERSISTENT_MAX_L or self.NB > self.PERSISTENT_MAX_NB
+                 or not self.lib.pmg_mstep_adam_supported(self.L, self.NB, self.N))
         need = int(self.lib.pmg_mstep_tiled_workspace_size(self.L, self.NB, self.N) if tiled
                    else self.lib.pmg_mstep_workspace_size(self.N, int(cfg.maxiter)))
         if self.ws_ad is None or self.ws_ad.numel() < need:

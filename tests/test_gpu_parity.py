@@ -215,9 +215,13 @@ def test_suffstats_nonint_spikes_use_f32_path():
                                                    (128, 256, 60, 0.0, False), (7, 48, 1, 1e-6, False),
                                                    (30, 100, 40, 0.0, True), (30, 100, 1000, 1e-6, True),
                                                    (7, 48, 1, 1e-6, True), (7, 48, 2, 1e-6, True),
-                                                   (64, 1024, 30, 0.0, True), (40, 700, 1000, 1e-6, True)])
+                                                   (64, 1024, 30, 0.0, True), (40, 700, 1000, 1e-6, True),
+                                                   (20, 100, 40, 0.0, False)])
 def test_adam_vs_oracle(N, L, maxiter, tol, tiled):
-    """tiled: pmg_mstep_adam_tiled (forced for small shapes; L > 512 / NB > 128 always)."""
+    """tiled: pmg_mstep_adam_tiled (forced for small shapes; L > 512 / NB > 128 always).
+    (20, 100, ..., False) is the class default basis (ls = 1 => NB = 101): the
+    persistent kernel does not hold it and pmg_mstep_adam_supported routes it to
+    the tiled kernel."""
     from poor_man_gplvm_amd.engine import AdamConfig
     d = make(N, L, 500)
     sp, eng = _engine(d, L)
