@@ -113,6 +113,25 @@ int pmg_naive_bayes_normalize(const float* delta, const double* rblk, int64_t T,
                               float* log_post, double* log_marginal_l, void* stream);
 
 /* ------------------------------------------------------------------ */
+/* Gaussian observation model -- GaussianGPLVMJump1D (core.py:852-917).  */
+/* tuning = basis @ W  (fit_tuning_helper.get_tuning_linear, :12-17).     */
+int pmg_tuning_linear(const float* basis, const double* W, int32_t L, int32_t NB, int32_t N,
+                      double* tuning64, float* tuning32, void* stream);
+/* ll[t,l] = sum_n m[t,n] norm.logpdf(y[t,n], tuning[l,n]*dt, noise_std), -1e20   */
+/* where ma_latent == 0 (decoder.get_loglikelihood_ma_gaussian, decoder.py:50-57). */
+/* f64 accumulation; output split as pmg_emission_poisson (delta, rblk).           */
+int pmg_emission_gaussian(const float* y, const double* tuning64, const float* ma_neuron, int32_t ma_is_2d,
+                          const uint8_t* ma_latent, double noise_std, double dt, int64_t T, int32_t L,
+                          int32_t N, float* delta, double* rblk, void* stream);
+/* Analytic M-step, fit_tuning_helper.gaussian_m_step_analytic (:44-61):          */
+/* W (NB,N) f64 = solve(B^T diag(t_w) B / s^2 + I / p^2, B^T y_w / s^2), Cholesky */
+/* in f64 (H is SPD).  status (device int32) = 1 if a pivot was not positive.      */
+size_t pmg_gaussian_mstep_workspace_size(int32_t NB, int32_t N);
+int pmg_gaussian_mstep(const float* basis, const double* yw, const double* tw, int32_t L, int32_t NB, int32_t N,
+                       double noise_std, double prior_std, double* W, int32_t* status, void* workspace,
+                       size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------ */
 /* Transition description (gp_kernel.create_transition_prob_1d,         */
 /* gp_kernel.py:42-89): continuous kernel K0[i,j] = g[|i-j|]*invz[i]     */
 /* (row-normalised RBF, exactly zero beyond |i-j| > band in the f32       */

@@ -45,7 +45,8 @@ __all__ = [
     "get_statistics", "poisson_m_step_objective", "poisson_m_step_grad",
     "adam_init", "adam_update", "adam_run", "m_step", "fit_em", "decode_latent",
     "naive_bayes_chunk", "init_latent_posterior_from_uniform", "sample_latent",
-    "sample_spikes", "jump_consensus", "downsampled_lml",
+    "sample_spikes", "jump_consensus", "downsampled_lml", "loglikelihood_gaussian_all",
+    "gaussian_m_step_analytic", "fit_em_gaussian",
 ]
 
 NEG_MASK = -1e20          # decoder.py:46  masked latent log-likelihood
@@ -248,8 +249,27 @@ def smooth_all_step(causal_post, causal_prior, logK, logA, carry_init=None, with
     return out, joint
 
 
+def loglikelihood_gaussian_all(y, tuning, noise_std, ma_neuron=None, ma_latent=None, dt=1.0):
+    """decoder.py:50-57 vmapped over time: ll[t,l] = sum_n m[t,n] *
+    norm.logpdf(y[t,n], tuning[l,n]*dt, noise_std); ll[:, ~ma_latent] = -1e20."""
+    y = np.asarray(y, _F)
+    mu = np.asarray(tuning, _F) * dt
+    T, N = y.shape
+    m = np.ones((T, N), _F) if ma_neuron is None else np.broadcast_to(np.asarray(ma_neuron, _F), (T, N))
+    s = float(noise_std)
+    c0 = -math.log(s) - 0.5 * math.log(2 * math.pi)
+    # sum_n m*(c0 - (y - mu)^2 / (2 s^2)), expanded into matrix products
+    ll = (c0 * m.sum(1, keepdims=True) - 0.5 / s ** 2 * ((m * y * y).sum(1, keepdims=True)
+                                                         - 2.0 * (m * y) @ mu.T + m @ (mu * mu).T))
+    if ma_latent is not None:
+        ml = np.asarray(ma_latent).astype(bool)
+        ll = np.where(ml[None, :], ll, NEG_MASK)
+    return ll
+
+
 def smooth_all_step_combined_ma_chunk(y, tuning, logK, logA, ma_neuron=None, ma_latent=None,
-                                      likelihood_scale=1.0, n_time_per_chunk=10000, with_joint=True):
+                                      likelihood_scale=1.0, n_time_per_chunk=10000, with_joint=True,
+                                      noise_std=None):
     """decoder.py:258-332: forward filter chunk by chunk with carry
     (post[-1], logZ) (:299), then backward smoother over chunks in reverse
     with carry (acausal[0], joint) (:322); the prior slice for chunk n is
@@ -271,7 +291,10 @@ def smooth_all_step_combined_ma_chunk(y, tuning, logK, logA, ma_neuron=None, ma_
             mn = ma_neuron_arr[sl]
         else:
             mn = ma_neuron_arr
-        ll = loglikelihood_poisson_all(y[sl], tuning, mn, ma_latent)
+        if noise_std is None:
+            ll = loglikelihood_poisson_all(y[sl], tuning, mn, ma_latent)
+        else:                                               # observation_model='gaussian'
+            ll = loglikelihood_gaussian_all(y[sl], tuning, noise_std, mn, ma_latent)
         p, logz, pr, c = filter_all_step(ll, logK, logA, carry_init=carry, likelihood_scale=likelihood_scale)
         carry = (p[-1], logz)
         posts.append(p); priors.append(pr); cs.append(c); lls.append(ll)
@@ -439,6 +462,46 @@ def fit_em(y, params, basis, log_posterior_init, n_iter=20, movement_variance=1.
             'log_marginal_saved': saved['log_marginal_saved'], 'posterior': posterior,
             'posterior_latent_marg': posterior.sum(1), 'posterior_dynamics_marg': posterior.sum(2),
             'm_step_res_l': m_step_res_l, 'opt_state': opt_state}
+
+
+def gaussian_m_step_analytic(basis, yw, tw, noise_std, param_prior_std):
+    """fit_tuning_helper.py:44-61: W = solve(B^T diag(tw) B / s^2 + I / p^2, B^T yw / s^2)."""
+    B = np.asarray(basis, _F)
+    G = np.einsum('qd,q,qb->db', B, np.asarray(tw, _F), B)
+    H = G / noise_std ** 2 + np.eye(B.shape[1]) / param_prior_std ** 2
+    return np.linalg.solve(H, B.T @ np.asarray(yw, _F) / noise_std ** 2)
+
+
+def fit_em_gaussian(y, params, basis, log_posterior_init, n_iter=20, movement_variance=1.0,
+                    p_move_to_jump=0.01, p_jump_to_move=0.01, noise_std=0.5, param_prior_std=1.0,
+                    ma_neuron=None, ma_latent=None, likelihood_scale=1.0, stats_dtype=None):
+    """GaussianGPLVMJump1D.fit_em (core.py:905-917) over AbstractGPLVMJump1D.fit_em
+    (core.py:592-713): analytic M-step (core.py:898-904), linear tuning
+    (fit_tuning_helper.py:12-17), Gaussian emission.  Returns params, tuning,
+    posterior, log_marginal_l.  stats_dtype (e.g. np.float32) rounds y_w, t_w to that
+    type before the solve: the tests use it to measure how far fp32 sufficient
+    statistics alone move the fit (the noise floor of an fp32-stats implementation)."""
+    y = np.asarray(y, _F)
+    L = basis.shape[0]
+    _, logK, _, logA = create_transition_prob_1d(L, movement_variance, p_move_to_jump, p_jump_to_move)
+    W = np.asarray(params, _F)
+    basis = np.asarray(basis, _F)
+    logpost = np.asarray(log_posterior_init, _F)
+    lml = []
+    for i in range(n_iter):
+        yw, tw = get_statistics(logpost, y)
+        if stats_dtype is not None:
+            yw, tw = yw.astype(stats_dtype).astype(_F), tw.astype(stats_dtype).astype(_F)
+        W = gaussian_m_step_analytic(basis, yw, tw, noise_std, param_prior_std)
+        tuning = basis @ W
+        out = smooth_all_step_combined_ma_chunk(y, tuning, logK.astype(_F), logA.astype(_F), ma_neuron, ma_latent,
+                                                likelihood_scale, with_joint=False, noise_std=noise_std)
+        lpa, logz = out[0], out[1]
+        logpost = logsumexp(lpa, axis=1)
+        lml.append(logz)
+    post = np.exp(lpa)
+    return {'params': W, 'tuning': tuning, 'posterior': post, 'posterior_latent_marg': post.sum(1),
+            'log_marginal_l': lml, 'log_marginal': lml[-1]}
 
 
 def decode_latent(y, tuning, movement_variance=1.0, p_move_to_jump=0.01, p_jump_to_move=0.01,

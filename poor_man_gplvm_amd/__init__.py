@@ -6,7 +6,8 @@ in include/pmg.h); PyTorch provides device memory, streams and torch.distributed
 """
 __version__ = "0.1.0"
 
-from .core import (PoissonGPLVM1D, PoissonGPLVMJump1D, compute_transition_posterior_prob,  # noqa: F401
+from .core import (GaussianGPLVMJump1D, PoissonGPLVM1D, PoissonGPLVMJump1D,  # noqa: F401
+                   compute_transition_posterior_prob,
                    compute_transition_posterior_prob_latent, run_em)
 from .engine import AdamConfig, ScanConfig  # noqa: F401
 from .gp_kernel import banded_transition, create_transition_prob_1d, generate_basis  # noqa: F401

@@ -34,6 +34,7 @@ EXPORTED_SYMBOLS = (
     "pmg_joint_accumulate", "pmg_fwdbwd_lpad", "pmg_fwdbwd_state",
     "pmg_mstep_tiled_workspace_size", "pmg_mstep_adam_tiled",
     "pmg_emission_poisson_dt", "pmg_naive_bayes_normalize",
+    "pmg_tuning_linear", "pmg_emission_gaussian", "pmg_gaussian_mstep_workspace_size", "pmg_gaussian_mstep",
 )
 
 
@@ -100,6 +101,12 @@ _SIGS = {
     "pmg_mstep_tiled_workspace_size": ([_I32, _I32, _I32], _SZ),
     "pmg_mstep_adam_tiled": ([_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, ctypes.POINTER(AdamCfg),
                               _P, _P, _P, _P, _SZ, _P], _I32),
+    "pmg_tuning_linear": ([_P, _P, _I32, _I32, _I32, _P, _P, _P], _I32),
+    "pmg_emission_gaussian": ([_P, _P, _P, _I32, _P, ctypes.c_double, ctypes.c_double, _I64, _I32, _I32,
+                               _P, _P, _P], _I32),
+    "pmg_gaussian_mstep_workspace_size": ([_I32, _I32], _SZ),
+    "pmg_gaussian_mstep": ([_P, _P, _P, _I32, _I32, _I32, ctypes.c_double, ctypes.c_double, _P, _P, _P, _SZ,
+                            _P], _I32),
     "pmg_joint_workspace_size": ([_I64, _I32], _SZ),
     "pmg_joint_accumulate": ([_P, _P, _I64, _I32, _P, _P, _SZ, _P], _I32),
 }

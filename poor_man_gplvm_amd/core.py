@@ -183,6 +183,9 @@ class PoissonGPLVMJump1D:
     def _check_latent_mask(self, tr, ma_latent):
         """Hook for models without a jump state (PoissonGPLVM1D)."""
 
+    def _observation(self, eng, hyperparam):
+        """Hook: the Gaussian model switches the engine's emission here."""
+
     def _run_decode(self, y, tuning, hyperparam, ma_neuron, ma_latent, likelihood_scale, joint=True,
                     logK=None, logA=None):
         mv = hyperparam.get('movement_variance', self.movement_variance)
@@ -194,6 +197,7 @@ class PoissonGPLVMJump1D:
         self._check_latent_mask(tr, ma_latent)
         sp = SpikeData(y, ma)
         eng = DeviceEM(sp, self.n_latent_bin, scan=self.scan_config)
+        self._observation(eng, hyperparam)
         eng.set_transition(tr)
         eng.set_ma_latent(ma_latent)
         eng.set_tuning(np.asarray(tuning))
@@ -334,6 +338,7 @@ class PoissonGPLVMJump1D:
         for m in masks:
             self._check_latent_mask(tr, m)
         eng = DeviceEM(SpikeData(np.asarray(y), ma), self.n_latent_bin, scan=self.scan_config)
+        self._observation(eng, hyperparam)
         eng.set_transition(tr)
         eng.set_tuning(np.asarray(tuning))
         logz = torch.zeros(len(masks), dtype=torch.float64, device=eng.dev)
@@ -388,7 +393,7 @@ class PoissonGPLVMJump1D:
                      save_every=save_every,
                      adam=AdamConfig(lr=m_step_step_size, maxiter=m_step_maxiter, tol=m_step_tol,
                                      prior_std=hp['param_prior_std']),
-                     scan=self.scan_config)
+                     scan=self.scan_config, noise_std=getattr(self, '_fit_noise_std', None))
         self.params = res['params']
         self.tuning = res['tuning']
         self.fit_info = info
@@ -504,8 +509,10 @@ def compute_transition_posterior_prob(log_accumulated_joint_total):
 
 def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=None, ma_latent=None,
            likelihood_scale=1.0, save_every=None, adam: AdamConfig | None = None,
-           scan: ScanConfig | None = None, opt_state=None, timing=None):
+           scan: ScanConfig | None = None, opt_state=None, timing=None, noise_std=None):
     """The EM loop of core.py:650-676 on one GPU; returns the fit_em dict (core.py:696-712).
+    noise_std: Gaussian observation model (analytic M-step, linear tuning; adam.prior_std
+    is the parameter prior) instead of the Poisson one.
     `timing`, if a list, receives per-iteration wall-clock seconds (bench)."""
     adam = adam or AdamConfig()
     y = np.asarray(y)
@@ -519,6 +526,8 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
     eng = DeviceEM(sp, L, basis=B, scan=scan)
     eng.set_transition(transition)
     eng.set_ma_latent(ma_latent)
+    if noise_std is not None:
+        eng.noise_std, eng.gauss_prior_std = float(noise_std), float(adam.prior_std)
     mlat = None if ma_latent is None else np.asarray(ma_latent).astype(bool)
     eng.set_log_posterior(log_posterior_init)
     dev = eng.dev
@@ -585,9 +594,84 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
            'posterior_latent_marg': posterior.sum(axis=1),
            'posterior_dynamics_marg': posterior.sum(axis=2),
            'm_step_res_l': m_step_res_l}
+    if noise_std is not None:
+        eng.gaussian_status()
+        res['m_step_res_l'] = {'params': [], 'opt_state': []}      # core.py:655-658 with m_step core.py:898-904
     info = {'opt_state': {'mu': _np(mu), 'nu': _np(nu), 'count': int(_np(cnt)[0])},
             'params64': _np(W), 'repairs': eng.repairs(), 'chunk': eng.C}
     return res, info
+
+
+class GaussianGPLVMJump1D(PoissonGPLVMJump1D):
+    """Gaussian GPLVM with jumps (core.py:852-917): tuning = basis @ W
+    (fit_tuning_helper.get_tuning_linear, :12-17), y ~ N(tuning[latent] * dt, noise_std),
+    analytic M-step (gaussian_m_step_analytic, fit_tuning_helper.py:44-61; no optimiser
+    state).  Same jump dynamics, scans, sufficient statistics and result dicts as the
+    Poisson model; the emission, tuning and M-step run in gaussian.hip."""
+
+    def __init__(self, n_neuron, noise_std=0.5, **kwargs):
+        super().__init__(n_neuron, **kwargs)
+        self.noise_std = noise_std
+
+    def _observation(self, eng, hyperparam):
+        eng.noise_std = float(hyperparam.get('noise_std', self.noise_std))
+        eng.gauss_prior_std = float(hyperparam.get('param_prior_std', self.param_prior_std))
+
+    def get_tuning(self, params, hyperparam, tuning_basis):
+        """fit_tuning_helper.get_tuning_linear (:12-17), on the device (f64)."""
+        B = np.asarray(tuning_basis, np.float32)
+        W = np.asarray(params, np.float64)
+        dev = default_device()
+        lib = nat.load()
+        bt = torch.as_tensor(np.ascontiguousarray(B), device=dev)
+        wt = torch.as_tensor(np.ascontiguousarray(W), device=dev)
+        out = torch.empty((B.shape[0], W.shape[1]), dtype=torch.float32, device=dev)
+        nat.check(lib.pmg_tuning_linear(nat.ptr(bt), nat.ptr(wt), B.shape[0], B.shape[1], W.shape[1],
+                                        None, nat.ptr(out), nat.stream_handle()), "pmg_tuning_linear")
+        return _np(out)
+
+    def m_step(self, param_curr, y, log_posterior_curr, tuning_basis, hyperparam, opt_state_curr=None):
+        """core.py:898-904: suff-stats then the analytic solve; {'params', 'opt_state': None}."""
+        y = np.asarray(y)
+        B = np.asarray(tuning_basis, np.float32)
+        eng = DeviceEM(SpikeData(y, None), B.shape[0], basis=B, scan=self.scan_config)
+        self._observation(eng, hyperparam)
+        eng.set_log_posterior(log_posterior_curr)
+        W = torch.zeros((B.shape[1], y.shape[1]), dtype=torch.float64, device=eng.dev)
+        eng.m_step(W, None, None, None, None, None, None, None)
+        eng.gaussian_status()
+        return {'params': _np(W).astype(np.float32), 'opt_state': None}
+
+    def fit_em(self, y, hyperparam={}, key=0, n_iter=20, log_posterior_init=None, ma_neuron=None,
+               ma_latent=None, n_time_per_chunk=10000, dt=1., likelihood_scale=1., save_every=None, **kwargs):
+        """core.py:905-917 over AbstractGPLVMJump1D.fit_em (core.py:592-713)."""
+        hp = dict(hyperparam)
+        hp['noise_std'] = hp.get('noise_std', self.noise_std)
+        hp['param_prior_std'] = hp.get('param_prior_std', self.param_prior_std)
+        self._fit_noise_std = hp['noise_std']
+        try:
+            return super().fit_em(y, hyperparam=hp, key=key, n_iter=n_iter, log_posterior_init=log_posterior_init,
+                                  ma_neuron=ma_neuron, ma_latent=ma_latent, n_time_per_chunk=n_time_per_chunk,
+                                  dt=dt, likelihood_scale=likelihood_scale, save_every=save_every, **kwargs)
+        finally:
+            self._fit_noise_std = None
+
+    def decode_latent(self, y, tuning=None, hyperparam={}, **kwargs):
+        """core.py:879-882: noise_std from hyperparam or the model."""
+        hp = dict(hyperparam)
+        hp['noise_std'] = hp.get('noise_std', self.noise_std)
+        return super().decode_latent(y, tuning=tuning, hyperparam=hp, **kwargs)
+
+    def decode_latent_naive_bayes(self, *args, **kwargs):
+        raise NotImplementedError("GaussianGPLVMJump1D.decode_latent_naive_bayes is not implemented on the device")
+
+    def sample_y(self, latent_l, hyperparam={}, tuning=None, dt=1., key=10):
+        """core.py:889-896: N(tuning[latent] * dt, noise_std * sqrt(dt))."""
+        if tuning is None:
+            tuning = self.tuning
+        s = hyperparam.get('noise_std', self.noise_std) * math.sqrt(dt)
+        rate = np.asarray(tuning, np.float64)[np.asarray(latent_l)] * dt
+        return _rng(key).normal(size=rate.shape) * s + rate
 
 
 class PoissonGPLVM1D(PoissonGPLVMJump1D):

@@ -1,0 +1,225 @@
+// Gaussian observation model (GaussianGPLVMJump1D, reference core.py:852-917):
+//   tuning   = basis @ W                         fit_tuning_helper.get_tuning_linear (:12-17)
+//   emission = sum_n m[t,n] norm.logpdf(y, tuning*dt, noise_std)
+//                                                decoder.get_loglikelihood_ma_gaussian (:50-57)
+//   M-step   = (B^T diag(t_w) B / s^2 + I / p^2) W = B^T y_w / s^2
+//                                                fit_tuning_helper.gaussian_m_step_analytic (:44-61)
+// The fwd-bwd scan and the sufficient statistics are the Poisson path's kernels: the
+// emission writes the same (delta, rblk) split, so the scans do not know the model.
+#include <math.h>
+
+#include "pmg_common.h"
+
+namespace pmg {
+
+// tuning[l,n] = sum_b basis[l,b] W[b,n] (f64); one thread per (l, n), W row reads coalesced in n.
+__global__ void __launch_bounds__(256) k_tuning_linear(const float* __restrict__ basis,
+                                                       const double* __restrict__ W, int L, int NB, int N,
+                                                       double* __restrict__ t64, float* __restrict__ t32) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  const int l = blockIdx.y;
+  if (n >= N) return;
+  const float* b = basis + (size_t)l * NB;
+  double a = 0.0;
+  for (int k = 0; k < NB; ++k) a = fma((double)b[k], W[(size_t)k * N + n], a);
+  if (t64) t64[(size_t)l * N + n] = a;
+  if (t32) t32[(size_t)l * N + n] = (float)a;
+}
+
+// ll[t,l] = sum_n m[t,n] (c0 - 0.5 ((y - mu dt) / s)^2),  c0 = -log(s) - 0.5 log(2 pi)
+// (jax.scipy.stats.norm.logpdf), -1e20 where ma_latent == 0.  Tiling as k_emission_dt:
+// 256 threads = 16 time bins x 64 latents, y / mask / tuning tiles staged in LDS.
+__global__ void __launch_bounds__(256) k_emission_gaussian(
+    const float* __restrict__ y, const float* __restrict__ ma, int ma_2d, const double* __restrict__ tuning,
+    const uint8_t* __restrict__ ma_latent, double inv_s, double c0, double dt, int64_t T, int L, int N, int Lp,
+    float* __restrict__ delta, double* __restrict__ rblk) {
+  __shared__ double sY[16][33];
+  __shared__ double sM[16][33];
+  __shared__ double sTu[32][65];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t t0 = (int64_t)blockIdx.x * 16;
+  const int l0 = blockIdx.y * 64;
+  double a[4] = {0, 0, 0, 0};
+  for (int n0 = 0; n0 < N; n0 += 32) {
+    for (int e = threadIdx.x; e < 16 * 32; e += 256) {
+      const int tt = e / 32, nn = e % 32;
+      const int64_t t = t0 + tt;
+      const int n = n0 + nn;
+      double yv = 0.0, mv = 0.0;
+      if (t < T && n < N) {
+        yv = y[t * N + n];
+        mv = ma ? (ma_2d ? ma[t * N + n] : ma[n]) : 1.0;
+      }
+      sY[tt][nn] = yv;
+      sM[tt][nn] = mv;
+    }
+    for (int e = threadIdx.x; e < 32 * 64; e += 256) {
+      const int nn = e / 64, ll = e % 64;
+      const int n = n0 + nn, l = l0 + ll;
+      sTu[nn][ll] = (n < N && l < L) ? tuning[(size_t)l * N + n] * dt : 0.0;
+    }
+    __syncthreads();
+    for (int nn = 0; nn < 32 && n0 + nn < N; ++nn) {
+      const double mu = sTu[nn][tx];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const double z = (sY[ty * 4 + j][nn] - mu) * inv_s;
+        a[j] = fma(sM[ty * 4 + j][nn], fma(-0.5 * z, z, c0), a[j]);
+      }
+    }
+    __syncthreads();
+  }
+  const int l = l0 + tx;
+  const int nblk = Lp >> 5;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t t = t0 + ty * 4 + j;
+    double v = -INFINITY;
+    if (l < L && t < T) {
+      v = a[j];
+      if (ma_latent && ma_latent[l] == 0) v = -1e20;
+    }
+    double mx = v;
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+    if (t < T) {
+      if ((tx & 31) == 0 && l < Lp) rblk[t * nblk + (l >> 5)] = mx;
+      if (l < L) delta[t * (int64_t)L + l] = (float)(v - mx);
+    }
+  }
+}
+
+// Normal equations.  Column c < N:  R[d,c] = sum_l B[l,d] yw[l,c] / s^2   (the right-hand side)
+//                    column N + b:  H[d,b] = sum_l B[l,d] tw[l] B[l,b] / s^2 + (d==b) / p^2
+// One thread per output, written to ws as [NB][N + NB] (f64).
+__global__ void __launch_bounds__(256) k_gauss_normal_eq(const float* __restrict__ basis,
+                                                         const double* __restrict__ yw,
+                                                         const double* __restrict__ tw, int L, int NB, int N,
+                                                         double inv_s2, double inv_p2, double* __restrict__ ws) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int d = blockIdx.y;
+  const int C = N + NB;
+  if (c >= C) return;
+  double a = 0.0;
+  if (c < N) {
+    for (int l = 0; l < L; ++l) a = fma((double)basis[(size_t)l * NB + d], yw[(size_t)l * N + c], a);
+    a *= inv_s2;
+  } else {
+    const int b = c - N;
+    for (int l = 0; l < L; ++l)
+      a = fma((double)basis[(size_t)l * NB + d] * tw[l], (double)basis[(size_t)l * NB + b], a);
+    a = a * inv_s2 + (d == b ? inv_p2 : 0.0);
+  }
+  ws[(size_t)d * C + c] = a;
+}
+
+__device__ __forceinline__ int tri(int i, int j) { return i * (i + 1) / 2 + j; }   // j <= i
+
+// Cholesky of H (packed lower triangle in LDS, f64) then W[:, n] = H^{-1} R[:, n] by
+// forward / backward substitution, one column per thread.  Every workgroup factors H
+// itself (NB^3/6 flops, cheap) and solves its own 256 columns, so there is no
+// inter-workgroup dependency.  Non-positive pivots flag the status word.
+__global__ void __launch_bounds__(256) k_gauss_chol_solve(const double* __restrict__ ws, int NB, int N,
+                                                          double* __restrict__ W, int* __restrict__ status) {
+  extern __shared__ double sA[];
+  const int C = N + NB;
+  const int tid = threadIdx.x;
+  const int ntri = NB * (NB + 1) / 2;
+  for (int e = tid; e < NB * NB; e += 256) {
+    const int i = e / NB, j = e % NB;
+    if (j <= i) sA[tri(i, j)] = ws[(size_t)i * C + N + j];
+  }
+  __syncthreads();
+  for (int k = 0; k < NB; ++k) {
+    const double piv = sA[tri(k, k)];
+    __syncthreads();
+    if (!(piv > 0.0)) {
+      if (tid == 0 && blockIdx.x == 0) status[0] = 1;
+      return;   // uniform across the workgroup: every thread read the same pivot
+    }
+    const double r = sqrt(piv);
+    for (int i = k + 1 + tid; i < NB; i += 256) sA[tri(i, k)] /= r;
+    if (tid == 0) sA[tri(k, k)] = r;
+    __syncthreads();
+    const int m = NB - k - 1;
+    for (int e = tid; e < m * m; e += 256) {
+      const int i = k + 1 + e / m, j = k + 1 + e % m;
+      if (j <= i) sA[tri(i, j)] -= sA[tri(i, k)] * sA[tri(j, k)];
+    }
+    __syncthreads();
+  }
+  (void)ntri;
+  const int n = blockIdx.x * 256 + tid;
+  if (n >= N) return;
+  // L z = R[:, n]
+  for (int i = 0; i < NB; ++i) {
+    double s = ws[(size_t)i * C + n];
+    for (int j = 0; j < i; ++j) s -= sA[tri(i, j)] * W[(size_t)j * N + n];
+    W[(size_t)i * N + n] = s / sA[tri(i, i)];
+  }
+  // L^T w = z
+  for (int i = NB - 1; i >= 0; --i) {
+    double s = W[(size_t)i * N + n];
+    for (int j = i + 1; j < NB; ++j) s -= sA[tri(j, i)] * W[(size_t)j * N + n];
+    W[(size_t)i * N + n] = s / sA[tri(i, i)];
+  }
+}
+
+}  // namespace pmg
+
+using namespace pmg;
+
+extern "C" {
+
+int pmg_tuning_linear(const float* basis, const double* W, int32_t L, int32_t NB, int32_t N, double* tuning64,
+                      float* tuning32, void* stream) {
+  PMG_REQUIRE(basis && W && L > 0 && NB > 0 && N > 0 && (tuning64 || tuning32), "pmg_tuning_linear: bad args");
+  hipLaunchKernelGGL(k_tuning_linear, dim3((unsigned)((N + 255) / 256), (unsigned)L), dim3(256), 0,
+                     as_stream(stream), basis, W, L, NB, N, tuning64, tuning32);
+  PMG_LAUNCH_CHECK();
+  return PMG_OK;
+}
+
+int pmg_emission_gaussian(const float* y, const double* tuning64, const float* ma_neuron, int32_t ma_is_2d,
+                          const uint8_t* ma_latent, double noise_std, double dt, int64_t T, int32_t L, int32_t N,
+                          float* delta, double* rblk, void* stream) {
+  PMG_REQUIRE(T > 0 && L > 0 && N > 0 && y && tuning64 && delta && rblk, "pmg_emission_gaussian: bad args");
+  PMG_REQUIRE(noise_std > 0.0, "pmg_emission_gaussian: noise_std must be > 0");
+  const int Lp = (int)round_up(L, 32);
+  const double c0 = -log(noise_std) - 0.5 * log(2.0 * M_PI);
+  dim3 grid((unsigned)((T + 15) / 16), (unsigned)((L + 63) / 64));
+  hipLaunchKernelGGL(k_emission_gaussian, grid, dim3(256), 0, as_stream(stream), y, ma_neuron, ma_is_2d, tuning64,
+                     ma_latent, 1.0 / noise_std, c0, dt, T, L, N, Lp, delta, rblk);
+  PMG_LAUNCH_CHECK();
+  return PMG_OK;
+}
+
+size_t pmg_gaussian_mstep_workspace_size(int32_t NB, int32_t N) {
+  return (size_t)NB * (size_t)(N + NB) * sizeof(double) + 256;
+}
+
+int pmg_gaussian_mstep(const float* basis, const double* yw, const double* tw, int32_t L, int32_t NB, int32_t N,
+                       double noise_std, double prior_std, double* W, int32_t* status, void* workspace,
+                       size_t workspace_bytes, void* stream) {
+  PMG_REQUIRE(basis && yw && tw && W && status && workspace && L > 0 && NB > 0 && N > 0,
+              "pmg_gaussian_mstep: bad args");
+  PMG_REQUIRE(noise_std > 0.0 && prior_std > 0.0, "pmg_gaussian_mstep: noise_std and prior_std must be > 0");
+  const size_t lds = (size_t)NB * (NB + 1) / 2 * sizeof(double);
+  PMG_REQUIRE(lds <= 160 * 1024, "pmg_gaussian_mstep: NB=%d too large (packed factor must fit 160 KiB LDS)", NB);
+  PMG_REQUIRE(workspace_bytes >= pmg_gaussian_mstep_workspace_size(NB, N), "pmg_gaussian_mstep: workspace too small");
+  hipStream_t st = as_stream(stream);
+  double* ws = reinterpret_cast<double*>(workspace);
+  PMG_HIP(hipMemsetAsync(status, 0, sizeof(int32_t), st));
+  hipLaunchKernelGGL(k_gauss_normal_eq, dim3((unsigned)((N + NB + 255) / 256), (unsigned)NB), dim3(256), 0, st,
+                     basis, yw, tw, L, NB, N, 1.0 / (noise_std * noise_std), 1.0 / (prior_std * prior_std), ws);
+  PMG_LAUNCH_CHECK();
+  if (lds > 64 * 1024)
+    PMG_HIP(hipFuncSetAttribute((const void*)k_gauss_chol_solve, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
+  hipLaunchKernelGGL(k_gauss_chol_solve, dim3((unsigned)((N + 255) / 256)), dim3(256), lds, st, ws, NB, N, W,
+                     status);
+  PMG_LAUNCH_CHECK();
+  return PMG_OK;
+}
+
+}  // extern "C"

@@ -226,6 +226,12 @@ class DeviceEM:
         self._tr_c = None
         self._invz = None
         self.ma_latent = None
+        # Gaussian observation model (GaussianGPLVMJump1D): when noise_std is set, the
+        # emission, tuning and M-step dispatch to gaussian.hip; the scans are shared.
+        self.noise_std = None
+        self.gauss_prior_std = 1.0
+        self._gstatus = None
+        self._ws_gm = None
 
     def _t(self, name):
         return self.timer(name) if self.timer is not None else _NO_TIMER
@@ -279,7 +285,30 @@ class DeviceEM:
             nat.check(self.lib.pmg_suffstats(nat.ptr(self.P), nat.ptr(self.sp.yext), self.T, self.L, self.N,
                                              self.sp.Np, nat.ptr(self.yw), nat.ptr(self.tw),
                                              nat.ptr(self.ws_ss), self.ws_ss.numel(), sh), "pmg_suffstats")
+        if self.noise_std is not None:
+            self.gaussian_m_step(W)
+            return
         self.adam(W, mu, nu, count, cfg, stats_out, lh_out, eh_out)
+
+    def gaussian_m_step(self, W):
+        """Analytic M-step of the Gaussian model (fit_tuning_helper.py:44-61) from the
+        current y_w, t_w; W (NB, N) f64 overwritten.  A non-SPD system sets the status
+        word, checked by gaussian_status() (no host sync here)."""
+        need = int(self.lib.pmg_gaussian_mstep_workspace_size(self.NB, self.N))
+        if self._ws_gm is None or self._ws_gm.numel() < need:
+            self._ws_gm = torch.empty(need, dtype=torch.uint8, device=self.dev)
+        if self._gstatus is None:
+            self._gstatus = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        with self._t('mstep_gaussian'):
+          nat.check(self.lib.pmg_gaussian_mstep(nat.ptr(self.basis), nat.ptr(self.yw), nat.ptr(self.tw), self.L,
+                                                self.NB, self.N, float(self.noise_std), float(self.gauss_prior_std),
+                                                nat.ptr(W), nat.ptr(self._gstatus), nat.ptr(self._ws_gm),
+                                                self._ws_gm.numel(), nat.stream_handle()), "pmg_gaussian_mstep")
+
+    def gaussian_status(self):
+        """Raise if the last Gaussian M-step met a non-positive pivot (device read: syncs)."""
+        if self._gstatus is not None and int(self._gstatus.item()) != 0:
+            raise nat.NativeError("pmg_gaussian_mstep: normal-equation matrix is not positive definite")
 
     # shapes the persistent one-launch Adam kernel holds (a latent row per thread, the
     # basis row in registers + LDS); larger ones use the tiled per-body kernels
@@ -305,6 +334,12 @@ class DeviceEM:
                     "pmg_mstep_adam_tiled" if tiled else "pmg_mstep_adam")
 
     def compute_tuning(self, W):
+        if self.noise_std is not None:
+            with self._t('tuning_linear'):
+              nat.check(self.lib.pmg_tuning_linear(nat.ptr(self.basis), nat.ptr(W), self.L, self.NB, self.N,
+                                                   nat.ptr(self.tuning64), nat.ptr(self.tuning32),
+                                                   nat.stream_handle()), "pmg_tuning_linear")
+            return
         with self._t('tuning_softplus'):
           nat.check(self.lib.pmg_tuning_softplus(nat.ptr(self.basis), nat.ptr(W), self.L, self.NB, self.N,
                                                nat.ptr(self.tuning64), nat.ptr(self.tuning32),
@@ -327,7 +362,12 @@ class DeviceEM:
                                                  nat.ptr(self.phi), nat.ptr(self.mref), sh), "pmg_emission_rowref")
 
     def _emission_call(self, sp, sh, dt):
-        if sp.int_path:
+        if self.noise_std is not None:
+            nat.check(self.lib.pmg_emission_gaussian(nat.ptr(sp.y), nat.ptr(self.tuning64), nat.ptr(sp.ma),
+                                                     int(sp.ma_2d), nat.ptr(self.ma_latent), float(self.noise_std),
+                                                     float(dt), self.T, self.L, self.N, nat.ptr(self.delta),
+                                                     nat.ptr(self.rblk), sh), "pmg_emission_gaussian")
+        elif sp.int_path:
             ma1 = sp.ma if (sp.ma is not None and not sp.ma_2d) else None
             nat.check(self.lib.pmg_emission_poisson(nat.ptr(sp.yq), nat.ptr(sp.gconst), nat.ptr(self.tuning64),
                                                     nat.ptr(ma1), nat.ptr(self.ma_latent), float(dt), self.T,

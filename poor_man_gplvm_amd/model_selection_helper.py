@@ -20,9 +20,10 @@ import itertools
 
 import numpy as np
 
-from .core import PoissonGPLVM1D, PoissonGPLVMJump1D
+from .core import GaussianGPLVMJump1D, PoissonGPLVM1D, PoissonGPLVMJump1D
 
-model_class_dict = {'poisson': PoissonGPLVMJump1D, 'poisson_latentonly': PoissonGPLVM1D}
+model_class_dict = {'poisson': PoissonGPLVMJump1D, 'gaussian': GaussianGPLVMJump1D,
+                    'poisson_latentonly': PoissonGPLVM1D}
 
 default_fit_kwargs = {'n_iter': 20, 'log_posterior_init': None, 'n_time_per_chunk': 10000, 'dt': 1.,
                       'likelihood_scale': 1., 'save_every': None,
