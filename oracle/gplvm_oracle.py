@@ -542,13 +542,16 @@ def create_transition_prob_latent_1d(n_latent, movement_variance=1.0):
     return K[0], logK[0]
 
 
-def smooth_latent_only(y, tuning, logK, ma_neuron=None, ma_latent=None, likelihood_scale=1.0):
+def smooth_latent_only(y, tuning, logK, ma_neuron=None, ma_latent=None, likelihood_scale=1.0, noise_std=None):
     """decoder_latentonly.py:34-226 in one chunk (the chunk carries are exact, so the
     result does not depend on n_time_per_chunk): filter from log(1/L)
     (:58-80), RTS smoother seeded with the last filter posterior and a -1e40 joint
     (:126-154).  Returns (acausal (T,L), logZ, causal (T,L), log c_t (T), joint (L,L),
     ll (T,L))."""
-    ll = loglikelihood_poisson_all(y, tuning, ma_neuron, ma_latent)
+    if noise_std is None:
+        ll = loglikelihood_poisson_all(y, tuning, ma_neuron, ma_latent)
+    else:                                                   # observation_model='gaussian'
+        ll = loglikelihood_gaussian_all(y, tuning, noise_std, ma_neuron, ma_latent)
     T, L = ll.shape
     post = np.log(np.ones(L, _F) / L)
     logz = 0.0

@@ -6,7 +6,7 @@ in include/pmg.h); PyTorch provides device memory, streams and torch.distributed
 """
 __version__ = "0.1.0"
 
-from .core import (GaussianGPLVMJump1D, PoissonGPLVM1D, PoissonGPLVMJump1D,  # noqa: F401
+from .core import (GaussianGPLVM1D, GaussianGPLVMJump1D, PoissonGPLVM1D, PoissonGPLVMJump1D,  # noqa: F401
                    compute_transition_posterior_prob,
                    compute_transition_posterior_prob_latent, run_em)
 from .engine import AdamConfig, ScanConfig  # noqa: F401

@@ -280,10 +280,13 @@ class PoissonGPLVMJump1D:
         ma = None if ma_neuron is None else np.asarray(ma_neuron, np.float32)
         sp = SpikeData(y, ma)
         eng = DeviceEM(sp, self.n_latent_bin, scan=self.scan_config)
+        self._observation(eng, hyperparam)
         eng.set_ma_latent(ma_latent)
         eng.set_tuning(np.asarray(tuning))
         dev, L = eng.dev, self.n_latent_bin
         lib, sh = eng.lib, nat.stream_handle()
+        if eng.noise_std is not None and not np.all(dt == dt[0]):
+            raise NotImplementedError("Gaussian naive-Bayes decoding with a per-time-bin dt_l is not implemented")
         if np.all(dt == dt[0]):
             eng._emission_call(sp, sh, float(dt[0]))
         else:
@@ -662,8 +665,12 @@ class GaussianGPLVMJump1D(PoissonGPLVMJump1D):
         hp['noise_std'] = hp.get('noise_std', self.noise_std)
         return super().decode_latent(y, tuning=tuning, hyperparam=hp, **kwargs)
 
-    def decode_latent_naive_bayes(self, *args, **kwargs):
-        raise NotImplementedError("GaussianGPLVMJump1D.decode_latent_naive_bayes is not implemented on the device")
+    def decode_latent_naive_bayes(self, y, tuning=None, hyperparam={}, **kwargs):
+        """core.py:884-887: the naive-Bayes decoder with the Gaussian emission
+        (constant dt; pmg_emission_gaussian + pmg_naive_bayes_normalize)."""
+        hp = dict(hyperparam)
+        hp['noise_std'] = hp.get('noise_std', self.noise_std)
+        return super().decode_latent_naive_bayes(y, tuning=tuning, hyperparam=hp, **kwargs)
 
     def sample_y(self, latent_l, hyperparam={}, tuning=None, dt=1., key=10):
         """core.py:889-896: N(tuning[latent] * dt, noise_std * sqrt(dt))."""
@@ -814,6 +821,16 @@ class PoissonGPLVM1D(PoissonGPLVMJump1D):
         mv = hyperparam.get('movement_variance', self.movement_variance)
         latent_l = self.sample_latent(T, k1, mv, init_latent)
         return latent_l, self.sample_y(latent_l, hyperparam, tuning, dt, k2)
+
+
+class GaussianGPLVM1D(GaussianGPLVMJump1D, PoissonGPLVM1D):
+    """Gaussian GPLVM with a latent-only chain (core.py:1022-1090): the Gaussian
+    observation model (emission, linear tuning, analytic M-step) of
+    GaussianGPLVMJump1D on PoissonGPLVM1D's pinned-dynamics engine (latent-only
+    outputs, uniform 1/L start, band-limited continuous kernel)."""
+
+    def __init__(self, n_neuron, noise_std=0.5, **kwargs):
+        super().__init__(n_neuron, noise_std=noise_std, **kwargs)
 
 
 def compute_transition_posterior_prob_latent(log_accumulated_joint_total):

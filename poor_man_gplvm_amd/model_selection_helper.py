@@ -20,10 +20,10 @@ import itertools
 
 import numpy as np
 
-from .core import GaussianGPLVMJump1D, PoissonGPLVM1D, PoissonGPLVMJump1D
+from .core import GaussianGPLVM1D, GaussianGPLVMJump1D, PoissonGPLVM1D, PoissonGPLVMJump1D
 
 model_class_dict = {'poisson': PoissonGPLVMJump1D, 'gaussian': GaussianGPLVMJump1D,
-                    'poisson_latentonly': PoissonGPLVM1D}
+                    'poisson_latentonly': PoissonGPLVM1D, 'gaussian_latentonly': GaussianGPLVM1D}
 
 default_fit_kwargs = {'n_iter': 20, 'log_posterior_init': None, 'n_time_per_chunk': 10000, 'dt': 1.,
                       'likelihood_scale': 1., 'save_every': None,
@@ -60,7 +60,7 @@ def fit_model_one_config(config, y_train, key=0, fit_kwargs=default_fit_kwargs, 
     """model_selection_helper.py:35-60.  `fit_fn(model, y, key, fit_kwargs) -> em_res`
     replaces model.fit_em (used by the CPU gloo tests to exercise the sharding)."""
     if model_class_str not in model_class_dict:
-        raise ValueError(f"Invalid model class: {model_class_str} (only 'poisson' is implemented)")
+        raise ValueError(f"Invalid model class: {model_class_str}")
     model_class = model_class_dict[model_class_str]
     key_l = list(key) if isinstance(key, list) else split_keys(key, n_repeat)
     dist = _dist()

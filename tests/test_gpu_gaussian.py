@@ -101,3 +101,41 @@ def test_gaussian_fit_em_vs_oracle():
         assert err <= 3 * floor + 1e-7, f"{k}: max err {err:.3e} vs fp32-stats floor {floor:.3e}"
     np.testing.assert_allclose(res['log_marginal_l'], ref['log_marginal_l'], rtol=1e-6)
     np.testing.assert_allclose(m.tuning, res['tuning'])
+
+
+def test_gaussian_latent_only_decode_vs_oracle():
+    """GaussianGPLVM1D.decode_latent (core.py:1049-1055, decoder_latentonly.py) on jump-free
+    data (the latent-only band limit)."""
+    import poor_man_gplvm_amd as P
+    N, L, T = 30, 100, 1200
+    d = _data(N, L, T)
+    lat = O.sample_latent(T, L, np.random.default_rng(1), 1.0, 0.0, 1.0)
+    y = (d['tuning'][lat[:, 1]] + SIG * np.random.default_rng(2).normal(size=(T, N))).astype(np.float32)
+    m = P.GaussianGPLVM1D(N, n_latent_bin=L, tuning_lengthscale=10., noise_std=SIG)
+    r = m.decode_latent(y, tuning=d['tuning'])
+    assert 'posterior_dynamics_marg' not in r
+    _, logK = O.create_transition_prob_latent_1d(L, 1.0)
+    lpa, lz, *_ = O.smooth_latent_only(y, d['tuning'], logK, noise_std=SIG)
+    close_prob(r['posterior_all'], np.exp(lpa))
+    np.testing.assert_allclose(r['log_marginal_final'], lz, rtol=1e-7)
+    res = m.fit_em(y, n_iter=2, log_posterior_init=d['lp0'])
+    assert res['posterior'].shape == (T, L) and np.isfinite(res['log_marginal_l']).all()
+
+
+@pytest.mark.parametrize("masked", [False, True])
+def test_gaussian_naive_bayes_vs_oracle(masked):
+    """decode_latent_naive_bayes with the Gaussian emission (core.py:884-887,
+    decoder.py:106-149): per-bin log posterior = ll - logsumexp_l ll."""
+    import poor_man_gplvm_amd as P
+    from scipy.special import logsumexp
+    N, L, T = 30, 100, 800
+    d = _data(N, L, T)
+    ml = (np.random.default_rng(4).random(L) > 0.3).astype(np.float32) if masked else None
+    m = P.GaussianGPLVMJump1D(N, n_latent_bin=L, tuning_lengthscale=10., noise_std=SIG)
+    r = m.decode_latent_naive_bayes(d['y'], tuning=d['tuning'], ma_latent=ml, dt_l=1.0)
+    ll = O.loglikelihood_gaussian_all(d['y'], d['tuning'], SIG, None, ml)
+    lml = logsumexp(ll, axis=1)
+    np.testing.assert_allclose(r['log_marginal_l'], lml, rtol=1e-6)
+    close_prob(r['posterior_latent'], np.exp(ll - lml[:, None]), rtol=1e-4, atol=1e-9)
+    with pytest.raises(NotImplementedError):
+        m.decode_latent_naive_bayes(d['y'], tuning=d['tuning'], dt_l=np.linspace(0.5, 1.5, T))

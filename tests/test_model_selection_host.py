@@ -91,3 +91,11 @@ def test_evaluate_model_one_config_with_oracle_models():
         np.testing.assert_equal(v['best_value'], np.max(v['value_per_fit']))
     # the one-step predictive marginals sum to logZ (decoder.py:174-187)
     np.testing.assert_allclose(ev['log_one_step_predictive_marginal_test']['value_per_fit'], lz, rtol=1e-9)
+
+
+def test_model_class_dict_matches_reference_names():
+    """model_selection_helper.py:14: the four model_class_str values."""
+    assert set(MS.model_class_dict) == {'poisson', 'gaussian', 'poisson_latentonly', 'gaussian_latentonly'}
+    import poor_man_gplvm_amd as P
+    assert MS.model_class_dict['gaussian_latentonly'] is P.GaussianGPLVM1D
+    assert issubclass(P.GaussianGPLVM1D, P.PoissonGPLVM1D)      # latent-only engine
