@@ -125,9 +125,8 @@ def get_jump_consensus(jump_p, jump_p_all_chain, window_size=5, jump_p_thresh=0.
     return frac, is_jump_filtered, ok
 
 
-def _jump_consensus_values(decoding_res_l, jump_dynamics_index, window_size, p_thresh, c_thresh):
-    chains = np.array([np.asarray(d['posterior_dynamics_marg'])[:, jump_dynamics_index]
-                       for d in decoding_res_l]).T  # (T, n_chain)
+def _jump_consensus_values(jump_p_l, window_size, p_thresh, c_thresh):
+    chains = np.array(jump_p_l).T  # (T, n_chain)
     return np.array([get_jump_consensus(jp, chains, window_size=window_size, jump_p_thresh=p_thresh,
                                         consensus_thresh=c_thresh)[0] for jp in chains.T])
 
@@ -141,31 +140,54 @@ def evaluate_model_one_config(model_fit_l, y_test, key=1, n_time_per_chunk=10000
     """model_selection_helper.py:62-147: per-fit metrics on the test data, each a dict
     {'value_per_fit', 'best_value', 'best_index'}; 'metric_overall' is the mean of
     the downsampled LMLs over latent_downsample_frac (so 'downsampled_lml' must be
-    requested, as in the reference)."""
+    requested, as in the reference).
+
+    Under torch.distributed the fits are sharded like the restarts: rank r decodes and
+    scores fits k with k % world_size == r (one decode + the downsampled-LML masks per
+    fit, all independent), then one all_gather_object of the per-fit scalars and jump
+    probabilities; every rank assembles the same result."""
+    want_ds = 'downsampled_lml' in metric_type_l
+    want_jump = 'jump_consensus' in metric_type_l
+    dist = _dist()
+    rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)
+    mine = {}
+    for k in range(rank, len(model_fit_l), world):
+        m = model_fit_l[k]
+        dec = m.decode_latent(y_test, n_time_per_chunk=n_time_per_chunk)
+        v = {'lml': dec['log_marginal_final'],
+             'os': np.asarray(dec['log_one_step_predictive_marginals_all']).sum()}
+        if want_ds:
+            v['ds'] = [get_downsampled_lml(m, y_test, downsample_frac=f, n_repeat=downsample_n_repeat, key=key)['value']
+                       for f in latent_downsample_frac]
+        if want_jump:
+            v['jp'] = np.asarray(dec['posterior_dynamics_marg'])[:, jump_dynamics_index]
+        mine[k] = v
+    if dist and world > 1:
+        parts = [None] * world
+        dist.all_gather_object(parts, mine)
+        mine = {k: v for part in parts for k, v in part.items()}
+    per = [mine[k] for k in range(len(model_fit_l))]
+
     res = {}
-    decoding_res_l = [m.decode_latent(y_test, n_time_per_chunk=n_time_per_chunk) for m in model_fit_l]
 
     def put(name, vals):
         res[name] = {'value_per_fit': np.array(vals), 'best_value': None, 'best_index': None}
 
     if 'log_marginal_test' in metric_type_l:
-        put('log_marginal_test', [d['log_marginal_final'] for d in decoding_res_l])
+        put('log_marginal_test', [v['lml'] for v in per])
     if 'log_one_step_predictive_marginal_test' in metric_type_l:
-        put('log_one_step_predictive_marginal_test',
-            [np.asarray(d['log_one_step_predictive_marginals_all']).sum() for d in decoding_res_l])
-    if 'downsampled_lml' in metric_type_l:
-        for frac in latent_downsample_frac:
-            put('downsampled_lml_' + str(frac),
-                [get_downsampled_lml(m, y_test, downsample_frac=frac, n_repeat=downsample_n_repeat, key=key)['value']
-                 for m in model_fit_l])
-    if 'jump_consensus' in metric_type_l:
-        args = (jump_dynamics_index,)
+        put('log_one_step_predictive_marginal_test', [v['os'] for v in per])
+    if want_ds:
+        for i, frac in enumerate(latent_downsample_frac):
+            put('downsampled_lml_' + str(frac), [v['ds'][i] for v in per])
+    if want_jump:
+        jp_l = [v['jp'] for v in per]
         thr = (jump_consensus_jump_p_thresh, jump_consensus_consensus_thresh)
         if isinstance(jump_consensus_window_size, int):
-            put('jump_consensus', _jump_consensus_values(decoding_res_l, *args, jump_consensus_window_size, *thr))
+            put('jump_consensus', _jump_consensus_values(jp_l, jump_consensus_window_size, *thr))
         elif isinstance(jump_consensus_window_size, list):
             for w in jump_consensus_window_size:
-                put('jump_consensus_' + str(w), _jump_consensus_values(decoding_res_l, *args, w, *thr))
+                put('jump_consensus_' + str(w), _jump_consensus_values(jp_l, w, *thr))
         else:
             print(f"jump_consensus_window_size {jump_consensus_window_size} is not supported")
 

@@ -53,3 +53,30 @@ def test_restart_sharding_world2_matches_single_process():
         assert [k for k, _ in got] == [k for k, _ in ref]
         for (_, a), (_, b) in zip(got, ref):
             np.testing.assert_allclose(a, b, rtol=0, atol=0)
+
+
+def _eval_worker(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from poor_man_gplvm_amd import model_selection_helper as msh
+    from tests.test_model_selection_host import _eval_case
+    out[rank] = _eval_case(msh)
+    dist.destroy_process_group()
+
+
+def test_evaluation_sharding_world2_matches_single_process():
+    """evaluate_model_one_config with fits sharded over 2 gloo ranks equals the
+    single-process result on every rank (stand-in models decode with the oracle)."""
+    from poor_man_gplvm_amd import model_selection_helper as msh
+    from tests.test_model_selection_host import _eval_case
+    ref = _eval_case(msh)
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_eval_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for rank in range(2):
+        got = out[rank]
+        assert list(got) == list(ref)
+        for k in ref:
+            np.testing.assert_array_equal(got[k]['value_per_fit'], ref[k]['value_per_fit'])
+            np.testing.assert_equal(got[k]['best_index'], ref[k]['best_index'])

@@ -68,6 +68,17 @@ class _OracleModel:
         return O.downsampled_lml(y, self.tuning, masks, movement_variance=self.mv)[0]
 
 
+def _eval_case(MS):
+    """3 stand-in fits on a small recording (shared with the gloo sharding test)."""
+    d = make(12, 30, 200)
+    rng = np.random.default_rng(5)
+    models = [_OracleModel(d['tuning'], 1.0),
+              _OracleModel(d['tuning'] * np.exp(0.3 * rng.normal(size=d['tuning'].shape)), 1.0),
+              _OracleModel(d['tuning'], 3.0)]
+    return MS.evaluate_model_one_config(models, d['y'], key=1, latent_downsample_frac=[0.4, 0.8],
+                                        downsample_n_repeat=3, jump_consensus_window_size=[3, 5])
+
+
 def test_evaluate_model_one_config_with_oracle_models():
     d = make(12, 30, 200)
     rng = np.random.default_rng(5)
