@@ -26,20 +26,28 @@ __global__ void __launch_bounds__(256) k_tuning_linear(const float* __restrict__
   if (t32) t32[(size_t)l * N + n] = (float)a;
 }
 
-// ll[t,l] = sum_n m[t,n] (c0 - 0.5 ((y - mu dt) / s)^2),  c0 = -log(s) - 0.5 log(2 pi)
-// (jax.scipy.stats.norm.logpdf), -1e20 where ma_latent == 0.  Tiling as k_emission_dt:
+// ll[t,l] = sum_n m[t,n] (c0 - 0.5 ((y - mu) / s)^2),  mu = tuning dt,  c0 = -log(s) - 0.5 log(2 pi)
+// (jax.scipy.stats.norm.logpdf), -1e20 where ma_latent == 0.  Expanded so the inner loop is
+// two f64 FMAs per (t, l, n):
+//   ll = sum_n m (c0 - y^2 / 2s^2)  +  (1/s^2) sum_n (m y) mu  -  (1/2s^2) sum_n m mu^2
+// (the first term per time bin, summed once per tile).  All sums are f64 (terms O(1e4) at
+// N = 512: rounding ~1e-12, far below the fp32 output).  Tiling as k_emission_dt:
 // 256 threads = 16 time bins x 64 latents, y / mask / tuning tiles staged in LDS.
 __global__ void __launch_bounds__(256) k_emission_gaussian(
     const float* __restrict__ y, const float* __restrict__ ma, int ma_2d, const double* __restrict__ tuning,
     const uint8_t* __restrict__ ma_latent, double inv_s, double c0, double dt, int64_t T, int L, int N, int Lp,
     float* __restrict__ delta, double* __restrict__ rblk) {
-  __shared__ double sY[16][33];
+  __shared__ double sMY[16][33];
   __shared__ double sM[16][33];
+  __shared__ double sQ[16][33];
   __shared__ double sTu[32][65];
+  __shared__ double sTu2[32][65];
+  __shared__ double sQs[16];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int64_t t0 = (int64_t)blockIdx.x * 16;
   const int l0 = blockIdx.y * 64;
-  double a[4] = {0, 0, 0, 0};
+  const double inv_s2 = inv_s * inv_s;
+  double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
   for (int n0 = 0; n0 < N; n0 += 32) {
     for (int e = threadIdx.x; e < 16 * 32; e += 256) {
       const int tt = e / 32, nn = e % 32;
@@ -50,24 +58,35 @@ __global__ void __launch_bounds__(256) k_emission_gaussian(
         yv = y[t * N + n];
         mv = ma ? (ma_2d ? ma[t * N + n] : ma[n]) : 1.0;
       }
-      sY[tt][nn] = yv;
+      sMY[tt][nn] = mv * yv;
       sM[tt][nn] = mv;
+      sQ[tt][nn] = mv * fma(-0.5 * inv_s2 * yv, yv, c0);
     }
     for (int e = threadIdx.x; e < 32 * 64; e += 256) {
       const int nn = e / 64, ll = e % 64;
       const int n = n0 + nn, l = l0 + ll;
-      sTu[nn][ll] = (n < N && l < L) ? tuning[(size_t)l * N + n] * dt : 0.0;
+      const double mu = (n < N && l < L) ? tuning[(size_t)l * N + n] * dt : 0.0;
+      sTu[nn][ll] = mu;
+      sTu2[nn][ll] = mu * mu;
     }
     __syncthreads();
-    for (int nn = 0; nn < 32 && n0 + nn < N; ++nn) {
-      const double mu = sTu[nn][tx];
+    if (threadIdx.x < 16) {
+      double acc = 0.0;
+      for (int nn = 0; nn < 32; ++nn) acc += sQ[threadIdx.x][nn];
+      sQs[threadIdx.x] = acc;
+    }
+    const int nlim = min(32, N - n0);
+    for (int nn = 0; nn < nlim; ++nn) {
+      const double mu = sTu[nn][tx], mu2 = sTu2[nn][tx];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const double z = (sY[ty * 4 + j][nn] - mu) * inv_s;
-        a[j] = fma(sM[ty * 4 + j][nn], fma(-0.5 * z, z, c0), a[j]);
+        a[j] = fma(sMY[ty * 4 + j][nn], mu, a[j]);
+        b[j] = fma(sM[ty * 4 + j][nn], mu2, b[j]);
       }
     }
     __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) q[j] += sQs[ty * 4 + j];
   }
   const int l = l0 + tx;
   const int nblk = Lp >> 5;
@@ -76,7 +95,7 @@ __global__ void __launch_bounds__(256) k_emission_gaussian(
     const int64_t t = t0 + ty * 4 + j;
     double v = -INFINITY;
     if (l < L && t < T) {
-      v = a[j];
+      v = q[j] + inv_s2 * a[j] - 0.5 * inv_s2 * b[j];
       if (ma_latent && ma_latent[l] == 0) v = -1e20;
     }
     double mx = v;
