@@ -27,83 +27,114 @@ __global__ void __launch_bounds__(256) k_tuning_linear(const float* __restrict__
 }
 
 // ll[t,l] = sum_n m[t,n] (c0 - 0.5 ((y - mu) / s)^2),  mu = tuning dt,  c0 = -log(s) - 0.5 log(2 pi)
-// (jax.scipy.stats.norm.logpdf), -1e20 where ma_latent == 0.  Expanded so the inner loop is
-// two f64 FMAs per (t, l, n):
-//   ll = sum_n m (c0 - y^2 / 2s^2)  +  (1/s^2) sum_n (m y) mu  -  (1/2s^2) sum_n m mu^2
-// (the first term per time bin, summed once per tile).  All sums are f64 (terms O(1e4) at
-// N = 512: rounding ~1e-12, far below the fp32 output).  Tiling as k_emission_dt:
-// 256 threads = 16 time bins x 64 latents, y / mask / tuning tiles staged in LDS.
+// (jax.scipy.stats.norm.logpdf), -1e20 where ma_latent == 0.  Expanded into two dense
+// contractions over neurons plus a per-time-bin constant:
+//   ll = q_t + (1/s^2) [(m*y) mu^T]_tl - (1/2s^2) [m (mu^2)^T]_tl,   q_t = sum_n m (c0 - y^2/2s^2)
+// both contractions on the f64 MFMA (v_mfma_f64_16x16x4_f64, full f64: same numbers as an
+// f64 dot product up to summation order).  Block = 4 waves, tile 64 time bins x 64 latents,
+// neurons staged through LDS 32 at a time; wave w owns time rows 16w..16w+15 and all four
+// 16-latent sub-tiles.  Operand maps (cdna_hip_programming.md, f64 16x16x4): A lane l =
+// A[l&15][k=l>>4], B lane l = B[k=l>>4][l&15], D reg r of lane l = D[(l>>4)+4r][l&15].
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
 __global__ void __launch_bounds__(256) k_emission_gaussian(
     const float* __restrict__ y, const float* __restrict__ ma, int ma_2d, const double* __restrict__ tuning,
     const uint8_t* __restrict__ ma_latent, double inv_s, double c0, double dt, int64_t T, int L, int N, int Lp,
     float* __restrict__ delta, double* __restrict__ rblk) {
-  __shared__ double sMY[16][33];
-  __shared__ double sM[16][33];
-  __shared__ double sQ[16][33];
+  __shared__ double sMY[64][33];
+  __shared__ double sM[64][33];
   __shared__ double sTu[32][65];
   __shared__ double sTu2[32][65];
-  __shared__ double sQs[16];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int64_t t0 = (int64_t)blockIdx.x * 16;
+  __shared__ double sQs[64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t t0 = (int64_t)blockIdx.x * 64;
   const int l0 = blockIdx.y * 64;
   const double inv_s2 = inv_s * inv_s;
-  double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
+  f64x4 acc_a[4], acc_b[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    acc_a[s] = (f64x4){0.0, 0.0, 0.0, 0.0};
+    acc_b[s] = (f64x4){0.0, 0.0, 0.0, 0.0};
+  }
+  double q[4] = {0, 0, 0, 0};
+  const int ar = 16 * w + (lane & 15);   // A row (time) this lane feeds
+  const int kq = lane >> 4;               // k index within a 4-step
   for (int n0 = 0; n0 < N; n0 += 32) {
-    for (int e = threadIdx.x; e < 16 * 32; e += 256) {
-      const int tt = e / 32, nn = e % 32;
+    {   // thread -> (time row tt, 8 consecutive neurons); the q_t partial is summed in
+        // registers and over the 4 lanes sharing a row (no LDS array, no division)
+      const int tt = threadIdx.x >> 2, nb = (threadIdx.x & 3) * 8;
       const int64_t t = t0 + tt;
-      const int n = n0 + nn;
-      double yv = 0.0, mv = 0.0;
-      if (t < T && n < N) {
-        yv = y[t * N + n];
-        mv = ma ? (ma_2d ? ma[t * N + n] : ma[n]) : 1.0;
+      double qp = 0.0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int n = n0 + nb + i;
+        double yv = 0.0, mv = 0.0;
+        if (t < T && n < N) {
+          yv = y[t * N + n];
+          mv = ma ? (ma_2d ? ma[t * N + n] : ma[n]) : 1.0;
+        }
+        sMY[tt][nb + i] = mv * yv;
+        sM[tt][nb + i] = mv;
+        qp = fma(mv, fma(-0.5 * inv_s2 * yv, yv, c0), qp);
       }
-      sMY[tt][nn] = mv * yv;
-      sM[tt][nn] = mv;
-      sQ[tt][nn] = mv * fma(-0.5 * inv_s2 * yv, yv, c0);
+      qp += __shfl_xor(qp, 1, 64);
+      qp += __shfl_xor(qp, 2, 64);
+      if ((threadIdx.x & 3) == 0) sQs[tt] = qp;
     }
-    for (int e = threadIdx.x; e < 32 * 64; e += 256) {
-      const int nn = e / 64, ll = e % 64;
+    for (int e = threadIdx.x; e < 32 * 64; e += 256) {   // n fastest: coalesced tuning rows
+      const int nn = e & 31, ll = e >> 5;
       const int n = n0 + nn, l = l0 + ll;
       const double mu = (n < N && l < L) ? tuning[(size_t)l * N + n] * dt : 0.0;
       sTu[nn][ll] = mu;
       sTu2[nn][ll] = mu * mu;
     }
     __syncthreads();
-    if (threadIdx.x < 16) {
-      double acc = 0.0;
-      for (int nn = 0; nn < 32; ++nn) acc += sQ[threadIdx.x][nn];
-      sQs[threadIdx.x] = acc;
-    }
-    const int nlim = min(32, N - n0);
-    for (int nn = 0; nn < nlim; ++nn) {
-      const double mu = sTu[nn][tx], mu2 = sTu2[nn][tx];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        a[j] = fma(sMY[ty * 4 + j][nn], mu, a[j]);
-        b[j] = fma(sM[ty * 4 + j][nn], mu2, b[j]);
+    for (int k0 = 0; k0 < 32; k0 += 4) {
+      const double am = sMY[ar][k0 + kq];
+      const double bm = sM[ar][k0 + kq];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const double mu = sTu[k0 + kq][16 * s + (lane & 15)];
+        const double mu2 = sTu2[k0 + kq][16 * s + (lane & 15)];
+        acc_a[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(am, mu, acc_a[s], 0, 0, 0);
+        acc_b[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(bm, mu2, acc_b[s], 0, 0, 0);
       }
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < 4; ++j) q[j] += sQs[ty * 4 + j];
+    for (int r = 0; r < 4; ++r) q[r] += sQs[16 * w + (lane >> 4) + 4 * r];
   }
-  const int l = l0 + tx;
   const int nblk = Lp >> 5;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int64_t t = t0 + ty * 4 + j;
-    double v = -INFINITY;
-    if (l < L && t < T) {
-      v = q[j] + inv_s2 * a[j] - 0.5 * inv_s2 * b[j];
-      if (ma_latent && ma_latent[l] == 0) v = -1e20;
-    }
-    double mx = v;
+  for (int r = 0; r < 4; ++r) {
+    const int64_t t = t0 + 16 * w + (lane >> 4) + 4 * r;
 #pragma unroll
-    for (int o = 16; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
-    if (t < T) {
-      if ((tx & 31) == 0 && l < Lp) rblk[t * nblk + (l >> 5)] = mx;
-      if (l < L) delta[t * (int64_t)L + l] = (float)(v - mx);
+    for (int h = 0; h < 2; ++h) {          // 32-latent block = sub-tiles 2h, 2h+1
+      double v[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int s = 2 * h + u;
+        const int l = l0 + 16 * s + (lane & 15);
+        double x = -INFINITY;
+        if (l < L && t < T) {
+          x = q[r] + inv_s2 * acc_a[s][r] - 0.5 * inv_s2 * acc_b[s][r];
+          if (ma_latent && ma_latent[l] == 0) x = -1e20;
+        }
+        v[u] = x;
+      }
+      double mx = fmax(v[0], v[1]);
+#pragma unroll
+      for (int o = 8; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+      if (t < T) {
+        const int lb = l0 + 32 * h;
+        if ((lane & 15) == 0 && lb < Lp) rblk[t * nblk + (lb >> 5)] = mx;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int l = lb + 16 * u + (lane & 15);
+          if (l < L) delta[t * (int64_t)L + l] = (float)(v[u] - mx);
+        }
+      }
     }
   }
 }
@@ -206,7 +237,7 @@ int pmg_emission_gaussian(const float* y, const double* tuning64, const float* m
   PMG_REQUIRE(noise_std > 0.0, "pmg_emission_gaussian: noise_std must be > 0");
   const int Lp = (int)round_up(L, 32);
   const double c0 = -log(noise_std) - 0.5 * log(2.0 * M_PI);
-  dim3 grid((unsigned)((T + 15) / 16), (unsigned)((L + 63) / 64));
+  dim3 grid((unsigned)((T + 63) / 64), (unsigned)((L + 63) / 64));
   hipLaunchKernelGGL(k_emission_gaussian, grid, dim3(256), 0, as_stream(stream), y, ma_neuron, ma_is_2d, tuning64,
                      ma_latent, 1.0 / noise_std, c0, dt, T, L, N, Lp, delta, rblk);
   PMG_LAUNCH_CHECK();
