@@ -41,10 +41,9 @@ __global__ void __launch_bounds__(256) k_emission_gaussian(
     const float* __restrict__ y, const float* __restrict__ ma, int ma_2d, const double* __restrict__ tuning,
     const uint8_t* __restrict__ ma_latent, double inv_s, double c0, double dt, int64_t T, int L, int N, int Lp,
     float* __restrict__ delta, double* __restrict__ rblk) {
-  __shared__ double sMY[64][33];
-  __shared__ double sM[64][33];
-  __shared__ double sTu[32][65];
-  __shared__ double sTu2[32][65];
+  __shared__ float sY[64][33];     // y and m stay f32 (their f64 product is exact)
+  __shared__ float sM[64][33];
+  __shared__ double sTu[32][65];   // mu = tuning * dt (f64); mu^2 is formed at use
   __shared__ double sQs[64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t t0 = (int64_t)blockIdx.x * 64;
@@ -73,8 +72,8 @@ __global__ void __launch_bounds__(256) k_emission_gaussian(
           yv = y[t * N + n];
           mv = ma ? (ma_2d ? ma[t * N + n] : ma[n]) : 1.0;
         }
-        sMY[tt][nb + i] = mv * yv;
-        sM[tt][nb + i] = mv;
+        sY[tt][nb + i] = (float)yv;
+        sM[tt][nb + i] = (float)mv;
         qp = fma(mv, fma(-0.5 * inv_s2 * yv, yv, c0), qp);
       }
       qp += __shfl_xor(qp, 1, 64);
@@ -86,19 +85,17 @@ __global__ void __launch_bounds__(256) k_emission_gaussian(
       const int n = n0 + nn, l = l0 + ll;
       const double mu = (n < N && l < L) ? tuning[(size_t)l * N + n] * dt : 0.0;
       sTu[nn][ll] = mu;
-      sTu2[nn][ll] = mu * mu;
     }
     __syncthreads();
 #pragma unroll
     for (int k0 = 0; k0 < 32; k0 += 4) {
-      const double am = sMY[ar][k0 + kq];
-      const double bm = sM[ar][k0 + kq];
+      const double bm = (double)sM[ar][k0 + kq];
+      const double am = bm * (double)sY[ar][k0 + kq];
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const double mu = sTu[k0 + kq][16 * s + (lane & 15)];
-        const double mu2 = sTu2[k0 + kq][16 * s + (lane & 15)];
         acc_a[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(am, mu, acc_a[s], 0, 0, 0);
-        acc_b[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(bm, mu2, acc_b[s], 0, 0, 0);
+        acc_b[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(bm, mu * mu, acc_b[s], 0, 0, 0);
       }
     }
     __syncthreads();
