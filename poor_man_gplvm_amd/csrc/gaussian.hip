@@ -162,16 +162,15 @@ __global__ void __launch_bounds__(256) k_gauss_normal_eq(const float* __restrict
 
 __device__ __forceinline__ int tri(int i, int j) { return i * (i + 1) / 2 + j; }   // j <= i
 
-// Cholesky of H (packed lower triangle in LDS, f64) then W[:, n] = H^{-1} R[:, n] by
-// forward / backward substitution, one column per thread.  Every workgroup factors H
-// itself (NB^3/6 flops, cheap) and solves its own 256 columns, so there is no
-// inter-workgroup dependency.  Non-positive pivots flag the status word.
-__global__ void __launch_bounds__(256) k_gauss_chol_solve(const double* __restrict__ ws, int NB, int N,
-                                                          double* __restrict__ W, int* __restrict__ status) {
+// Cholesky of H (packed lower triangle in LDS, f64), then Linv = L^{-1} (row-major NB x NB,
+// zero above the diagonal) by one column solve per thread.  One workgroup: NB^3/6 flops for
+// the factor and NB^3/6 for the inverse, with no dependency chain longer than NB^2 per
+// thread.  A non-positive pivot sets the status word (the host raises) and skips Linv.
+__global__ void __launch_bounds__(256) k_gauss_chol_inv(const double* __restrict__ ws, int NB, int N,
+                                                        double* __restrict__ Linv, int* __restrict__ status) {
   extern __shared__ double sA[];
   const int C = N + NB;
   const int tid = threadIdx.x;
-  const int ntri = NB * (NB + 1) / 2;
   for (int e = tid; e < NB * NB; e += 256) {
     const int i = e / NB, j = e % NB;
     if (j <= i) sA[tri(i, j)] = ws[(size_t)i * C + N + j];
@@ -181,7 +180,7 @@ __global__ void __launch_bounds__(256) k_gauss_chol_solve(const double* __restri
     const double piv = sA[tri(k, k)];
     __syncthreads();
     if (!(piv > 0.0)) {
-      if (tid == 0 && blockIdx.x == 0) status[0] = 1;
+      if (tid == 0) status[0] = 1;
       return;   // uniform across the workgroup: every thread read the same pivot
     }
     const double r = sqrt(piv);
@@ -195,21 +194,33 @@ __global__ void __launch_bounds__(256) k_gauss_chol_solve(const double* __restri
     }
     __syncthreads();
   }
-  (void)ntri;
-  const int n = blockIdx.x * 256 + tid;
+  for (int j = tid; j < NB; j += 256) {   // column j of L^{-1}: L x = e_j
+    for (int i = 0; i < j; ++i) Linv[(size_t)i * NB + j] = 0.0;
+    for (int i = j; i < NB; ++i) {
+      double v = (i == j) ? 1.0 : 0.0;
+      for (int k = j; k < i; ++k) v -= sA[tri(i, k)] * Linv[(size_t)k * NB + j];
+      Linv[(size_t)i * NB + j] = v / sA[tri(i, i)];
+    }
+  }
+}
+
+// Triangular products of the solve W = L^{-T} (L^{-1} R), one thread per output (d, n):
+//   trans = 0:  out[d,n] = sum_{k<=d} Linv[d,k] X[k,n]
+//   trans = 1:  out[d,n] = sum_{k>=d} Linv[k,d] X[k,n]
+// X rows have stride ldx; Linv reads are uniform across the workgroup (same d).
+__global__ void __launch_bounds__(256) k_gauss_tri_mm(const double* __restrict__ Linv,
+                                                      const double* __restrict__ X, int64_t ldx, int NB, int N,
+                                                      int trans, double* __restrict__ out) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  const int d = blockIdx.y;
   if (n >= N) return;
-  // L z = R[:, n]
-  for (int i = 0; i < NB; ++i) {
-    double s = ws[(size_t)i * C + n];
-    for (int j = 0; j < i; ++j) s -= sA[tri(i, j)] * W[(size_t)j * N + n];
-    W[(size_t)i * N + n] = s / sA[tri(i, i)];
+  double a = 0.0;
+  if (!trans) {
+    for (int k = 0; k <= d; ++k) a = fma(Linv[(size_t)d * NB + k], X[(size_t)k * ldx + n], a);
+  } else {
+    for (int k = d; k < NB; ++k) a = fma(Linv[(size_t)k * NB + d], X[(size_t)k * ldx + n], a);
   }
-  // L^T w = z
-  for (int i = NB - 1; i >= 0; --i) {
-    double s = W[(size_t)i * N + n];
-    for (int j = i + 1; j < NB; ++j) s -= sA[tri(j, i)] * W[(size_t)j * N + n];
-    W[(size_t)i * N + n] = s / sA[tri(i, i)];
-  }
+  out[(size_t)d * N + n] = a;
 }
 
 }  // namespace pmg
@@ -242,7 +253,8 @@ int pmg_emission_gaussian(const float* y, const double* tuning64, const float* m
 }
 
 size_t pmg_gaussian_mstep_workspace_size(int32_t NB, int32_t N) {
-  return (size_t)NB * (size_t)(N + NB) * sizeof(double) + 256;
+  // [R | H] (NB x (N+NB)), Linv (NB x NB), Z = Linv R (NB x N)
+  return ((size_t)NB * (size_t)(N + NB) + (size_t)NB * NB + (size_t)NB * N) * sizeof(double) + 256;
 }
 
 int pmg_gaussian_mstep(const float* basis, const double* yw, const double* tw, int32_t L, int32_t NB, int32_t N,
@@ -260,11 +272,17 @@ int pmg_gaussian_mstep(const float* basis, const double* yw, const double* tw, i
   hipLaunchKernelGGL(k_gauss_normal_eq, dim3((unsigned)((N + NB + 255) / 256), (unsigned)NB), dim3(256), 0, st,
                      basis, yw, tw, L, NB, N, 1.0 / (noise_std * noise_std), 1.0 / (prior_std * prior_std), ws);
   PMG_LAUNCH_CHECK();
+  double* Linv = ws + (size_t)NB * (N + NB);
+  double* Z = Linv + (size_t)NB * NB;
   if (lds > 64 * 1024)
-    PMG_HIP(hipFuncSetAttribute((const void*)k_gauss_chol_solve, hipFuncAttributeMaxDynamicSharedMemorySize,
+    PMG_HIP(hipFuncSetAttribute((const void*)k_gauss_chol_inv, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds));
-  hipLaunchKernelGGL(k_gauss_chol_solve, dim3((unsigned)((N + 255) / 256)), dim3(256), lds, st, ws, NB, N, W,
-                     status);
+  hipLaunchKernelGGL(k_gauss_chol_inv, dim3(1), dim3(256), lds, st, ws, NB, N, Linv, status);
+  PMG_LAUNCH_CHECK();
+  const dim3 g((unsigned)((N + 255) / 256), (unsigned)NB);
+  hipLaunchKernelGGL(k_gauss_tri_mm, g, dim3(256), 0, st, Linv, ws, (int64_t)(N + NB), NB, N, 0, Z);
+  PMG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_gauss_tri_mm, g, dim3(256), 0, st, Linv, Z, (int64_t)N, NB, N, 1, W);
   PMG_LAUNCH_CHECK();
   return PMG_OK;
 }
