@@ -167,7 +167,8 @@ __device__ __forceinline__ int tri(int i, int j) { return i * (i + 1) / 2 + j; }
 // the factor and NB^3/6 for the inverse, with no dependency chain longer than NB^2 per
 // thread.  A non-positive pivot sets the status word (the host raises) and skips Linv.
 __global__ void __launch_bounds__(256) k_gauss_chol_inv(const double* __restrict__ ws, int NB, int N,
-                                                        double* __restrict__ Linv, int* __restrict__ status) {
+                                                        double* __restrict__ Linv, int* __restrict__ status,
+                                                        int x_in_lds) {
   extern __shared__ double sA[];
   const int C = N + NB;
   const int tid = threadIdx.x;
@@ -194,13 +195,20 @@ __global__ void __launch_bounds__(256) k_gauss_chol_inv(const double* __restrict
     }
     __syncthreads();
   }
+  // the inverse is built in LDS when it fits next to the factor (NB <= 118), else in place
+  // in global memory; a column's values are re-read by the thread that wrote them
+  double* X = x_in_lds ? sA + NB * (NB + 1) / 2 : Linv;
   for (int j = tid; j < NB; j += 256) {   // column j of L^{-1}: L x = e_j
-    for (int i = 0; i < j; ++i) Linv[(size_t)i * NB + j] = 0.0;
+    for (int i = 0; i < j; ++i) X[(size_t)i * NB + j] = 0.0;
     for (int i = j; i < NB; ++i) {
       double v = (i == j) ? 1.0 : 0.0;
-      for (int k = j; k < i; ++k) v -= sA[tri(i, k)] * Linv[(size_t)k * NB + j];
-      Linv[(size_t)i * NB + j] = v / sA[tri(i, i)];
+      for (int k = j; k < i; ++k) v -= sA[tri(i, k)] * X[(size_t)k * NB + j];
+      X[(size_t)i * NB + j] = v / sA[tri(i, i)];
     }
+  }
+  if (x_in_lds) {
+    __syncthreads();
+    for (int e = tid; e < NB * NB; e += 256) Linv[e] = X[e];
   }
 }
 
@@ -274,10 +282,13 @@ int pmg_gaussian_mstep(const float* basis, const double* yw, const double* tw, i
   PMG_LAUNCH_CHECK();
   double* Linv = ws + (size_t)NB * (N + NB);
   double* Z = Linv + (size_t)NB * NB;
-  if (lds > 64 * 1024)
+  const size_t lds_x = lds + (size_t)NB * NB * sizeof(double);
+  const int x_in_lds = lds_x <= 160 * 1024 ? 1 : 0;
+  const size_t lds_use = x_in_lds ? lds_x : lds;
+  if (lds_use > 64 * 1024)
     PMG_HIP(hipFuncSetAttribute((const void*)k_gauss_chol_inv, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds));
-  hipLaunchKernelGGL(k_gauss_chol_inv, dim3(1), dim3(256), lds, st, ws, NB, N, Linv, status);
+                                (int)lds_use));
+  hipLaunchKernelGGL(k_gauss_chol_inv, dim3(1), dim3(256), lds_use, st, ws, NB, N, Linv, status, x_in_lds);
   PMG_LAUNCH_CHECK();
   const dim3 g((unsigned)((N + 255) / 256), (unsigned)NB);
   hipLaunchKernelGGL(k_gauss_tri_mm, g, dim3(256), 0, st, Linv, ws, (int64_t)(N + NB), NB, N, 0, Z);
