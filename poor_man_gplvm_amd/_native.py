@@ -19,6 +19,10 @@ LIB_PATH = os.path.join(_HERE, "csrc", "libpmg_hip.so")
 PMG_MAX_BAND = 32
 # pmg_fwdbwd_state slots (include/pmg.h)
 STATE_FWD_IN, STATE_FWD_OUT, STATE_BWD_IN, STATE_BWD_FIRST = 0, 1, 2, 3
+# int32 control words at the start of a pmg_fwdbwd workspace (fb_kernels.h kCtl*):
+# a forward block and a backward block, each {chunks recomputed, relaxation rounds, timeout}
+CTL_WORDS, CTL_FWD, CTL_BWD = 32, 0, 16
+CTL_REPAIRS, CTL_ROUNDS, CTL_ERR = 0, 1, 2
 ABI_VERSION = 1
 
 # every symbol the header declares (checked by tests/test_capi_symbols.py)

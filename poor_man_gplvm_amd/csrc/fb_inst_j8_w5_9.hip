@@ -1,0 +1,8 @@
+// Scan kernel instances: 8 latent(s) per lane, band half-widths 5, 9
+// (see fb_kernels.h; split so that `make -j` compiles them in parallel).
+#include "fb_kernels.h"
+
+namespace pmg {
+PMG_FB_INST(8, 5)
+PMG_FB_INST(8, 9)
+}  // namespace pmg

@@ -11,15 +11,22 @@
 //     below ~1e-38 of the total flush to 0 -- probability-space outputs unchanged);
 //   * the continuous kernel is a row-normalised Toeplitz band K0[i,j] = g[|i-j|]/Z_i
 //     (exactly zero beyond |i-j| = band in the reference's f32), applied
-//     as a 1-D convolution through a per-wave LDS line; the jump kernel is rank-1
-//     (a wave reduction); the 2x2 dynamics mix is elementwise;
-//   * one wave per time chunk; each chunk starts from a uniform guess `warmup`
-//     steps early (HMM forgetting), then every chunk boundary is verified in the
-//     Hilbert projective metric (max-min of log ratios, a contraction of positive
-//     linear maps, so a boundary error <= tol bounds every later output's relative
-//     error by tol) and chunks that fail are recomputed exactly from their
-//     predecessor's state by a single-wave repair pass (rare; sequential only over
-//     consecutive failures);
+//     as a 1-D convolution across the lanes of one wave (DPP shifts); the jump kernel
+//     is rank-1 (a wave reduction); the 2x2 dynamics mix is elementwise;
+//   * main pass: one wave per time chunk; each chunk starts from a uniform guess
+//     `warmup` steps early (HMM forgetting);
+//   * every chunk boundary is then verified in the Hilbert projective metric (max-min
+//     of log ratios; positive linear maps contract it, so a boundary error <= tol
+//     bounds every later output's relative error by tol), and the chunks behind a
+//     failing boundary are recomputed by a persistent RELAXATION kernel: one wave per
+//     segment of G consecutive chunks (<= one workgroup per CU, all co-resident),
+//     rounds separated by a grid barrier.  In a round a segment recomputes its chunks
+//     sequentially from its first inconsistent boundary (stopping as soon as a
+//     recomputed state coalesces with the old one); a segment whose end state moved
+//     hands it to its right neighbour for the next round.  The rounds end when no
+//     segment end moved, i.e. every boundary verifies.  A slowly forgetting chain (the
+//     nearly flat tuning of the first EM iterations) thus costs ~(forgetting length)
+//     sequential steps, not T;
 //   * the smoother uses the equivalent alpha-beta form gamma_t ~ alpha_t * beta_t
 //     with beta_{T-1} = 1 (the reference's RTS seed acausal_{T-1} = post_{T-1}), so
 //     the backward pass needs only alpha_t and the emission -- no stored priors.
@@ -39,13 +46,34 @@
 namespace pmg {
 
 constexpr int kMaxBand = 32;
-constexpr int kFixRounds = 2;  // parallel repair rounds before the sequential fallback
 // Emission / alpha rows are prefetched this many steps ahead on the chunk-parallel
 // kernels: with ~2 waves per SIMD the step's VALU work (~0.3 us) cannot cover an HBM
 // round trip (~2 us), so the row ring, not other waves, hides the latency.
 constexpr int kPfFwd = 4;
 constexpr int kPfBwdWarm = 4;
 constexpr int kPfBwdOut = 2;
+// the relaxation kernel runs <= 1 wave per CU: a deeper ring covers the latency alone,
+// as deep as the registers allow (a backward row is 3J floats)
+template <int J> constexpr int pf_relax_fwd() { return J >= 16 ? 4 : 8; }
+template <int J> constexpr int pf_relax_bwd() { return J >= 16 ? 2 : (J >= 8 ? 4 : 8); }
+
+// Control words at the start of the scan workspace (int32), one block per direction
+// (forward at word 0, backward at word kCtlStride):
+//   +0 chunks recomputed, +1 relaxation rounds, +2 timeout flag      (zeroed by phase 1)
+//   +4 boundaries flagged by the verify, +5 barrier arrivals,
+//   +6..+8 segment-end changes of rounds k % 3                       (zeroed by phase 2)
+enum {
+  kCtlRepairs = 0,
+  kCtlRounds = 1,
+  kCtlErr = 2,
+  kCtlPending = 4,
+  kCtlArrive = 5,
+  kCtlChanged = 6,
+  kCtlStride = 16,
+};
+constexpr int kCtlPhase2Words = 12;                    // words 4 .. 15 of a block
+constexpr uint64_t kSpinTicks = 200000000ull;          // 2 s of the 100 MHz real-time clock
+constexpr int kRelaxMaxSeg = 512;                      // segment-state slots in the workspace
 
 struct FBParams {
   const float* delta;
@@ -66,6 +94,7 @@ struct FBParams {
   float* alpha;
   double* logc;
   double* chunk_logz;
+  double* logz;
   float* s_in;
   float* s_out;
   // backward
@@ -76,7 +105,11 @@ struct FBParams {
   float* b_in;
   float* b_first;
   int* flags;
-  int* repairs;
+  int* ctl;       // this direction's control block
+  // relaxation: segments of G chunks, S segments; end states double-buffered by round
+  float* seg_end;  // [2][S][2*Lpad]
+  int* seg_chg;    // [2][S]
+  int G, S;
   int Lpad;  // 64*J
 };
 
@@ -94,19 +127,6 @@ __device__ __forceinline__ void load_row(const float* __restrict__ row, int L, i
   } else {
 #pragma unroll
     for (int j = 0; j < J; ++j) v[j] = (j0 + j < L) ? row[j0 + j] : 0.f;
-  }
-}
-
-template <int J>
-__device__ __forceinline__ void store_row(float* __restrict__ row, int L, int j0, const float v[J]) {
-  if ((L & 3) == 0 && (J & 3) == 0 && j0 + J <= L) {
-#pragma unroll
-    for (int j = 0; j < J; j += 4)
-      *reinterpret_cast<float4*>(row + j0 + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
-  } else {
-#pragma unroll
-    for (int j = 0; j < J; ++j)
-      if (j0 + j < L) row[j0 + j] = v[j];
   }
 }
 
@@ -130,27 +150,6 @@ __device__ __forceinline__ void em_exp(const FBParams& p, int j0, const EmRaw<J>
   for (int j = 0; j < J; ++j) e[j] = (j0 + j < p.L) ? exp_acc(fmaf(p.s, r.d[j], r.ph)) : 0.f;
 }
 
-// out[j] = sum_{k=-WP..WP} g[|k|] * in[j+k]  over the whole latent line (zero halo)
-// Multi-wave teams: through an LDS line (one barrier each side).
-template <int J, int WP>
-__device__ __forceinline__ void band_conv_lds(const FBParams& p, float* lds, int j0, const float in[J],
-                                              float out[J]) {
-#pragma unroll
-  for (int j = 0; j < J; ++j) lds[WP + j0 + j] = in[j];
-  __syncthreads();
-  float win[J + 2 * WP];
-#pragma unroll
-  for (int k = 0; k < J + 2 * WP; ++k) win[k] = lds[j0 + k];
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    float acc = p.g[0] * win[j + WP];
-#pragma unroll
-    for (int k = 1; k <= WP; ++k) acc = fmaf(p.g[k], win[j + WP - k] + win[j + WP + k], acc);
-    out[j] = acc;
-  }
-  __syncthreads();
-}
-
 // One wave holds the whole line (lane l owns latents lJ .. lJ+J-1): the halo comes
 // from the neighbouring lanes through wavefront-shift DPP moves (wave_shr:1 /
 // wave_shl:1; the lanes past either end read 0), so the step touches no LDS.  The
@@ -164,8 +163,9 @@ __device__ __forceinline__ float wave_shl1(float v) {  // lane i <- lane i+1 (la
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
 }
 
+// out[j] = sum_{k=-WP..WP} g[|k|] * in[j+k]  over the whole latent line (zero halo)
 template <int J, int WP>
-__device__ __forceinline__ void band_conv_dpp(const FBParams& p, const float in[J], float out[J]) {
+__device__ __forceinline__ void band_conv(const FBParams& p, const float in[J], float out[J]) {
   constexpr int NL = (WP + J - 1) / J;  // neighbour lanes on each side
   constexpr int C = NL * J;             // window index of this lane's first latent
   float win[J + 2 * C];
@@ -196,88 +196,29 @@ __device__ __forceinline__ void band_conv_dpp(const FBParams& p, const float in[
   }
 }
 
-template <int J, int WP, class Team>
-__device__ __forceinline__ void band_conv(const FBParams& p, float* lds, int j0, const float in[J],
-                                          float out[J]) {
-  if constexpr (Team::NW == 1) {
-    (void)lds;
-    (void)j0;
-    band_conv_dpp<J, WP>(p, in, out);
-  } else {
-    band_conv_lds<J, WP>(p, lds, j0, in, out);
-  }
+// wave-wide reductions of one chain (one wave carries it)
+__device__ __forceinline__ void chain_sum2(float& a, float& b) { wave_sum2(a, b); }
+__device__ __forceinline__ float chain_sum(float a) { return wave_sum(a); }
+
+// ---------------------------------------------------------------------------
+// Hilbert projective distance between two non-negative (2, Lpad) states.
+// Unweighted (state space): components below 1e-30 of the max on both sides are
+// ignored, a component above 1e-20 on one side only counts as a failure.  Weighted by
+// w (the alpha row in its (2, L) layout; backward boundaries compare the POSTERIOR,
+// |posterior| <= 1): components below 1e-14 move no output by more than 1e-14
+// absolute (parity atol 1e-12); above it the ratio spread bounds the relative error.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float hilbert_finish(float lo, float hi, int bad) {
+  lo = wave_min_shfl(lo);
+  hi = wave_max_shfl(hi);
+  if (__ballot(bad)) return INFINITY;
+  if (hi < lo) return 0.f;
+  return hi - lo;
 }
 
-// ---------------------------------------------------------------------------
-// Teams: the threads that carry ONE chain.  The chunk-parallel kernels use one wave
-// per chunk (DPP reductions, no block barriers); the sequential repair of a long
-// cascade uses NW waves on the same chain (wave DPP + LDS partials behind a block
-// barrier; the scratch is double-buffered so one barrier per reduction suffices).
-// Thread t owns latents j0 = t*J .. t*J+J-1 in both cases.
-// ---------------------------------------------------------------------------
-struct WaveTeam {
-  static constexpr int NW = 1;
-  __device__ explicit WaveTeam(float*) {}
-  __device__ void sum2(float& a, float& b) { wave_sum2(a, b); }
-  __device__ float sum(float a) { return wave_sum(a); }
-  __device__ float vmax(float a) { return wave_max_shfl(a); }
-  __device__ float vmin(float a) { return wave_min_shfl(a); }
-  __device__ bool any(bool b) { return __ballot(b) != 0ull; }
-};
-
-template <int NW_>
-struct BlockTeam {
-  static constexpr int NW = NW_;
-  float* red;  // LDS scratch, 2 x 2 x NW floats
-  int buf = 0;
-  __device__ explicit BlockTeam(float* r) : red(r) {}
-  __device__ float* slot() {
-    float* r = red + buf * 2 * NW;
-    buf ^= 1;
-    return r;
-  }
-  __device__ void sum2(float& a, float& b) {
-    wave_sum2(a, b);
-    float* r = slot();
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-      r[w] = a;
-      r[NW + w] = b;
-    }
-    __syncthreads();
-    float A = 0.f, B = 0.f;
-#pragma unroll
-    for (int i = 0; i < NW; ++i) {
-      A += r[i];
-      B += r[NW + i];
-    }
-    a = A;
-    b = B;
-  }
-  __device__ float sum(float a) {
-    float b = 0.f;
-    sum2(a, b);
-    return a;
-  }
-  __device__ float vmax(float a) {
-    a = wave_max_shfl(a);
-    float* r = slot();
-    if ((threadIdx.x & 63) == 0) r[threadIdx.x >> 6] = a;
-    __syncthreads();
-    float m = r[0];
-#pragma unroll
-    for (int i = 1; i < NW; ++i) m = fmaxf(m, r[i]);
-    return m;
-  }
-  __device__ float vmin(float a) { return -vmax(-a); }
-  __device__ bool any(bool b) { return vmax(__ballot(b) ? 1.f : 0.f) > 0.f; }
-};
-
-// Hilbert projective distance between two non-negative (2, Lpad) states held in
-// memory; components below 1e-30 of the max on both sides are ignored, a
-// component significant (> 1e-20) on one side only counts as a failure.
+// both states in memory, lane-strided (one wave)
 __device__ __forceinline__ float hilbert_dist(const float* __restrict__ x, const float* __restrict__ y, int n,
-                              const float* __restrict__ w = nullptr, int L = 0, int Lpad = 0) {
+                                              const float* __restrict__ w = nullptr, int L = 0, int Lpad = 0) {
   const int lane = threadIdx.x & 63;
   // every operand is fetched up front (n = 2*Lpad <= 2048: at most 32 per lane) so the
   // wave pays one memory round trip, not one per strided pass
@@ -289,7 +230,7 @@ __device__ __forceinline__ float hilbert_dist(const float* __restrict__ x, const
     float wi = 0.f;
     if (i < n) {
       wi = 1.f;
-      if (w) {  // optional weights w in the (2, L) alpha-row layout for state index i = d*Lpad + j
+      if (w) {  // state index i = d*Lpad + j
         const int d = i >= Lpad ? 1 : 0, j = i - d * Lpad;
         wi = j < L ? w[d * L + j] : 0.f;
       }
@@ -307,10 +248,6 @@ __device__ __forceinline__ float hilbert_dist(const float* __restrict__ x, const
   ym = wave_max_shfl(ym);
   if (!(xm > 0.f) || !(ym > 0.f)) return INFINITY;
   const float ix = 1.f / xm, iy = 1.f / ym;
-  // unweighted (state space): ratios of components above 1e-30 of the max, a component
-  // above 1e-20 on one side only fails.  Weighted (posterior space, |posterior| <= 1):
-  // components below 1e-14 move no output by more than 1e-14 absolute (parity atol is
-  // 1e-12); above it the ratio spread bounds the relative error.
   const float lo_thr = w ? 1e-14f : 1e-30f, hi_thr = w ? 1e-12f : 1e-20f;
   float lo = INFINITY, hi = -INFINITY;
   int bad = 0;
@@ -325,52 +262,58 @@ __device__ __forceinline__ float hilbert_dist(const float* __restrict__ x, const
       bad = 1;
     }
   }
-  lo = wave_min_shfl(lo);
-  hi = wave_max_shfl(hi);
-  if (__ballot(bad)) return INFINITY;
-  if (hi < lo) return 0.f;
-  return hi - lo;
+  return hilbert_finish(lo, hi, bad);
 }
 
-// same metric, x held in registers with the (2, Lpad) lane layout, y in memory
-template <int J, class Team>
-__device__ float hilbert_reg(Team& tm, const float x0[J], const float x1[J], const float* __restrict__ y,
-                             int Lpad, int j0) {
-  float xm = 0.f, ym = 0.f;
+// same metric, x held in registers in the (2, Lpad) lane layout, y in memory;
+// optional weights w in the (2, L) alpha-row layout
+template <int J>
+__device__ float hilbert_reg(const float x0[J], const float x1[J], const float* __restrict__ y, int Lpad, int j0,
+                             const float* __restrict__ w = nullptr, int L = 0) {
+  float a[2 * J], b[2 * J];
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    xm = fmaxf(xm, fmaxf(x0[j], x1[j]));
-    ym = fmaxf(ym, fmaxf(y[j0 + j], y[Lpad + j0 + j]));
+    float w0 = 1.f, w1 = 1.f;
+    if (w) {
+      w0 = j0 + j < L ? w[j0 + j] : 0.f;
+      w1 = j0 + j < L ? w[L + j0 + j] : 0.f;
+    }
+    a[j] = x0[j] * w0;
+    a[J + j] = x1[j] * w1;
+    b[j] = y[j0 + j] * w0;
+    b[J + j] = y[Lpad + j0 + j] * w1;
   }
-  xm = tm.vmax(xm);
-  ym = tm.vmax(ym);
+  float xm = 0.f, ym = 0.f;
+#pragma unroll
+  for (int j = 0; j < 2 * J; ++j) {
+    xm = fmaxf(xm, a[j]);
+    ym = fmaxf(ym, b[j]);
+  }
+  xm = wave_max_shfl(xm);
+  ym = wave_max_shfl(ym);
   if (!(xm > 0.f) || !(ym > 0.f)) return INFINITY;
   const float ix = 1.f / xm, iy = 1.f / ym;
+  const float lo_thr = w ? 1e-14f : 1e-30f, hi_thr = w ? 1e-12f : 1e-20f;
   float lo = INFINITY, hi = -INFINITY;
   int bad = 0;
 #pragma unroll
   for (int j = 0; j < 2 * J; ++j) {
-    const float a = (j < J ? x0[j] : x1[j - J]) * ix;
-    const float b = (j < J ? y[j0 + j] : y[Lpad + j0 + j - J]) * iy;
-    if (a > 1e-30f && b > 1e-30f) {
-      const float r = __logf(a) - __logf(b);
+    const float u = a[j] * ix, v = b[j] * iy;
+    if (u > lo_thr && v > lo_thr) {
+      const float r = __logf(u) - __logf(v);
       lo = fminf(lo, r);
       hi = fmaxf(hi, r);
-    } else if (fmaxf(a, b) > 1e-20f) {
+    } else if (fmaxf(u, v) > hi_thr) {
       bad = 1;
     }
   }
-  lo = tm.vmin(lo);
-  hi = tm.vmax(hi);
-  if (tm.any(bad != 0)) return INFINITY;
-  if (hi < lo) return 0.f;
-  return hi - lo;
+  return hilbert_finish(lo, hi, bad);
 }
 
 // ---------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------
-template <int J, int WP, class Team = WaveTeam>
+template <int J, int WP>
 struct Fwd {
   float p0[J], p1[J];
   float P0, P1;  // sum of p0, p1 (wave-uniform)
@@ -385,7 +328,7 @@ struct Fwd {
     P0 = 0.5f;
     P1 = 0.5f;
   }
-  __device__ void load_state(Team& tm, const FBParams& p, const float* src, int j0) {
+  __device__ void load_state(const FBParams& p, const float* src, int j0) {
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       p0[j] = src[j0 + j];
@@ -397,7 +340,7 @@ struct Fwd {
       a += p0[j];
       b += p1[j];
     }
-    tm.sum2(a, b);
+    chain_sum2(a, b);
     const float inv = 1.f / (a + b);
 #pragma unroll
     for (int j = 0; j < J; ++j) {
@@ -415,14 +358,13 @@ struct Fwd {
     }
   }
   // one filter step with emission e; returns the normaliser S
-  __device__ float step(Team& tm, const FBParams& p, float* lds, int j0, const float invz[J],
-                        const float e[J]) {
+  __device__ float step(const FBParams& p, int j0, const float invz[J], const float e[J]) {
     float a0[J];
 #pragma unroll
     for (int j = 0; j < J; ++j) a0[j] = fmaf(p0[j], p.A00, p1[j] * p.A10) * invz[j];
     const float jump = fmaf(p.A01, P0, p.A11 * P1) * p.invL;
     float pr0[J];
-    band_conv<J, WP, Team>(p, lds, j0, a0, pr0);
+    band_conv<J, WP>(p, a0, pr0);
     float U0 = 0.f, U1 = 0.f;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
@@ -431,7 +373,7 @@ struct Fwd {
       U0 += p0[j];
       U1 += p1[j];
     }
-    tm.sum2(U0, U1);
+    chain_sum2(U0, U1);
     const float S = U0 + U1;
     const float inv = 1.f / S;
 #pragma unroll
@@ -445,84 +387,10 @@ struct Fwd {
   }
 };
 
-// run forward from t0 (state initialised) to t_e; writes outputs for t >= t_c and the
-// state at t_c-1 into s_in_dst (if given)
-template <int J, int WP, class Team, int PF = 1>
-__device__ double fwd_run(Team& tm, const FBParams& p, Fwd<J, WP, Team>& st, float* lds, int j0,
-                          const float invz[J], int64_t t0, int64_t t_c, int64_t t_e, float* s_in_dst) {
-  double logz = 0.0;
-  if (t0 >= t_e) return 0.0;
-  // emission rows PF steps ahead (the sequential repair chain is latency-bound; the
-  // chunk-parallel kernels hide latency across waves and use PF = 1)
-  // the row reference m[t] of logc rides in the same ring: a load consumed in its own
-  // step would make the compiler drain every outstanding load (s_waitcnt vmcnt(0))
-  EmRaw<J> ring[PF];
-  double mr[PF];
-#pragma unroll
-  for (int q = 0; q < PF; ++q)
-    if (t0 + q < t_e) {
-      em_load<J>(p, t0 + q, j0, ring[q]);
-      mr[q] = p.m[t0 + q];
-    }
-  for (int64_t tb = t0; tb < t_e; tb += PF) {
-#pragma unroll
-    for (int q = 0; q < PF; ++q) {
-      const int64_t t = tb + q;
-      if (t < t_e) {
-        float e[J];
-        em_exp<J>(p, j0, ring[q], e);
-        const double mt = mr[q];
-        if (t + PF < t_e) {
-          em_load<J>(p, t + PF, j0, ring[q]);
-          mr[q] = p.m[t + PF];
-        }
-        const float S = st.step(tm, p, lds, j0, invz, e);
-        if (t >= t_c) {
-          float* arow = p.alpha + t * 2 * (int64_t)p.L;
-          store_row<J>(arow, p.L, j0, st.p0);
-          store_row<J>(arow + p.L, p.L, j0, st.p1);
-          const double lc = (double)__logf(S) + p.s_d * mt;
-          if (threadIdx.x == 0) p.logc[t] = lc;
-          logz += lc;
-        } else if (t == t_c - 1 && s_in_dst) {
-          st.save_state(p, s_in_dst, j0);
-        }
-      }
-    }
-  }
-  return logz;
-}
-
-#define PMG_FB_PROLOGUE_T(JJ, NWW)                                      \
-  __shared__ __attribute__((aligned(16))) float lds[64 * (NWW) * (JJ) + 2 * WP + 4 * (NWW)]; \
-  float* team_red = lds + 64 * (NWW) * (JJ) + 2 * WP;                   \
-  const int lane = threadIdx.x & 63;                                    \
-  (void)lane;                                                           \
-  const int j0 = threadIdx.x * (JJ);                                    \
-  for (int k = threadIdx.x; k < 64 * (NWW) * (JJ) + 2 * WP; k += 64 * (NWW)) lds[k] = 0.f; \
-  __syncthreads();                                                      \
-  float invz[JJ];                                                       \
-  _Pragma("unroll") for (int j = 0; j < (JJ); ++j) invz[j] = (j0 + j < p.L) ? p.invz[j0 + j] : 0.f; \
-  const size_t SZ = (size_t)2 * p.Lpad;                                 \
-  (void)SZ;                                                             \
-  (void)team_red;
-
-#define PMG_FB_PROLOGUE                                                 \
-  __shared__ __attribute__((aligned(16))) float lds[64 * J + 2 * WP];  \
-  const int lane = threadIdx.x & 63;                                    \
-  const int j0 = lane * J;                                              \
-  WaveTeam tm(nullptr);                                                 \
-  for (int k = lane; k < 64 * J + 2 * WP; k += 64) lds[k] = 0.f;        \
-  __syncthreads();                                                      \
-  float invz[J];                                                        \
-  _Pragma("unroll") for (int j = 0; j < J; ++j) invz[j] = (j0 + j < p.L) ? p.invz[j0 + j] : 0.f; \
-  const size_t SZ = (size_t)2 * p.Lpad;                                 \
-  (void)SZ;
-
 // ---------------------------------------------------------------------------
-// Chunk-parallel streaming path (one wave per chain).  Every row access is a raw
-// buffer load/store through a per-row resource (num_records = row bytes), so lanes
-// past L read 0 / drop their writes without exec masking, and the step loop is
+// Streaming step loops (one wave per chain).  Every row access is a raw buffer
+// load/store through a per-row resource (num_records = row bytes), so lanes past L
+// read 0 / drop their writes without exec masking, and the step loop is
 // straight-line: the rows of the next PF steps stay in flight across steps (the
 // waitcnt pass only sees one in-order vmcnt stream; any divergent load or store in
 // the loop would make it drain the ring).  VEC: L % 4 == 0 (16-byte row accesses).
@@ -590,7 +458,6 @@ __device__ __forceinline__ void bem_load(const FBParams& p, int64_t t, int j0, E
 template <int J, int WP, int PF, bool VEC, bool OUT>
 __device__ __forceinline__ double fwd_stream(const FBParams& p, Fwd<J, WP>& st, int j0, const float invz[J],
                                              int64_t t_a, int64_t t_b) {
-  WaveTeam tm(nullptr);
   double logz = 0.0;
   if (t_a >= t_b) return 0.0;
   const int64_t last = t_b - 1;
@@ -612,7 +479,7 @@ __device__ __forceinline__ double fwd_stream(const FBParams& p, Fwd<J, WP>& st, 
       bem_load<J, VEC>(p, tl, j0, ring[q]);
       if constexpr (OUT) mr[q] = p.m[tl];
     }
-    const float S = st.step(tm, p, nullptr, j0, invz, e);
+    const float S = st.step(p, j0, invz, e);
     if constexpr (OUT) {
       float* arow = p.alpha + t * 2 * (int64_t)p.L;
       bstore_row<J, VEC>(arow, p.L, j0, st.p0);
@@ -633,31 +500,6 @@ __device__ __forceinline__ double fwd_stream(const FBParams& p, Fwd<J, WP>& st, 
   return logz;
 }
 
-template <int J, int WP, bool VEC>
-__device__ __forceinline__ void forward_chunk(const FBParams& p, int c, int j0, const float invz[J], bool fix) {
-  const size_t SZ = (size_t)2 * p.Lpad;
-  const int64_t t_c = (int64_t)c * p.C;
-  const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
-  Fwd<J, WP> st;
-  float* sin = p.s_in + (size_t)c * SZ;
-  if (fix) {
-    WaveTeam tm(nullptr);
-    st.load_state(tm, p, sin, j0);
-  } else {
-    int64_t t0 = (c == 0) ? 0 : t_c - p.B;
-    if (t0 < 0) t0 = 0;
-    st.init_uniform(p, j0);
-    fwd_stream<J, WP, kPfFwd, VEC, false>(p, st, j0, invz, t0, t_c);
-    if (c > 0) st.save_state(p, sin, j0);  // the restart state of a later repair (the guess if no warm-up)
-  }
-  const double lz = fwd_stream<J, WP, kPfFwd, VEC, true>(p, st, j0, invz, t_c, t_e);
-  st.save_state(p, p.s_out + (size_t)c * SZ, j0);
-  if ((threadIdx.x & 63) == 0) {
-    p.chunk_logz[c] = lz;
-    if (fix) atomicAdd(&p.repairs[0], 1);
-  }
-}
-
 #define PMG_FB_LANE_SETUP                                               \
   const int lane = threadIdx.x & 63;                                    \
   const int j0 = lane * J;                                              \
@@ -665,78 +507,192 @@ __device__ __forceinline__ void forward_chunk(const FBParams& p, int c, int j0, 
   _Pragma("unroll") for (int j = 0; j < J; ++j) invz[j] = (j0 + j < p.L) ? p.invz[j0 + j] : 0.f;
 
 // speculative pass: chunk c starts `B` steps early from a uniform guess
+template <int J, int WP, bool VEC>
+__device__ __forceinline__ void forward_chunk(const FBParams& p, int c, int j0, const float invz[J]) {
+  const size_t SZ = (size_t)2 * p.Lpad;
+  const int64_t t_c = (int64_t)c * p.C;
+  const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
+  Fwd<J, WP> st;
+  int64_t t0 = (c == 0) ? 0 : t_c - p.B;
+  if (t0 < 0) t0 = 0;
+  st.init_uniform(p, j0);
+  fwd_stream<J, WP, kPfFwd, VEC, false>(p, st, j0, invz, t0, t_c);
+  if (c > 0) st.save_state(p, p.s_in + (size_t)c * SZ, j0);  // the start the verify checks
+  const double lz = fwd_stream<J, WP, kPfFwd, VEC, true>(p, st, j0, invz, t_c, t_e);
+  st.save_state(p, p.s_out + (size_t)c * SZ, j0);
+  if ((threadIdx.x & 63) == 0) p.chunk_logz[c] = lz;
+}
+
 template <int J, int WP>
 __global__ void __launch_bounds__(64) k_forward(FBParams p) {
   const int c = blockIdx.x;
   if (c >= p.M) return;
   PMG_FB_LANE_SETUP
+  (void)lane;
   if constexpr (J % 4 == 0) {
     if ((p.L & 3) == 0) {
-      forward_chunk<J, WP, true>(p, c, j0, invz, false);
+      forward_chunk<J, WP, true>(p, c, j0, invz);
       return;
     }
   }
-  forward_chunk<J, WP, false>(p, c, j0, invz, false);
+  forward_chunk<J, WP, false>(p, c, j0, invz);
 }
 
-// parallel repair round: every flagged chunk restarts from its snapshot s_in[c]
-template <int J, int WP>
-__global__ void __launch_bounds__(64) k_forward_fix(FBParams p) {
-  const int c = blockIdx.x;
-  if (c >= p.M || c == 0 || p.flags[c] == 0) return;
-  PMG_FB_LANE_SETUP
-  if constexpr (J % 4 == 0) {
-    if ((p.L & 3) == 0) {
-      forward_chunk<J, WP, true>(p, c, j0, invz, true);
-      return;
-    }
-  }
-  forward_chunk<J, WP, false>(p, c, j0, invz, true);
-}
-
-// sequential fallback for whatever is still flagged after the parallel rounds.  A long
-// cascade (slowly forgetting chain, e.g. the flat tuning of the first EM iterations)
-// is latency-critical, so NW waves carry the one chain (J/NW latents per thread).
-template <int J> constexpr int repair_nw() { return J >= 8 ? 8 : J; }
-
-template <int J, int WP>
-__global__ void __launch_bounds__(64 * repair_nw<J>()) k_forward_repair(FBParams p) {
-  constexpr int NW = repair_nw<J>(), JB = J / NW;
-  PMG_FB_PROLOGUE_T(JB, NW)
-  BlockTeam<NW> tm(team_red);
-  int repairs = 0;
-  bool changed = false;
-  int c = 1;
-  Fwd<JB, WP, BlockTeam<NW>> st;
-  while (c < p.M) {
-    if (!changed) {  // jump to the next flagged chunk, 64 flags at a time (every wave alike)
-      int found = -1;
-      for (int base = c; base < p.M && found < 0; base += 64) {
-        const int idx = base + lane;
-        const bool f = idx < p.M && p.flags[idx] != 0;
-        const unsigned long long bal = __ballot(f);
-        if (bal) found = base + (int)__builtin_ctzll(bal);
+// ---------------------------------------------------------------------------
+// relaxation-kernel plumbing
+// ---------------------------------------------------------------------------
+// Grid barrier of the S co-resident single-wave workgroups (a monotone arrival
+// counter): drain this wave's stores, agent-scope release, arrive, relaxed poll,
+// agent-scope acquire.  The spin is bounded (kSpinTicks of the real-time clock, or
+// another wave's timeout): on expiry the timeout word is set and false returned.
+__device__ __forceinline__ bool relax_barrier(int* ctl, int target) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int ok = 1;
+  if ((threadIdx.x & 63) == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(ctl + kCtlArrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(ctl + kCtlArrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__hip_atomic_load(ctl + kCtlErr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+          __builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
+        __hip_atomic_store(ctl + kCtlErr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
       }
-      if (found < 0) break;
-      c = found;
-      st.load_state(tm, p, p.s_out + (size_t)(c - 1) * SZ, j0);
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  return __builtin_amdgcn_readfirstlane(ok) != 0;
+}
+
+__device__ __forceinline__ int ctl_load(int* ctl, int w) {
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctl + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// Per-round change counters rotate over 3 slots: round k counts into slot k % 3 and
+// every wave reads it after barrier k (so all take the same exit decision); wave 0
+// zeroes slot (k+1) % 3 during round k -- its last readers passed barrier k-1, its
+// next writers start after barrier k.
+__device__ __forceinline__ void relax_publish(const FBParams& p, int k, int s, bool changed) {
+  if ((threadIdx.x & 63) == 0) {
+    p.seg_chg[(k & 1) * p.S + s] = changed ? 1 : 0;
+    if (changed) __hip_atomic_fetch_add(p.ctl + kCtlChanged + k % 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (s == 0) __hip_atomic_store(p.ctl + kCtlChanged + (k + 1) % 3, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// first (lowest, DIR > 0) or last (highest, DIR < 0) flagged index in [lo, hi), or -1
+template <int DIR>
+__device__ __forceinline__ int find_flag(const int* flags, int lo, int hi) {
+  const int lane = threadIdx.x & 63;
+  if constexpr (DIR > 0) {
+    for (int base = lo; base < hi; base += 64) {
+      const int idx = base + lane;
+      const unsigned long long bal = __ballot(idx < hi && flags[idx] != 0);
+      if (bal) return base + (int)__builtin_ctzll(bal);
+    }
+  } else {
+    for (int top = hi - 1; top >= lo; top -= 64) {
+      const int idx = top - lane;
+      const unsigned long long bal = __ballot(idx >= lo && flags[idx] != 0);
+      if (bal) return top - (int)__builtin_ctzll(bal);
+    }
+  }
+  return -1;
+}
+
+// f64 sum of x[0..n) in one fixed order (lane-strided partials, then the wave butterfly)
+__device__ __forceinline__ double wave_sum_fixed(const double* x, int n) {
+  double a = 0.0;
+  for (int i = threadIdx.x & 63; i < n; i += 64) a += x[i];
+  return wave_sum_f64(a);
+}
+
+// ---------------------------------------------------------------------------
+// forward relaxation
+// ---------------------------------------------------------------------------
+// recompute chunks c0 .. b-1 from st (the filter state at c0*C - 1).  After chunk c,
+// if its new end state is within tol of the old s_out[c] and boundary c+1 is not
+// flagged (flg, round 0 only), the rest of the segment is consistent: stop.  Returns
+// true iff the segment's end state (chunk b-1) moved.
+template <int J, int WP, bool VEC>
+__device__ bool fwd_segment(const FBParams& p, Fwd<J, WP>& st, int c0, int b, int j0, const float invz[J],
+                            const int* flg, int& nrep) {
+  const size_t SZ = (size_t)2 * p.Lpad;
+  for (int c = c0; c < b; ++c) {
     const int64_t t_c = (int64_t)c * p.C;
     const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
     st.save_state(p, p.s_in + (size_t)c * SZ, j0);
-    const double lz = fwd_run<JB, WP, BlockTeam<NW>, 16 / JB>(tm, p, st, lds, j0, invz, t_c, t_c, t_e, (float*)nullptr);
-    float* sout = p.s_out + (size_t)c * SZ;
-    const float d = hilbert_reg<JB>(tm, st.p0, st.p1, sout, p.Lpad, j0);
-    changed = !(d <= p.tol);
-    __syncthreads();  // every wave has read sout before it is overwritten
-    st.save_state(p, sout, j0);
-    if (threadIdx.x == 0) p.chunk_logz[c] = lz;
-    __threadfence();
-    __syncthreads();
-    ++repairs;
-    ++c;
+    const double lz = fwd_stream<J, WP, pf_relax_fwd<J>(), VEC, true>(p, st, j0, invz, t_c, t_e);
+    if ((threadIdx.x & 63) == 0) p.chunk_logz[c] = lz;
+    ++nrep;
+    float* so = p.s_out + (size_t)c * SZ;
+    const float d = hilbert_reg<J>(st.p0, st.p1, so, p.Lpad, j0);  // each lane reads only its own slots
+    st.save_state(p, so, j0);
+    if (d <= p.tol && (c + 1 >= b || !(flg && flg[c + 1]))) return false;
   }
-  if (threadIdx.x == 0) p.repairs[0] += repairs;
+  return true;
+}
+
+template <int J, int WP, bool VEC>
+__device__ void forward_relax(const FBParams& p, int j0, const float invz[J]) {
+  const size_t SZ = (size_t)2 * p.Lpad;
+  const int s = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  int nrep = 0, rounds = 0;
+  if (ctl_load(p.ctl, kCtlPending) > 0) {
+    const int a = s * p.G;
+    const int b = a + p.G < p.M ? a + p.G : p.M;
+    Fwd<J, WP> st;
+    bool changed = false;
+    // round 0: from the first boundary the verify flagged (it snapshotted the carry into s_in)
+    const int c0 = find_flag<1>(p.flags, a > 1 ? a : 1, b);
+    if (c0 >= 0) {
+      st.load_state(p, p.s_in + (size_t)c0 * SZ, j0);
+      changed = fwd_segment<J, WP, VEC>(p, st, c0, b, j0, invz, p.flags, nrep);
+    }
+    for (int k = 0;; ++k) {
+      if (changed) st.save_state(p, p.seg_end + ((size_t)(k & 1) * p.S + s) * SZ, j0);
+      relax_publish(p, k, s, changed);
+      ++rounds;
+      if (!relax_barrier(p.ctl, (k + 1) * p.S)) break;
+      if (ctl_load(p.ctl, kCtlChanged + k % 3) == 0) break;  // no segment end moved: all verified
+      // round k+1: re-verify the first boundary against the left neighbour's new end state
+      changed = false;
+      if (s > 0 && p.seg_chg[(k & 1) * p.S + s - 1]) {
+        const float* X = p.seg_end + ((size_t)(k & 1) * p.S + s - 1) * SZ;
+        const float d = hilbert_dist(X, p.s_in + (size_t)a * SZ, (int)SZ);
+        if (!(d <= p.tol)) {
+          st.load_state(p, X, j0);
+          changed = fwd_segment<J, WP, VEC>(p, st, a, b, j0, invz, nullptr, nrep);
+        }
+      }
+    }
+  }
+  if (lane == 0 && nrep) atomicAdd(p.ctl + kCtlRepairs, nrep);
+  if (s == 0) {  // after the last barrier's acquire (or with no repair at all)
+    const double lz = wave_sum_fixed(p.chunk_logz, p.M);
+    if (lane == 0) {
+      p.logz[0] = lz;
+      p.ctl[kCtlRounds] = rounds;
+    }
+  }
+}
+
+template <int J, int WP>
+__global__ void __launch_bounds__(64) k_forward_relax(FBParams p) {
+  PMG_FB_LANE_SETUP
+  (void)lane;
+  if constexpr (J % 4 == 0) {
+    if ((p.L & 3) == 0) {
+      forward_relax<J, WP, true>(p, j0, invz);
+      return;
+    }
+  }
+  forward_relax<J, WP, false>(p, j0, invz);
 }
 
 // ---------------------------------------------------------------------------
@@ -745,7 +701,7 @@ __global__ void __launch_bounds__(64 * repair_nw<J>()) k_forward_repair(FBParams
 // on the warm-up and on the output path, so two chunks that have converged to
 // the same beta produce bit-identical continuations (as the forward does).
 // ---------------------------------------------------------------------------
-template <int J, int WP, class Team = WaveTeam>
+template <int J, int WP>
 struct Bwd {
   float b0[J], b1[J];  // beta at the current time
 
@@ -771,8 +727,8 @@ struct Bwd {
     }
   }
   // v = e*beta scaled by 1/(V0+V1) (returned in v0/v1); beta <- Trans(v)
-  __device__ void step_back(const FBParams& p, float* lds, int j0, const float invz[J],
-                            const float e[J], float V0, float V1, float v0[J], float v1[J]) {
+  __device__ void step_back(const FBParams& p, int j0, const float invz[J], const float e[J], float V0, float V1,
+                            float v0[J], float v1[J]) {
     const float sc = 1.f / (V0 + V1);
 #pragma unroll
     for (int j = 0; j < J; ++j) {
@@ -780,7 +736,7 @@ struct Bwd {
       v1[j] = e[j] * b1[j] * sc;
     }
     float w0[J];
-    band_conv<J, WP, Team>(p, lds, j0, v0, w0);
+    band_conv<J, WP>(p, v0, w0);
     const float w1 = V1 * sc * p.invL;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
@@ -793,9 +749,9 @@ struct Bwd {
 };
 
 // one plain backward step at time t (beta_t -> beta_{t-1}); v kept in (v0, v1)
-template <int J, int WP, class Team>
-__device__ __forceinline__ void bwd_plain(Team& tm, const FBParams& p, Bwd<J, WP, Team>& st, float* lds,
-                                          int j0, const float invz[J], int64_t t, float v0[J], float v1[J]) {
+template <int J, int WP>
+__device__ __forceinline__ void bwd_plain(const FBParams& p, Bwd<J, WP>& st, int j0, const float invz[J],
+                                          int64_t t, float v0[J], float v1[J]) {
   EmRaw<J> r;
   em_load<J>(p, t, j0, r);
   float e[J];
@@ -806,132 +762,14 @@ __device__ __forceinline__ void bwd_plain(Team& tm, const FBParams& p, Bwd<J, WP
     V0 += e[j] * st.b0[j];
     V1 += e[j] * st.b1[j];
   }
-  tm.sum2(V0, V1);
-  st.step_back(p, lds, j0, invz, e, V0, V1, v0, v1);
+  chain_sum2(V0, V1);
+  st.step_back(p, j0, invz, e, V0, V1, v0, v1);
 }
 
-// plain backward steps t = t_hi .. t_lo (descending) with the emission rows PF steps
-// ahead in a register ring (the warm-up of the chunk-parallel pass)
-template <int J, int WP, class Team, int PF>
-__device__ __forceinline__ void bwd_warm(Team& tm, const FBParams& p, Bwd<J, WP, Team>& st, float* lds,
-                                         int j0, const float invz[J], int64_t t_hi, int64_t t_lo) {
-  if (t_hi < t_lo) return;
-  EmRaw<J> ring[PF];
-#pragma unroll
-  for (int q = 0; q < PF; ++q)
-    if (t_hi - q >= t_lo) em_load<J>(p, t_hi - q, j0, ring[q]);
-  for (int64_t tb = t_hi; tb >= t_lo; tb -= PF) {
-#pragma unroll
-    for (int q = 0; q < PF; ++q) {
-      const int64_t t = tb - q;
-      if (t >= t_lo) {
-        float e[J];
-        em_exp<J>(p, j0, ring[q], e);
-        if (t - PF >= t_lo) em_load<J>(p, t - PF, j0, ring[q]);
-        float V0 = 0.f, V1 = 0.f;
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-          V0 += e[j] * st.b0[j];
-          V1 += e[j] * st.b1[j];
-        }
-        tm.sum2(V0, V1);
-        float v0[J], v1[J];
-        st.step_back(p, lds, j0, invz, e, V0, V1, v0, v1);
-      }
-    }
-  }
-}
-
-// output steps t = t_e-1 .. t_c.  On entry st holds beta_{t_e-1} and (vp0, vp1) the v that
-// produced it (has_prev false at the sequence end).  On exit st holds beta_{t_c}.
-// RHO: also write the joint partner rho (decode); the EM path drops vp0/vp1.
-template <int J>
-struct BwdRow {
-  EmRaw<J> em;
-  float a0[J], a1[J];
-};
-
-template <int J>
-__device__ __forceinline__ void bwd_row_load(const FBParams& p, int64_t t, int j0, BwdRow<J>& r) {
-  em_load<J>(p, t, j0, r.em);
-  const float* arow = p.alpha_in + t * 2 * (int64_t)p.L;
-  load_row<J>(arow, p.L, j0, r.a0);
-  load_row<J>(arow + p.L, p.L, j0, r.a1);
-}
-
-template <int J, int WP, class Team, int PF, bool RHO>
-__device__ void bwd_out(Team& tm, const FBParams& p, Bwd<J, WP, Team>& st, float* lds, int j0,
-                        const float invz[J], int64_t t_c, int64_t t_e, float vp0[J], float vp1[J],
-                        bool has_prev) {
-  const int64_t L = p.L;
-  BwdRow<J> ring[PF];
-#pragma unroll
-  for (int q = 0; q < PF; ++q)
-    if (t_e - 1 - q >= t_c) bwd_row_load<J>(p, t_e - 1 - q, j0, ring[q]);
-  for (int64_t tb = t_e - 1; tb >= t_c; tb -= PF) {
-#pragma unroll
-    for (int q = 0; q < PF; ++q) {
-      const int64_t t = tb - q;
-      if (t >= t_c) {
-        float a0[J], a1[J], e[J];
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-          a0[j] = ring[q].a0[j];
-          a1[j] = ring[q].a1[j];
-        }
-        em_exp<J>(p, j0, ring[q].em, e);
-        if (t - PF >= t_c) bwd_row_load<J>(p, t - PF, j0, ring[q]);
-        float G = 0.f, V0 = 0.f, V1 = 0.f;
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-          a0[j] *= st.b0[j];
-          a1[j] *= st.b1[j];
-          G += a0[j] + a1[j];
-          V0 += e[j] * st.b0[j];
-          V1 += e[j] * st.b1[j];
-        }
-        tm.sum2(V0, V1);
-        G = tm.sum(G);
-        const float iG = 1.f / G;
-        float pp[J];
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-          a0[j] *= iG;
-          a1[j] *= iG;
-          pp[j] = a0[j] + a1[j];
-        }
-        if (p.P) store_row<J>(p.P + t * L, p.L, j0, pp);
-        if (p.gamma) {
-          store_row<J>(p.gamma + t * 2 * L, p.L, j0, a0);
-          store_row<J>(p.gamma + t * 2 * L + L, p.L, j0, a1);
-        }
-        if constexpr (RHO) {
-          if (p.rho && has_prev && t + 1 < p.T) {  // rho_{t+1} = v_{t+1} / sum(alpha_t * beta_t)
-            float r0[J], r1[J];
-#pragma unroll
-            for (int j = 0; j < J; ++j) {
-              r0[j] = vp0[j] * iG;
-              r1[j] = vp1[j] * iG;
-            }
-            store_row<J>(p.rho + (t + 1) * 2 * L, p.L, j0, r0);
-            store_row<J>(p.rho + (t + 1) * 2 * L + L, p.L, j0, r1);
-          }
-        }
-        if (t != t_c) {
-          st.step_back(p, lds, j0, invz, e, V0, V1, vp0, vp1);
-          has_prev = true;
-        }
-      }
-    }
-  }
-}
-
-// ---- chunk-parallel streaming backward (buffer IO, straight-line step loops) ----
 // plain steps t = t_hi .. t_lo (descending), emission rows PF steps ahead
 template <int J, int WP, int PF, bool VEC>
 __device__ __forceinline__ void bwd_stream_warm(const FBParams& p, Bwd<J, WP>& st, int j0, const float invz[J],
                                                 int64_t t_hi, int64_t t_lo) {
-  WaveTeam tm(nullptr);
   if (t_hi < t_lo) return;
   EmRaw<J> ring[PF];
 #pragma unroll
@@ -946,9 +784,9 @@ __device__ __forceinline__ void bwd_stream_warm(const FBParams& p, Bwd<J, WP>& s
       V0 += e[j] * st.b0[j];
       V1 += e[j] * st.b1[j];
     }
-    tm.sum2(V0, V1);
+    chain_sum2(V0, V1);
     float v0[J], v1[J];
-    st.step_back(p, nullptr, j0, invz, e, V0, V1, v0, v1);
+    st.step_back(p, j0, invz, e, V0, V1, v0, v1);
   };
   int64_t tb = t_hi;
   for (; tb - (PF - 1) >= t_lo; tb -= PF) {
@@ -974,13 +812,13 @@ __device__ __forceinline__ void brow_load(const FBParams& p, int64_t t, int j0, 
   bload_row<J, VEC>(arow + p.L, p.L, j0, r.a1);
 }
 
-// output steps t = t_e-1 .. t_c; on entry st = beta_{t_e-1}, on exit beta_{t_c}.
-// MODE 0 (EM): P only.  MODE 1: P / gamma / rho as given (decode, repair).
+// output steps t = t_e-1 .. t_c; on entry st = beta_{t_e-1} and (vp0, vp1) the v that
+// produced it (has_prev false at the sequence end), on exit beta_{t_c}.
+// MODE 0 (EM): P only.  MODE 1: P / gamma / rho as given (decode, relaxation).
 template <int J, int WP, int PF, bool VEC, int MODE>
 __device__ __forceinline__ void bwd_stream_out(const FBParams& p, Bwd<J, WP>& st, int j0, const float invz[J],
                                                int64_t t_c, int64_t t_e, float vp0[J], float vp1[J],
                                                bool has_prev) {
-  WaveTeam tm(nullptr);
   if (t_e - 1 < t_c) return;
   const int64_t L = p.L;
   BRow<J> ring[PF];
@@ -1004,8 +842,8 @@ __device__ __forceinline__ void bwd_stream_out(const FBParams& p, Bwd<J, WP>& st
       V0 += e[j] * st.b0[j];
       V1 += e[j] * st.b1[j];
     }
-    tm.sum2(V0, V1);
-    G = tm.sum(G);
+    chain_sum2(V0, V1);
+    G = chain_sum(G);
     const float iG = 1.f / G;
     float pp[J];
 #pragma unroll
@@ -1034,7 +872,7 @@ __device__ __forceinline__ void bwd_stream_out(const FBParams& p, Bwd<J, WP>& st
       }
     }
     if (t != t_c) {
-      st.step_back(p, nullptr, j0, invz, e, V0, V1, vp0, vp1);
+      st.step_back(p, j0, invz, e, V0, V1, vp0, vp1);
       has_prev = true;
     }
   };
@@ -1048,9 +886,9 @@ __device__ __forceinline__ void bwd_stream_out(const FBParams& p, Bwd<J, WP>& st
     if (tb - q >= t_c) body(q, tb - q, false);
 }
 
+// speculative pass: beta guess (ones) `B` steps after the chunk, warmed up backwards
 template <int J, int WP, bool VEC, int MODE>
-__device__ __forceinline__ void backward_chunk(const FBParams& p, int c, int j0, const float invz[J], bool fix) {
-  WaveTeam tm(nullptr);
+__device__ __forceinline__ void backward_chunk(const FBParams& p, int c, int j0, const float invz[J]) {
   const size_t SZ = (size_t)2 * p.Lpad;
   const int64_t t_c = (int64_t)c * p.C;
   const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
@@ -1059,34 +897,27 @@ __device__ __forceinline__ void backward_chunk(const FBParams& p, int c, int j0,
 #pragma unroll
   for (int j = 0; j < J; ++j) vp0[j] = vp1[j] = 0.f;
   bool has_prev = false;
-  if (fix) {
-    st.load_state(p, p.b_in + (size_t)c * SZ, j0);
-    bwd_plain(tm, p, st, nullptr, j0, invz, t_e, vp0, vp1);
+  st.init_ones(p, j0);
+  if (c < p.M - 1) {
+    int64_t t_w = t_e + p.B;  // beta guess (ones) at t_w, exact when t_w is the last bin
+    if (t_w > p.T - 1) t_w = p.T - 1;
+    bwd_stream_warm<J, WP, kPfBwdWarm, VEC>(p, st, j0, invz, t_w, t_e + 1);
+    st.save_state(p, p.b_in + (size_t)c * SZ, j0);  // beta_{t_e}: the start the verify checks
+    bwd_plain(p, st, j0, invz, t_e, vp0, vp1);       // -> beta_{t_e-1}
     has_prev = true;
-  } else {
-    st.init_ones(p, j0);
-    if (c < p.M - 1) {
-      int64_t t_w = t_e + p.B;  // beta guess (ones) at t_w, exact when t_w is the last bin
-      if (t_w > p.T - 1) t_w = p.T - 1;
-      bwd_stream_warm<J, WP, kPfBwdWarm, VEC>(p, st, j0, invz, t_w, t_e + 1);
-      st.save_state(p, p.b_in + (size_t)c * SZ, j0);            // beta_{t_e}
-      bwd_plain(tm, p, st, nullptr, j0, invz, t_e, vp0, vp1);   // -> beta_{t_e-1}
-      has_prev = true;
-    }
   }
   bwd_stream_out<J, WP, kPfBwdOut, VEC, MODE>(p, st, j0, invz, t_c, t_e, vp0, vp1, has_prev);
   st.save_state(p, p.b_first + (size_t)c * SZ, j0);
-  if (fix && (threadIdx.x & 63) == 0) atomicAdd(&p.repairs[1], 1);
 }
 
-#define PMG_BWD_DISPATCH(MODE, FIX)                                     \
+#define PMG_BWD_DISPATCH(MODE)                                          \
   if constexpr (J % 4 == 0) {                                           \
     if ((p.L & 3) == 0) {                                               \
-      backward_chunk<J, WP, true, MODE>(p, c, j0, invz, FIX);           \
+      backward_chunk<J, WP, true, MODE>(p, c, j0, invz);                \
       return;                                                           \
     }                                                                   \
   }                                                                     \
-  backward_chunk<J, WP, false, MODE>(p, c, j0, invz, FIX);
+  backward_chunk<J, WP, false, MODE>(p, c, j0, invz);
 
 // speculative pass, EM outputs (P only)
 template <int J, int WP>
@@ -1094,7 +925,8 @@ __global__ void __launch_bounds__(64) k_backward(FBParams p) {
   const int c = blockIdx.x;
   if (c >= p.M) return;
   PMG_FB_LANE_SETUP
-  PMG_BWD_DISPATCH(0, false)
+  (void)lane;
+  PMG_BWD_DISPATCH(0)
 }
 
 // speculative pass, decode outputs (P / gamma / rho as given)
@@ -1103,97 +935,115 @@ __global__ void __launch_bounds__(64) k_backward_full(FBParams p) {
   const int c = blockIdx.x;
   if (c >= p.M) return;
   PMG_FB_LANE_SETUP
-  PMG_BWD_DISPATCH(1, false)
+  (void)lane;
+  PMG_BWD_DISPATCH(1)
 }
 
-// parallel repair round: flagged chunk c restarts from its snapshot b_in[c] = beta_{t_e}
-template <int J, int WP>
-__global__ void __launch_bounds__(64) k_backward_fix(FBParams p) {
-  const int c = blockIdx.x;
-  if (c >= p.M - 1 || p.flags[c] == 0) return;
-  PMG_FB_LANE_SETUP
-  PMG_BWD_DISPATCH(1, true)
-}
-
-// sequential fallback (descending chunks), NW waves on the one chain
-template <int J, int WP>
-__global__ void __launch_bounds__(64 * repair_nw<J>()) k_backward_repair(FBParams p) {
-  constexpr int NW = repair_nw<J>(), JB = J / NW;
-  PMG_FB_PROLOGUE_T(JB, NW)
-  BlockTeam<NW> tm(team_red);
-  int repairs = 0;
-  bool changed = false;
-  int c = p.M - 2;
-  while (c >= 0) {
-    if (!changed) {
-      int found = -1;
-      for (int top = c; top >= 0 && found < 0; top -= 64) {
-        const int idx = top - lane;
-        const bool f = idx >= 0 && p.flags[idx] != 0;
-        const unsigned long long bal = __ballot(f);
-        if (bal) found = top - (int)__builtin_ctzll(bal);
-      }
-      if (found < 0) break;
-      c = found;
-    }
+// ---------------------------------------------------------------------------
+// backward relaxation (chunks in descending order; a segment's "left" neighbour in
+// the data flow is the segment above it)
+// ---------------------------------------------------------------------------
+// recompute chunks c0, c0-1, .., a from st (beta at (c0+1)*C).  After chunk c, if its
+// new beta at c*C is within tol of the old b_first[c] (weighted by alpha at c*C, the
+// boundary metric of k_verify) and boundary c-1 is not flagged, stop.  Returns true
+// iff the segment's end state (b_first[a]) moved.
+template <int J, int WP, bool VEC>
+__device__ bool bwd_segment(const FBParams& p, Bwd<J, WP>& st, int c0, int a, int j0, const float invz[J],
+                            const int* flg, int& nrep) {
+  const size_t SZ = (size_t)2 * p.Lpad;
+  for (int c = c0; c >= a; --c) {
     const int64_t t_c = (int64_t)c * p.C;
-    const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
-    Bwd<JB, WP, BlockTeam<NW>> st;
-    st.load_state(p, p.b_first + (size_t)(c + 1) * SZ, j0);
+    const int64_t t_e = t_c + p.C;  // c <= M-2: a whole chunk with a successor
     st.save_state(p, p.b_in + (size_t)c * SZ, j0);
-    float vp0[JB], vp1[JB];
-    bwd_plain(tm, p, st, lds, j0, invz, t_e, vp0, vp1);
-    bwd_out<JB, WP, BlockTeam<NW>, 16 / JB, true>(tm, p, st, lds, j0, invz, t_c, t_e, vp0, vp1, true);
+    float vp0[J], vp1[J];
+    bwd_plain(p, st, j0, invz, t_e, vp0, vp1);
+    bwd_stream_out<J, WP, pf_relax_bwd<J>(), VEC, 1>(p, st, j0, invz, t_c, t_e, vp0, vp1, true);
+    ++nrep;
     float* bf = p.b_first + (size_t)c * SZ;
-    const float d = hilbert_reg<JB>(tm, st.b0, st.b1, bf, p.Lpad, j0);
-    changed = !(d <= p.tol);
-    __syncthreads();  // every wave has read bf before it is overwritten
+    const float d = hilbert_reg<J>(st.b0, st.b1, bf, p.Lpad, j0, p.alpha_in + t_c * 2 * (int64_t)p.L, p.L);
     st.save_state(p, bf, j0);
-    __threadfence();
-    __syncthreads();
-    ++repairs;
-    --c;
+    if (d <= p.tol && (c == a || !(flg && flg[c - 1]))) return false;
   }
-  if (threadIdx.x == 0) p.repairs[1] += repairs;
+  return true;
+}
+
+template <int J, int WP, bool VEC>
+__device__ void backward_relax(const FBParams& p, int j0, const float invz[J]) {
+  const size_t SZ = (size_t)2 * p.Lpad;
+  const int s = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  int nrep = 0, rounds = 0;
+  if (ctl_load(p.ctl, kCtlPending) > 0) {
+    const int a = s * p.G;
+    const int b = a + p.G < p.M ? a + p.G : p.M;
+    const int top = b < p.M - 1 ? b : p.M - 1;  // boundaries c <= M-2 have a successor
+    Bwd<J, WP> st;
+    bool changed = false;
+    const int c0 = find_flag<-1>(p.flags, a, top);
+    if (c0 >= 0) {
+      st.load_state(p, p.b_in + (size_t)c0 * SZ, j0);
+      changed = bwd_segment<J, WP, VEC>(p, st, c0, a, j0, invz, p.flags, nrep);
+    }
+    for (int k = 0;; ++k) {
+      if (changed) st.save_state(p, p.seg_end + ((size_t)(k & 1) * p.S + s) * SZ, j0);
+      relax_publish(p, k, s, changed);
+      ++rounds;
+      if (!relax_barrier(p.ctl, (k + 1) * p.S)) break;
+      if (ctl_load(p.ctl, kCtlChanged + k % 3) == 0) break;
+      changed = false;
+      if (s + 1 < p.S && p.seg_chg[(k & 1) * p.S + s + 1]) {
+        const float* X = p.seg_end + ((size_t)(k & 1) * p.S + s + 1) * SZ;
+        const float* w = p.alpha_in + (int64_t)b * p.C * 2 * (int64_t)p.L;
+        const float d = hilbert_dist(p.b_in + (size_t)(b - 1) * SZ, X, (int)SZ, w, p.L, p.Lpad);
+        if (!(d <= p.tol)) {
+          st.load_state(p, X, j0);
+          changed = bwd_segment<J, WP, VEC>(p, st, b - 1, a, j0, invz, nullptr, nrep);
+        }
+      }
+    }
+  }
+  if (lane == 0) {
+    if (nrep) atomicAdd(p.ctl + kCtlRepairs, nrep);
+    if (s == 0) p.ctl[kCtlRounds] = rounds;
+  }
+}
+
+template <int J, int WP>
+__global__ void __launch_bounds__(64) k_backward_relax(FBParams p) {
+  PMG_FB_LANE_SETUP
+  (void)lane;
+  if constexpr (J % 4 == 0) {
+    if ((p.L & 3) == 0) {
+      backward_relax<J, WP, true>(p, j0, invz);
+      return;
+    }
+  }
+  backward_relax<J, WP, false>(p, j0, invz);
 }
 
 typedef void (*fb_kernel_t)(FBParams);
 
 // the kernels of one (J, WP) instance (fb_inst_j*.hip)
 struct FBKernelSet {
-  fb_kernel_t forward, forward_fix, forward_repair;
-  fb_kernel_t backward, backward_full, backward_fix, backward_repair;
+  fb_kernel_t forward, forward_relax;
+  fb_kernel_t backward, backward_full, backward_relax;
 };
-
-bool fb_set_j1(int WP, FBKernelSet* k);
-bool fb_set_j2(int WP, FBKernelSet* k);
-bool fb_set_j4(int WP, FBKernelSet* k);
-bool fb_set_j8(int WP, FBKernelSet* k);
-bool fb_set_j16(int WP, FBKernelSet* k);
 
 template <int J, int WP>
 inline void fb_fill(FBKernelSet* k) {
   k->forward = k_forward<J, WP>;
-  k->forward_fix = k_forward_fix<J, WP>;
-  k->forward_repair = k_forward_repair<J, WP>;
+  k->forward_relax = k_forward_relax<J, WP>;
   k->backward = k_backward<J, WP>;
   k->backward_full = k_backward_full<J, WP>;
-  k->backward_fix = k_backward_fix<J, WP>;
-  k->backward_repair = k_backward_repair<J, WP>;
+  k->backward_relax = k_backward_relax<J, WP>;
 }
 
-// one instance file per J
-#define PMG_FB_INSTANCES(JJ)                          \
-  bool fb_set_j##JJ(int WP, FBKernelSet* k) {         \
-    switch (WP) {                                     \
-      case 5: fb_fill<JJ, 5>(k); return true;         \
-      case 9: fb_fill<JJ, 9>(k); return true;         \
-      case 13: fb_fill<JJ, 13>(k); return true;       \
-      case 17: fb_fill<JJ, 17>(k); return true;       \
-      case 25: fb_fill<JJ, 25>(k); return true;       \
-      case 32: fb_fill<JJ, 32>(k); return true;       \
-      default: return false;                          \
-    }                                                 \
-  }
+// one (J, WP) instance fb_set_j<J>_w<WP>, defined in the fb_inst_j*_w*.hip unit that lists it
+#define PMG_FB_WPS(X, JJ) X(JJ, 5) X(JJ, 9) X(JJ, 13) X(JJ, 17) X(JJ, 25) X(JJ, 32)
+#define PMG_FB_ALL(X) PMG_FB_WPS(X, 1) PMG_FB_WPS(X, 2) PMG_FB_WPS(X, 4) PMG_FB_WPS(X, 8) PMG_FB_WPS(X, 16)
+#define PMG_FB_DECL(JJ, WPP) void fb_set_j##JJ##_w##WPP(FBKernelSet* k);
+PMG_FB_ALL(PMG_FB_DECL)
+#define PMG_FB_INST(JJ, WPP) \
+  void fb_set_j##JJ##_w##WPP(FBKernelSet* k) { fb_fill<JJ, WPP>(k); }
 
 }  // namespace pmg

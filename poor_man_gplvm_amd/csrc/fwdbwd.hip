@@ -6,76 +6,85 @@
 namespace pmg {
 
 // boundary verification: flags[c] = hilbert(x[c], y[c + off]) > tol; a failing
-// boundary also snapshots y[c + off] into x[c] (the restart state of the repair).
+// boundary also snapshots y[c + off] into x[c] (the restart state of the relaxation)
+// and counts itself in *pending.
 // Backward (w != nullptr): both betas are weighted by alpha at the boundary time
 // t_e = (c+1) C, i.e. the POSTERIOR at t_e is compared.  An error of beta_{t_e}(j)
 // reaches gamma_t(i), t < t_e, only through the joint P(x_t = i, x_{t_e} = j) <=
 // gamma_{t_e}(j), so components with negligible posterior cannot move any output
 // above ~1e-18 probability, while they are exactly the ones the chain forgets slowly.
-// prev (nullable): the flags of the previous round.  A boundary that passed before can
-// only fail again if the chunk whose output it compares against (c + off) was
-// recomputed in that round, so every other boundary is skipped without a load.
 __global__ void __launch_bounds__(256) k_verify(float* __restrict__ x, const float* __restrict__ y,
                                                 int first, int last, int off, int SZ, float tol,
                                                 int* __restrict__ flags, const float* __restrict__ w,
-                                                int C, int L, int Lpad, const int* __restrict__ prev) {
+                                                int C, int L, int Lpad, int* __restrict__ pending) {
   const int wv = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int c = first + wv;
   if (c > last) return;
-  if (prev && prev[c + off] == 0) {
-    if ((threadIdx.x & 63) == 0) flags[c] = 0;
-    return;
-  }
   const float* yc = y + (size_t)(c + off) * SZ;
   float* xc = x + (size_t)c * SZ;
   const float* wc = w ? w + (size_t)(c + 1) * C * 2 * L : nullptr;
   const float d = hilbert_dist(xc, yc, SZ, wc, L, Lpad);
   const bool bad = !(d <= tol);
-  if ((threadIdx.x & 63) == 0) flags[c] = bad ? 1 : 0;
+  if ((threadIdx.x & 63) == 0) {
+    flags[c] = bad ? 1 : 0;
+    if (bad) atomicAdd(pending, 1);
+  }
   if (bad)
     for (int i = threadIdx.x & 63; i < SZ; i += 64) xc[i] = yc[i];
-}
-
-__global__ void k_sum_f64(const double* __restrict__ x, int n, double* __restrict__ out) {
-  __shared__ double sm[256];
-  double a = 0.0;
-  for (int i = threadIdx.x; i < n; i += 256) a += x[i];
-  sm[threadIdx.x] = a;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) sm[threadIdx.x] += sm[threadIdx.x + o];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) out[0] = sm[0];
 }
 
 // ---------------------------------------------------------------------------
 // host dispatch
 // ---------------------------------------------------------------------------
 struct FBWork {
+  int* ctl;       // control words: forward block at 0, backward at kCtlStride
   float *s_in, *s_out, *b_in, *b_first;
   double* chunk_logz;
   int* flags;
-  int* flags_b;   // the other verify round's flags (double-buffered)
-  int* repairs;
+  float* seg_end;  // [2][kRelaxMaxSeg][2*Lpad]
+  int* seg_chg;    // [2][kRelaxMaxSeg]
 };
 
-// workspace layout (the Python diagnostics mirror it): repairs[64] | s_in | s_out |
-// b_in | b_first (M x 2 x Lpad f32 each) | chunk_logz[M] | flags[M] | flags_b[M]
+// workspace layout (the Python diagnostics mirror it): ctl[64] | s_in | s_out | b_in |
+// b_first (M x 2 x Lpad f32 each) | chunk_logz[M] | flags[M] | seg_end | seg_chg
 static FBWork carve_fb(void* ws, int64_t T, int Lpad, int C, size_t* total = nullptr) {
   const int64_t M = (T + C - 1) / C;
   Carver c(ws);
   FBWork w;
-  w.repairs = c.take<int>(64);
+  w.ctl = c.take<int>(64);
   w.s_in = c.take<float>((size_t)M * 2 * Lpad);
   w.s_out = c.take<float>((size_t)M * 2 * Lpad);
   w.b_in = c.take<float>((size_t)M * 2 * Lpad);
   w.b_first = c.take<float>((size_t)M * 2 * Lpad);
   w.chunk_logz = c.take<double>(M);
   w.flags = c.take<int>(M);
-  w.flags_b = c.take<int>(M);
+  w.seg_end = c.take<float>((size_t)2 * kRelaxMaxSeg * 2 * Lpad);
+  w.seg_chg = c.take<int>(2 * kRelaxMaxSeg);
   if (total) *total = c.off + 256;
   return w;
+}
+
+// Relaxation segments: at most one single-wave workgroup per CU (so all are resident
+// whatever else the device runs: 64 threads, no LDS), G chunks each.
+static int device_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 64;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 64;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
+static void relax_shape(FBParams& p) {
+  int S = device_cus();
+  if (S > kRelaxMaxSeg) S = kRelaxMaxSeg;
+  if (S > p.M) S = p.M;
+  if (S < 1) S = 1;
+  p.G = (p.M + S - 1) / S;
+  p.S = (p.M + p.G - 1) / p.G;
 }
 
 static int pick_J(int L) {
@@ -97,18 +106,16 @@ static int pick_WP(int band) {
   return -1;
 }
 
-static int repair_nw_rt(int J) { return J >= 8 ? 8 : J; }
-
-// kernel sets are instantiated per latents-per-lane J in fb_inst_j*.hip (parallel builds)
+// kernel sets are instantiated per (J, WP) in fb_inst_j*_w*.hip (parallel builds)
 static bool fb_set(int J, int WP, FBKernelSet* k) {
-  switch (J) {
-    case 1: return fb_set_j1(WP, k);
-    case 2: return fb_set_j2(WP, k);
-    case 4: return fb_set_j4(WP, k);
-    case 8: return fb_set_j8(WP, k);
-    case 16: return fb_set_j16(WP, k);
-    default: return false;
+#define PMG_FB_CASE(JJ, WPP)      \
+  if (J == JJ && WP == WPP) {     \
+    fb_set_j##JJ##_w##WPP(k);     \
+    return true;                  \
   }
+  PMG_FB_ALL(PMG_FB_CASE)
+#undef PMG_FB_CASE
+  return false;
 }
 
 static int fill_params(FBParams& p, const pmg_transition* tr, int64_t T, int C, int B,
@@ -157,7 +164,7 @@ size_t pmg_fwdbwd_workspace_size(int64_t T, int32_t L, int32_t chunk) {
 
 size_t pmg_fwdbwd_repair_counter_offset(int64_t T, int32_t L, int32_t chunk) {
   (void)T; (void)L; (void)chunk;
-  return 0;  // repairs[0] (forward), repairs[1] (backward) at the workspace start
+  return 0;  // int32 control blocks at the workspace start: forward words 0.., backward kCtlStride..
 }
 
 int32_t pmg_fwdbwd_lpad(int32_t L) {
@@ -182,7 +189,7 @@ float* pmg_fwdbwd_state(void* workspace, int64_t T, int32_t L, int32_t chunk, in
   return base + (size_t)c * 2 * (64 * J);
 }
 
-// phase: 1 = speculative chunk-parallel pass, 2 = verify / repair / logZ, 3 = both
+// phase: 1 = speculative chunk-parallel pass, 2 = verify / relaxation / logZ, 3 = both
 static int forward_impl(const float* delta, const float* phi, const double* m, int64_t T,
                         const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                         int32_t warmup, double tol, float* alpha, double* logc, double* logz,
@@ -200,44 +207,35 @@ static int forward_impl(const float* delta, const float* phi, const double* m, i
   p.m = m;
   p.alpha = alpha;
   p.logc = logc;
+  p.logz = logz;
   p.chunk_logz = w.chunk_logz;
   p.s_in = w.s_in;
   p.s_out = w.s_out;
   p.flags = w.flags;
-  p.repairs = w.repairs;
+  p.ctl = w.ctl;
+  p.seg_end = w.seg_end;
+  p.seg_chg = w.seg_chg;
+  relax_shape(p);
   const int J = p.Lpad / 64, WP = pick_WP(tr->band);
   FBKernelSet ks;
   const bool have = fb_set(J, WP, &ks);
-  fb_kernel_t kf = have ? ks.forward : nullptr, kfix = have ? ks.forward_fix : nullptr,
-              kr = have ? ks.forward_repair : nullptr;
-  PMG_REQUIRE(kf && kfix && kr, "pmg_forward_filter: no kernel for J=%d WP=%d", J, WP);
+  PMG_REQUIRE(have && ks.forward && ks.forward_relax, "pmg_forward_filter: no kernel for J=%d WP=%d", J, WP);
   if (phase & 1) {
-    PMG_HIP(hipMemsetAsync(w.repairs, 0, sizeof(int), st));
-    hipLaunchKernelGGL(kf, dim3(p.M), dim3(64), 0, st, p);
+    PMG_HIP(hipMemsetAsync(p.ctl, 0, 4 * sizeof(int), st));  // repairs, rounds, timeout
+    hipLaunchKernelGGL(ks.forward, dim3(p.M), dim3(64), 0, st, p);
     PMG_LAUNCH_CHECK();
   }
   if (phase & 2) {
+    PMG_HIP(hipMemsetAsync(p.ctl + kCtlPending, 0, kCtlPhase2Words * sizeof(int), st));
     if (p.M > 1) {
+      // PMG_DEBUG_NO_REPAIR (diagnostics): verify only, count nothing, repair nothing
+      int* pend = getenv("PMG_DEBUG_NO_REPAIR") ? p.ctl + kCtlStride - 1 : p.ctl + kCtlPending;
       const int nver = p.M - 1;
-      const bool no_repair = getenv("PMG_DEBUG_NO_REPAIR") != nullptr;
-      for (int round = 0; round <= kFixRounds; ++round) {
-        int* cur = (round & 1) ? w.flags_b : w.flags;
-        const int* prev = round == 0 ? nullptr : ((round & 1) ? w.flags : w.flags_b);
-        p.flags = cur;
-        hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4), dim3(256), 0, st, w.s_in,
-                           (const float*)w.s_out, 1, p.M - 1, -1, 2 * p.Lpad, p.tol, cur,
-                           (const float*)nullptr, 0, 0, 0, prev);
-        PMG_LAUNCH_CHECK();
-        if (no_repair) break;
-        if (round < kFixRounds) {
-          hipLaunchKernelGGL(kfix, dim3(p.M), dim3(64), 0, st, p);
-        } else {
-          hipLaunchKernelGGL(kr, dim3(1), dim3(64 * repair_nw_rt(J)), 0, st, p);
-        }
-        PMG_LAUNCH_CHECK();
-      }
+      hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4), dim3(256), 0, st, w.s_in, (const float*)w.s_out, 1,
+                         p.M - 1, -1, 2 * p.Lpad, p.tol, w.flags, (const float*)nullptr, 0, 0, 0, pend);
+      PMG_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(k_sum_f64, dim3(1), dim3(256), 0, st, (const double*)w.chunk_logz, p.M, logz);
+    hipLaunchKernelGGL(ks.forward_relax, dim3(p.S), dim3(64), 0, st, p);  // also sums logZ
     PMG_LAUNCH_CHECK();
   }
   return PMG_OK;
@@ -281,37 +279,29 @@ static int backward_impl(const float* delta, const float* phi, const float* alph
   p.b_in = w.b_in;
   p.b_first = w.b_first;
   p.flags = w.flags;
-  p.repairs = w.repairs;
+  p.ctl = w.ctl + kCtlStride;
+  p.seg_end = w.seg_end;
+  p.seg_chg = w.seg_chg;
+  relax_shape(p);
   const int J = p.Lpad / 64, WP = pick_WP(tr->band);
   FBKernelSet ks;
   const bool have = fb_set(J, WP, &ks);
-  fb_kernel_t kb = !have ? nullptr : (rho || gamma || !P) ? ks.backward_full : ks.backward,
-              kfix = have ? ks.backward_fix : nullptr, kr = have ? ks.backward_repair : nullptr;
-  PMG_REQUIRE(kb && kfix && kr, "pmg_backward_smoother: no kernel for J=%d WP=%d", J, WP);
+  fb_kernel_t kb = !have ? nullptr : (rho || gamma || !P) ? ks.backward_full : ks.backward;
+  PMG_REQUIRE(kb && ks.backward_relax, "pmg_backward_smoother: no kernel for J=%d WP=%d", J, WP);
   if (phase & 1) {
-    PMG_HIP(hipMemsetAsync(w.repairs + 1, 0, sizeof(int), st));
+    PMG_HIP(hipMemsetAsync(p.ctl, 0, 4 * sizeof(int), st));
     hipLaunchKernelGGL(kb, dim3(p.M), dim3(64), 0, st, p);
     PMG_LAUNCH_CHECK();
   }
   if ((phase & 2) && p.M > 1) {
+    PMG_HIP(hipMemsetAsync(p.ctl + kCtlPending, 0, kCtlPhase2Words * sizeof(int), st));
+    int* pend = getenv("PMG_DEBUG_NO_REPAIR") ? p.ctl + kCtlStride - 1 : p.ctl + kCtlPending;
     const int nver = p.M - 1;
-    const bool no_repair = getenv("PMG_DEBUG_NO_REPAIR") != nullptr;
-    for (int round = 0; round <= kFixRounds; ++round) {
-      int* cur = (round & 1) ? w.flags_b : w.flags;
-      const int* prev = round == 0 ? nullptr : ((round & 1) ? w.flags : w.flags_b);
-      p.flags = cur;
-      hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4), dim3(256), 0, st, w.b_in,
-                         (const float*)w.b_first, 0, p.M - 2, 1, 2 * p.Lpad, p.tol, cur,
-                         alpha, p.C, p.L, p.Lpad, prev);
-      PMG_LAUNCH_CHECK();
-      if (no_repair) break;
-      if (round < kFixRounds) {
-        hipLaunchKernelGGL(kfix, dim3(p.M), dim3(64), 0, st, p);
-      } else {
-        hipLaunchKernelGGL(kr, dim3(1), dim3(64 * repair_nw_rt(J)), 0, st, p);
-      }
-      PMG_LAUNCH_CHECK();
-    }
+    hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4), dim3(256), 0, st, w.b_in, (const float*)w.b_first, 0,
+                       p.M - 2, 1, 2 * p.Lpad, p.tol, w.flags, alpha, p.C, p.L, p.Lpad, pend);
+    PMG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(ks.backward_relax, dim3(p.S), dim3(64), 0, st, p);
+    PMG_LAUNCH_CHECK();
   }
   return PMG_OK;
 }

@@ -50,10 +50,20 @@ class AdamConfig:
 class ScanConfig:
     """Time-parallel scan parameters (see fwdbwd.hip)."""
     chunk: int | None = None     # time steps per chunk (None: ~2048 chunks)
-    warmup: int = 64             # forgetting warm-up before each chunk (initial value)
-    tol: float = 1e-6            # Hilbert-metric boundary tolerance
-    adaptive: bool = True        # per pass: double the warm-up when >1% of chunks needed
-                                 # repair, halve it after two E-steps with <=0.1%
+    warmup: int = 48             # forgetting warm-up before each chunk (initial value)
+    tol: float = 3e-6            # Hilbert-metric boundary tolerance.  A posterior's relative
+                                 # error is bounded by the forward + backward boundary
+                                 # distances, so 2 x tol stays inside the 1e-5 parity bar.
+                                 # In slowly mixing regimes (the flat tuning of the first EM
+                                 # iterations) two f32 chains of one filter settle 1.4e-6
+                                 # (median) to 7.6e-6 (q99) apart and never coalesce bitwise
+                                 # (profiles/r02_diag_cascade_c3.log); boundaries that fail on
+                                 # that noise alone cost a short relaxation, not a rescan of T
+    adaptive: bool = False       # per pass: double the warm-up when >1% of chunks needed
+                                 # repair, halve it after two E-steps with <=0.1%.  Off by
+                                 # default: the relaxation kernel absorbs the cascades of the
+                                 # first EM iterations, and a doubled warm-up taxes every
+                                 # later main pass (C3: 0.19 -> 0.36 ms forward at 192 steps)
     max_warmup: int = 1024
     min_warmup: int = 16
     chunk_bwd: int | None = None  # backward chunk (None: = chunk if set, else 2x the default)
@@ -219,7 +229,7 @@ class DeviceEM:
         self.ws_ad = None
         self.warm = [int(self.scan.warmup), int(self.scan.warmup)]   # forward, backward
         self._clean = [0, 0]
-        self._rep_host = torch.zeros(2, dtype=torch.int32).pin_memory()
+        self._rep_host = torch.zeros(nat.CTL_WORDS, dtype=torch.int32).pin_memory()
         self._rep_evt = None
         self.timer = None       # optional KernelTimer (bench): per-call HIP events
         self._tr = None
@@ -387,7 +397,8 @@ class DeviceEM:
         if not self.scan.adaptive or self._rep_evt is None or not self._rep_evt.query():
             return
         Ms = ((self.T + self.C - 1) // self.C, (self.T + self.Cb - 1) // self.Cb)
-        for i, r in enumerate(int(v) for v in self._rep_host.tolist()):
+        ctl = self._rep_host.tolist()
+        for i, r in enumerate((ctl[nat.CTL_FWD + nat.CTL_REPAIRS], ctl[nat.CTL_BWD + nat.CTL_REPAIRS])):
             M = Ms[i]
             if r > max(1, M // 100):
                 self.warm[i] = min(self.scan.max_warmup, 2 * self.warm[i])
@@ -401,8 +412,12 @@ class DeviceEM:
                 self._clean[i] = 0
         self._rep_evt = None
 
+    def ctl_words(self):
+        """The scans' int32 control words (device view; see fb_kernels.h kCtl*)."""
+        return self.ws_fb[:4 * nat.CTL_WORDS].view(torch.int32)
+
     def _snapshot_repairs(self):
-        self._rep_host.copy_(self.ws_fb[:8].view(torch.int32), non_blocking=True)
+        self._rep_host.copy_(self.ctl_words(), non_blocking=True)
         self._rep_evt = torch.cuda.Event()
         self._rep_evt.record()
 
@@ -415,7 +430,7 @@ class DeviceEM:
                 nat.stream_handle())
         with self._t('forward_filter'):          # main chunk-parallel pass (k_forward)
             nat.check(self.lib.pmg_forward_filter_phase(*args, 1), "pmg_forward_filter")
-        with self._t('forward_repair'):          # verify / repair rounds / logZ
+        with self._t('forward_repair'):          # verify / relaxation / logZ
             nat.check(self.lib.pmg_forward_filter_phase(*args, 2), "pmg_forward_filter")
 
     def backward(self, likelihood_scale, P=True, gamma=None, rho=None):
@@ -426,7 +441,7 @@ class DeviceEM:
                 self.ws_fb.numel(), nat.stream_handle())
         with self._t('backward_smoother'):       # main chunk-parallel pass (k_backward)
             nat.check(self.lib.pmg_backward_smoother_phase(*args, 1), "pmg_backward_smoother")
-        with self._t('backward_repair'):         # verify / repair rounds
+        with self._t('backward_repair'):         # verify / relaxation
             nat.check(self.lib.pmg_backward_smoother_phase(*args, 2), "pmg_backward_smoother")
 
     def e_step(self, likelihood_scale, logz_out, gamma=None, rho=None):
@@ -436,9 +451,17 @@ class DeviceEM:
         self._snapshot_repairs()
 
     def repairs(self):
-        """(forward, backward) chunks repaired by the last scans (device read: syncs)."""
-        r = self.ws_fb[:8].view(torch.int32).cpu().numpy()
-        return int(r[0]), int(r[1])
+        """(forward, backward) chunks recomputed by the last scans' relaxation (device
+        read: syncs).  Raises if a relaxation kernel's bounded grid barrier timed out."""
+        r = self.ctl_words().cpu().numpy()
+        if r[nat.CTL_FWD + nat.CTL_ERR] or r[nat.CTL_BWD + nat.CTL_ERR]:
+            raise nat.NativeError("scan relaxation: grid barrier timed out (results invalid)")
+        return int(r[nat.CTL_FWD + nat.CTL_REPAIRS]), int(r[nat.CTL_BWD + nat.CTL_REPAIRS])
+
+    def relax_rounds(self):
+        """(forward, backward) relaxation rounds of the last scans (device read: syncs)."""
+        r = self.ctl_words().cpu().numpy()
+        return int(r[nat.CTL_FWD + nat.CTL_ROUNDS]), int(r[nat.CTL_BWD + nat.CTL_ROUNDS])
 
     def loglik(self):
         ll = torch.empty((self.T, self.L), dtype=torch.float32, device=self.dev)

@@ -280,7 +280,9 @@ class ShardEM(DeviceEM):
             nat.check(self.lib.pmg_backward_smoother_phase(*args, 2), "pmg_backward_smoother")
 
     def repair_count(self):
-        return self.ws_fb[:8].view(torch.int32).clone()
+        """(forward, backward) chunk-recompute counters (device tensor)."""
+        w = self.ctl_words()
+        return torch.stack([w[nat.CTL_FWD + nat.CTL_REPAIRS], w[nat.CTL_BWD + nat.CTL_REPAIRS]])
 
     def own_logz(self, out):
         torch.sum(self.logc[self.own], dim=0, keepdim=True, out=out)

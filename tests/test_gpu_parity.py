@@ -102,8 +102,8 @@ SCAN_CASES = [
     (20, 64, 1, 1.0, 0.01, 0.01, None, 64, 1.0),        # T = 1
     (20, 64, 2, 1.0, 0.2, 0.3, None, 64, 1.0),          # T = 2
     (24, 300, 700, 1.0, 0.01, 0.01, 100, 16, 1.0),      # L between 256 and 512
-    (30, 512, 1200, 1.0, 0.01, 0.01, 16, 0, 1.0),       # sequential repair, 8-wave team
-    (16, 1024, 300, 1.0, 0.01, 0.01, 16, 0, 1.0),       # sequential repair, 2 latents/thread
+    (30, 512, 1200, 1.0, 0.01, 0.01, 16, 0, 1.0),       # every boundary relaxed, 8 latents/lane
+    (16, 1024, 300, 1.0, 0.01, 0.01, 16, 0, 1.0),       # every boundary relaxed, 16 latents/lane
     (40, 512, 3000, 1.0, 0.01, 0.01, 64, 64, 1.0),      # C3 lane layout (8 latents/lane), chunk-parallel
     (40, 1024, 1500, 1.0, 0.01, 0.01, 64, 64, 1.0),     # 16 latents/lane, chunk-parallel
     (40, 512, 2000, 3.0, 0.01, 0.01, 50, 48, 1.0),      # band 25 at 8 latents/lane (4 halo lanes)
@@ -121,8 +121,9 @@ def test_forward_backward_vs_oracle(case):
     rho = torch.zeros((T, 2, L), dtype=torch.float32, device='cuda')
     eng.e_step(s, logz, gamma=gamma, rho=rho)
     K, logK, A, logA = O.create_transition_prob_1d(L, mv, pmj, pjm)
+    want_joint = 1 < T and L <= 512        # the f64 (2,2,L,L) joint costs minutes at L = 1024
     lpa, lz, lca, cs, lj, _ = O.smooth_all_step_combined_ma_chunk(
-        d['y'], d['tuning'], logK, logA, likelihood_scale=s, with_joint=True)
+        d['y'], d['tuning'], logK, logA, likelihood_scale=s, with_joint=want_joint)
     post = np.exp(lpa)
     g = gamma.cpu().numpy()
     close_prob(g, post)
@@ -132,16 +133,16 @@ def test_forward_backward_vs_oracle(case):
     close_prob(eng.alpha.cpu().numpy(), np.exp(lca))
     assert abs(logz.item() - lz) <= 1e-7 * abs(lz)
     np.testing.assert_allclose(eng.logc.cpu().numpy(), cs, rtol=1e-6, atol=1e-5)
-    if 1 < T and L <= 512:
+    if want_joint:
         S = eng.joint(rho).cpu().numpy().reshape(2, L, 2, L).transpose(0, 2, 1, 3)
         J = np.exp(logA)[:, :, None, None] * K[None] * S
         np.testing.assert_allclose(J, np.exp(lj), rtol=1e-4, atol=1e-5 * max(1.0, np.exp(lj).max()))
 
 
 def test_flat_tuning_cascade():
-    """Nearly flat tuning (the first EM iteration after a random init): the chain does
-    not forget within any warm-up, every chunk boundary fails and the sequential
-    multi-wave repair recomputes the whole sequence; results must still match."""
+    """Nearly flat tuning (the first EM iteration after a random init): the chain
+    forgets slowly, every chunk boundary fails and the relaxation kernel recomputes
+    whole segments over several rounds; results must still match."""
     N, L, T = 24, 256, 3000
     d = make(N, L, T)
     rng = np.random.default_rng(11)
