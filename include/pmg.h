@@ -211,6 +211,45 @@ int32_t pmg_fwdbwd_lpad(int32_t L);
 float* pmg_fwdbwd_state(void* workspace, int64_t T, int32_t L, int32_t chunk, int32_t which, int64_t c);
 
 /* ------------------------------------------------------------------ */
+/* Dense log-domain scans: any continuous kernel (custom_transition_kernel,  */
+/* gp_kernel.py:30-34 and 61-66; RBF kernels wider than PMG_MAX_BAND; the     */
+/* latent-only model of decoder_latentonly.py:33-224 with A = [[1,0],[1,0]]). */
+/* The reference's own log-space recursion (decoder.py:151-226):               */
+/*   prior[0,j] = LSE_i(LSE_d(post[d,i] + logA[d,0]) + logK0[i,j]),            */
+/*   prior[1,j] = LSE_i(LSE_d(post[d,i] + logA[d,1])) - log L,                  */
+/* with the chunk parallelism, boundary verification (Hilbert metric in log    */
+/* space) and relaxation of the banded scans.  Emission input as              */
+/* pmg_forward_filter (delta, phi, m).                                         */
+typedef struct pmg_dense_transition {
+  int32_t L;
+  const float* logK;    /* (L, L) DEVICE f32 log continuous kernel [i_prev][j_next] */
+  const float* logKT;   /* (L, L) DEVICE f32 its transpose [j_next][i_prev]          */
+  const float* logK_lo; /* (L, L) DEVICE f32 residual logK0 - logK (0 where -inf):   */
+  const float* logKT_lo;/*   hi + lo keeps far weights (-2500) to ~1e-10; transpose  */
+  float logA[4];        /* host values logA00 logA01 logA10 logA11 (-inf allowed)    */
+} pmg_dense_transition;
+size_t pmg_dense_workspace_size(int64_t T, int32_t L, int32_t chunk);
+/* outputs: log_alpha (T,2,L) f32 log filter posteriors (required: the backward */
+/* pass reads it); alpha (T,2,L) f32 = exp(log_alpha) (may be NULL); logc, logz */
+/* as pmg_forward_filter.                                                       */
+int pmg_dense_forward(const float* delta, const float* phi, const double* m, int64_t T,
+                      const pmg_dense_transition* tr, double likelihood_scale, int32_t chunk, int32_t warmup,
+                      double tol, float* alpha, float* log_alpha, double* logc, double* logz, void* workspace,
+                      size_t workspace_bytes, void* stream);
+/* outputs (each may be NULL): P (T,L), gamma (T,2,L), log_gamma (T,2,L) (exact   */
+/* log posteriors, the reference's log_acausal_posterior_all), rho (T,2,L) as      */
+/* pmg_backward_smoother, log_rho (T,2,L) = log(rho) (no overflow).                */
+int pmg_dense_backward(const float* delta, const float* phi, const float* log_alpha, int64_t T,
+                       const pmg_dense_transition* tr, double likelihood_scale, int32_t chunk, int32_t warmup,
+                       double tol, float* P, float* gamma, float* log_gamma, float* rho, float* log_rho,
+                       void* workspace, size_t workspace_bytes, void* stream);
+/* Pairwise joint in log space (decode, dense scans): logS (2L x 2L) f64 =           */
+/* LSE_{t<T-1} log_alpha_t[x] + log_rho_{t+1}[x'], x = (d,i); the caller forms the   */
+/* log joint logA[d,d'] + logK[d',i,j] + logS (decoder.py:215-221).                  */
+int pmg_joint_log_accumulate(const float* log_alpha, const float* log_rho, int64_t T, int32_t L, double* logS,
+                             void* stream);
+
+/* ------------------------------------------------------------------ */
 /* Sufficient statistics -- fit_tuning_helper.get_statistics             */
 /* (fit_tuning_helper.py:28-42): y_w = P^T y (L,N), t_w = sum_t P (L).    */
 /* P (T,L) f32 probabilities; yext from pmg_spikes_prepare.  fp32 MFMA    */

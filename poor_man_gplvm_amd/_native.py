@@ -39,6 +39,7 @@ EXPORTED_SYMBOLS = (
     "pmg_mstep_tiled_workspace_size", "pmg_mstep_adam_tiled",
     "pmg_emission_poisson_dt", "pmg_naive_bayes_normalize",
     "pmg_tuning_linear", "pmg_emission_gaussian", "pmg_gaussian_mstep_workspace_size", "pmg_gaussian_mstep",
+    "pmg_dense_workspace_size", "pmg_dense_forward", "pmg_dense_backward", "pmg_joint_log_accumulate",
 )
 
 
@@ -51,6 +52,12 @@ class Transition(ctypes.Structure):
     _fields_ = [("L", ctypes.c_int32), ("band", ctypes.c_int32),
                 ("g", ctypes.c_float * (PMG_MAX_BAND + 1)), ("invz", ctypes.c_void_p),
                 ("A", ctypes.c_float * 4)]
+
+
+class DenseTransition(ctypes.Structure):
+    """pmg_dense_transition (include/pmg.h)."""
+    _fields_ = [("L", ctypes.c_int32), ("logK", ctypes.c_void_p), ("logKT", ctypes.c_void_p),
+                ("logK_lo", ctypes.c_void_p), ("logKT_lo", ctypes.c_void_p), ("logA", ctypes.c_float * 4)]
 
 
 class AdamCfg(ctypes.Structure):
@@ -112,6 +119,12 @@ _SIGS = {
     "pmg_gaussian_mstep": ([_P, _P, _P, _I32, _I32, _I32, ctypes.c_double, ctypes.c_double, _P, _P, _P, _SZ,
                             _P], _I32),
     "pmg_joint_workspace_size": ([_I64, _I32], _SZ),
+    "pmg_dense_workspace_size": ([_I64, _I32, _I32], _SZ),
+    "pmg_dense_forward": ([_P, _P, _P, _I64, ctypes.POINTER(DenseTransition), _D, _I32, _I32, _D,
+                           _P, _P, _P, _P, _P, _SZ, _P], _I32),
+    "pmg_dense_backward": ([_P, _P, _P, _I64, ctypes.POINTER(DenseTransition), _D, _I32, _I32, _D,
+                            _P, _P, _P, _P, _P, _P, _SZ, _P], _I32),
+    "pmg_joint_log_accumulate": ([_P, _P, _I64, _I32, _P, _P], _I32),
     "pmg_joint_accumulate": ([_P, _P, _I64, _I32, _P, _P, _SZ, _P], _I32),
 }
 

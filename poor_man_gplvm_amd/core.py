@@ -25,7 +25,8 @@ import torch
 
 from . import _native as nat
 from .engine import AdamConfig, DeviceEM, ScanConfig, SpikeData, default_device, log_of
-from .gp_kernel import banded_transition, create_transition_prob_1d, generate_basis
+from .gp_kernel import (DenseTransition, banded_transition, create_transition_prob_1d, dense_transition,
+                        generate_basis, make_transition, transition_from_log_kernels)
 
 try:  # optional, as in the reference's TsdFrame handling
     import pynapple as nap  # type: ignore
@@ -132,8 +133,11 @@ class PoissonGPLVMJump1D:
 
     # ------------------------------------------------------------------ transitions
     def _transition(self, movement_variance, p_move_to_jump, p_jump_to_move):
-        return banded_transition(self.n_latent_bin, movement_variance, p_move_to_jump, p_jump_to_move,
-                                 custom_kernel=self.custom_transition_kernel)
+        """gp_kernel.py:42-89 in device form: the banded linear-space scans when the
+        continuous kernel is a <= 32-bin RBF band, else the dense log-domain scans
+        (custom_transition_kernel, wide movement_variance)."""
+        return make_transition(self.n_latent_bin, movement_variance, p_move_to_jump, p_jump_to_move,
+                               custom_kernel=self.custom_transition_kernel)
 
     # ------------------------------------------------------------------ M-step
     def m_step(self, param_curr, y, log_posterior_curr, tuning_basis, hyperparam, opt_state_curr=None):
@@ -171,9 +175,9 @@ class PoissonGPLVMJump1D:
                        log_dynamics_transition_kernel, ma_neuron, ma_latent=None, likelihood_scale=1.,
                        n_time_per_chunk=10000):
         """core.py:777-786 -> decoder.smooth_all_step_combined_ma_chunk (decoder.py:258-332).
-        The transition is rebuilt in banded form from this model's hyper-parameters
-        (hyperparam overrides); the passed log kernels are used only for the joint's
-        log-space outputs.  Returns the reference's 6-tuple (numpy)."""
+        The scan runs with the log kernels passed in (their device form, see
+        _scan_transition) and the joint's log-space outputs are assembled from them.
+        Returns the reference's 6-tuple (numpy)."""
         res = self._run_decode(y, tuning, hyperparam, ma_neuron, ma_latent, likelihood_scale, joint=True,
                                logK=log_latent_transition_kernel_l, logA=log_dynamics_transition_kernel)
         return (res['log_posterior_all'], res['log_marginal_final'], res['log_causal_posterior_all'],
@@ -186,6 +190,26 @@ class PoissonGPLVMJump1D:
     def _observation(self, eng, hyperparam):
         """Hook: the Gaussian model switches the engine's emission here."""
 
+    def _scan_transition(self, mv, pmj, pjm, logK=None, logA=None):
+        """Device transition for a scan: this model's own (hyper-parameters), or, when
+        log kernels are passed (the _decode_latent arguments), the device form of
+        exactly those kernels.  Kernels equal to the model's own (1e-6) keep its
+        transition bit for bit."""
+        tr = self._transition(mv, pmj, pjm)
+        if logK is None or logA is None:
+            return tr
+        lk = np.asarray(logK, np.float64)
+        la = np.asarray(logA, np.float64)
+        L = self.n_latent_bin
+        if lk.shape == (2, L, L) and la.shape == (2, 2):
+            _, lk_m, _, la_m = create_transition_prob_1d(L, mv, pmj, pjm, self.custom_transition_kernel)
+            with np.errstate(invalid='ignore'):
+                same = (np.allclose(np.exp(lk), np.exp(lk_m), rtol=1e-6, atol=1e-300)
+                        and np.allclose(np.exp(la), np.exp(la_m), rtol=1e-6, atol=1e-12))
+            if same:
+                return tr
+        return transition_from_log_kernels(lk, la, force_dense=isinstance(tr, DenseTransition))
+
     def _run_decode(self, y, tuning, hyperparam, ma_neuron, ma_latent, likelihood_scale, joint=True,
                     logK=None, logA=None):
         mv = hyperparam.get('movement_variance', self.movement_variance)
@@ -193,7 +217,7 @@ class PoissonGPLVMJump1D:
         pjm = hyperparam.get('p_jump_to_move', self.p_jump_to_move)
         y = np.asarray(y)
         ma = None if ma_neuron is None else np.asarray(ma_neuron, np.float32)
-        tr = self._transition(mv, pmj, pjm)
+        tr = self._scan_transition(mv, pmj, pjm, logK, logA)
         self._check_latent_mask(tr, ma_latent)
         sp = SpikeData(y, ma)
         eng = DeviceEM(sp, self.n_latent_bin, scan=self.scan_config)
@@ -206,24 +230,35 @@ class PoissonGPLVMJump1D:
         logz = torch.zeros(1, dtype=torch.float64, device=dev)
         gamma = torch.empty((T, 2, L), dtype=torch.float32, device=dev)
         rho = torch.zeros((T, 2, L), dtype=torch.float32, device=dev) if joint else None
-        eng.e_step(likelihood_scale, logz, gamma=gamma, rho=rho)
+        lgam = torch.empty((T, 2, L), dtype=torch.float32, device=dev) if eng.dense else None
+        eng.e_step(likelihood_scale, logz, gamma=gamma, rho=rho, log_gamma=lgam)
         ml = None if ma_latent is None else np.asarray(ma_latent).astype(bool)
+        if eng.dense:     # the log-domain scans hold the exact log posteriors
+            log_post, log_causal = _np(lgam), _np(eng.log_alpha)
+        else:
+            log_post, log_causal = _np(log_of(gamma)), _np(log_of(eng.alpha))
         out = {
-            'log_posterior_all': _masked_log(_np(log_of(gamma)), ml),
+            'log_posterior_all': _masked_log(log_post, ml),
             'log_marginal_final': float(_np(logz)[0]),
             'posterior_all': _np(gamma),
-            'log_causal_posterior_all': _masked_log(_np(log_of(eng.alpha)), ml),
+            'log_causal_posterior_all': _masked_log(log_causal, ml),
             'log_one_step_predictive_marginals_all': _np(eng.logc).astype(np.float32),
             'log_likelihood_all': _np(eng.loglik()),
         }
         if joint:
-            S = _np(eng.joint(rho))  # (2L, 2L) f64
             if logK is None or logA is None:
                 _, logK, _, logA = create_transition_prob_1d(L, mv, pmj, pjm, self.custom_transition_kernel)
             logK = np.asarray(logK, np.float64)
             logA = np.asarray(logA, np.float64)
-            S4 = S.reshape(2, L, 2, L).transpose(0, 2, 1, 3)          # [d, d', i, j]
-            lj = log_joint_from_counts(S4, logK, logA, ml)
+            if eng.dense:   # rho holds log(rho): the joint is accumulated in log space
+                logS4 = _np(eng.joint_log(rho)).reshape(2, L, 2, L).transpose(0, 2, 1, 3)
+                with np.errstate(invalid='ignore'):
+                    lj = np.asarray(logA, np.float64)[:, :, None, None] + logK[None] + logS4
+                lj = np.where(np.isnan(lj), -np.inf, lj)
+            else:
+                S = _np(eng.joint(rho))  # (2L, 2L) f64
+                S4 = S.reshape(2, L, 2, L).transpose(0, 2, 1, 3)          # [d, d', i, j]
+                lj = log_joint_from_counts(S4, logK, logA, ml)
             out['log_accumulated_joint'] = lj
         return out
 
@@ -466,13 +501,24 @@ class PoissonGPLVMJump1D:
         self.__dict__.update(state)
 
 
+# Floor of the linear joint count S: pairs (x, x') whose every alpha_t[x] rho_{t+1}[x']
+# product underflowed fp32 (states the posterior never visits) get log S = log(1e-300)
+# instead of -inf.  The reference's log-domain accumulation (decoder.py:215-221) keeps a
+# finite, very negative value there; the floor keeps log_joint_* finite, and a row with
+# no mass at all normalises to the prior transition A[d,d'] K[d',i,:] (its reference
+# value when the smoothed ratio is flat) instead of NaN.  Probability-space outputs
+# differ from the reference by < 1e-290 there.
+JOINT_COUNT_FLOOR = 1e-300
+
+
 def log_joint_from_counts(S4, logK, logA, ml=None):
     """log accumulated joint [d, d', i, j] = logA + logK + log S, where S = sum_t
     alpha_t (x) rho_{t+1} is the device's linear-space joint count (decoder.py:215-221
-    accumulates the same quantity with logaddexp)."""
+    accumulates the same quantity with logaddexp).  Never -inf / NaN (see
+    JOINT_COUNT_FLOOR); masked latents keep the reference's -1e20 sentinel sums."""
     S4 = np.asarray(S4, np.float64)
-    with np.errstate(divide='ignore'):
-        logS = np.log(np.maximum(S4, 0.0))
+    zero = ~(S4 > JOINT_COUNT_FLOOR)
+    logS = np.log(np.where(zero, JOINT_COUNT_FLOOR, S4))
     if ml is not None and not ml.all():
         # decoder.py:215 in log space carries ll = -1e20 (core.py:59-60) into every
         # joint entry that starts or ends in a masked latent; those entries are exact
@@ -480,7 +526,7 @@ def log_joint_from_counts(S4, logK, logA, ml=None):
         # match the reference's arithmetic.
         nm = (~ml).astype(np.float64)
         sent = -1e20 * (nm[:, None] + nm[None, :])
-        logS = np.where((S4 == 0.0) & (sent < 0.0), sent[None, None], logS)
+        logS = np.where(zero & (sent < 0.0), sent[None, None], logS)
     return np.asarray(logA, np.float64)[:, :, None, None] + np.asarray(logK, np.float64)[None] + logS
 
 
@@ -549,6 +595,10 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
     eh = torch.zeros((n_iter, mi), dtype=torch.float64, device=dev)
     logz = torch.zeros(max(n_iter, 1), dtype=torch.float64, device=dev)
     gamma = torch.empty((T, 2, L), dtype=torch.float32, device=dev)
+    lgam = torch.empty((T, 2, L), dtype=torch.float32, device=dev) if eng.dense else None
+
+    def log_post():
+        return _masked_log(_np(lgam) if eng.dense else _np(log_of(gamma)), mlat)
     saved = {'log_posterior_all_saved': [], 'params_saved': [], 'tuning_saved': [], 'iter_saved': [],
              'log_marginal_saved': []}
     saved_idx = []
@@ -558,9 +608,10 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
         eng.m_step(W, mu, nu, cnt, adam, stats[i], lh[i], eh[i])
         eng.compute_tuning(W)
         want_gamma = (i == n_iter - 1) or (i % save_every == 0)
-        eng.e_step(likelihood_scale, logz[i:i + 1], gamma=gamma if want_gamma else None)
+        eng.e_step(likelihood_scale, logz[i:i + 1], gamma=gamma if want_gamma else None,
+                   log_gamma=lgam if want_gamma else None)
         if i % save_every == 0:
-            saved['log_posterior_all_saved'].append(_masked_log(_np(log_of(gamma)), mlat))
+            saved['log_posterior_all_saved'].append(log_post())
             saved['params_saved'].append(_np(W).astype(np.float32))
             saved['tuning_saved'].append(_np(eng.tuning32))
             saved['iter_saved'].append(i)
@@ -589,7 +640,7 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
            'iter_saved': saved['iter_saved'],
            'params': _np(W).astype(np.float32),
            'tuning': _np(eng.tuning32),
-           'log_posterior_final': _masked_log(_np(log_of(gamma)), mlat),
+           'log_posterior_final': log_post(),
            'log_marginal': float(lz[n_iter - 1]) if n_iter else float('nan'),
            'log_marginal_l': [float(v) for v in lz[:n_iter]],
            'log_marginal_saved': saved['log_marginal_saved'],
@@ -712,22 +763,35 @@ class PoissonGPLVM1D(PoissonGPLVMJump1D):
         del self.possible_dynamics
 
     def _transition(self, movement_variance, p_move_to_jump=0.0, p_jump_to_move=1.0):
-        return banded_transition(self.n_latent_bin, movement_variance, 0.0, 1.0, self.custom_transition_kernel)
+        """Always the dense log-domain scans: without a jump state the only way between
+        distant latents is the continuous kernel itself, with weights like
+        exp(-d^2/mv^2) far below the fp32 / f64 range that the reference's log-space
+        recursion (decoder_latentonly.py:33-123) keeps exactly."""
+        return dense_transition(self.n_latent_bin, movement_variance, 0.0, 1.0, self.custom_transition_kernel)
 
     def _check_latent_mask(self, tr, ma_latent):
-        """Without a jump state, the only way across a run of masked latent bins is one
-        continuous-kernel step of weight exp(-gap^2/mv^2).  The reference keeps those
-        log-domain terms (logK is dense, gp_kernel.py:42-89); the device band stops at
-        tr.band bins (weights below 1e-30 of the centre, under the fp32 range).  A mask
-        whose kept bins are more than tr.band apart therefore has no faithful banded
-        form: raise instead of returning a different log marginal."""
-        if ma_latent is None:
-            return
-        kept = np.flatnonzero(np.asarray(ma_latent) != 0)
-        if kept.size > 1 and int(np.diff(kept).max()) > tr.band:
-            raise NotImplementedError(
-                f"PoissonGPLVM1D: ma_latent leaves a gap of {int(np.diff(kept).max())} latent bins between kept "
-                f"bins, wider than the continuous-kernel band ({tr.band}) of the device scan")
+        """Masks with wide gaps are exact on the dense log-domain scans: nothing to check."""
+
+    def _decode_latent(self, y, tuning, hyperparam, log_latent_transition_kernel, ma_neuron, ma_latent=None,
+                       likelihood_scale=1., n_time_per_chunk=10000):
+        """core.py:943-953 -> decoder_latentonly.smooth_all_step_combined_ma_chunk_latent
+        (decoder_latentonly.py:156-224) with the (L, L) log kernel passed in.  Returns the
+        latent-only 6-tuple: log_acausal (T, L), log marginal, log_causal (T, L),
+        one-step predictive marginals (T,), log joint (L, L), log likelihood (T, L)."""
+        lk = np.asarray(log_latent_transition_kernel, np.float64)
+        L = self.n_latent_bin
+        if lk.shape != (L, L):
+            raise ValueError(f"log_latent_transition_kernel must be ({L}, {L})")
+        hp = dict(hyperparam)
+        hp['p_move_to_jump'], hp['p_jump_to_move'] = 0.0, 1.0
+        logK = np.stack([lk, np.full((L, L), -math.log(L))])
+        with np.errstate(divide='ignore'):
+            logA = np.log(np.array([[1.0, 0.0], [1.0, 0.0]]))
+        r = self._run_decode(y, tuning, hp, ma_neuron, ma_latent, likelihood_scale, joint=True, logK=logK,
+                             logA=logA)
+        return (r['log_posterior_all'][:, 0], r['log_marginal_final'], r['log_causal_posterior_all'][:, 0],
+                r['log_one_step_predictive_marginals_all'], r['log_accumulated_joint'][0, 0],
+                r['log_likelihood_all'])
 
     def init_latent_posterior(self, T, key, random_scale=0.1):
         """core.py:241-251: (1/L + U(0,1)*scale), row-normalised, log (numpy RNG)."""

@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from . import _native as nat
-from .gp_kernel import BandedTransition, banded_transition
+from .gp_kernel import BandedTransition, DenseTransition, banded_transition
 
 
 def _ru(x, m):
@@ -72,6 +72,14 @@ class ScanConfig:
         if self.chunk:
             return int(self.chunk)
         return max(32, int(math.ceil(T / 2048)))
+
+    def chunk_dense_for(self, T):
+        """Chunk of the dense log-domain scans: one 256-thread workgroup per chain and
+        ~13 us per step at L = 512, so ~2 chains per CU and a warm-up that is small
+        next to the chunk."""
+        if self.chunk:
+            return int(self.chunk)
+        return max(64, int(math.ceil(T / 512)))
 
     def chunk_bwd_for(self, T):
         """The backward pass runs at ~1 wave per SIMD with twice the forward chunk: its
@@ -235,6 +243,9 @@ class DeviceEM:
         self._tr = None
         self._tr_c = None
         self._invz = None
+        self.dense = False          # transition held by the dense log-domain scans
+        self.ws_dense = None
+        self.log_alpha = None       # (T, 2, L) log filter state (dense scans)
         self.ma_latent = None
         # Gaussian observation model (GaussianGPLVMJump1D): when noise_std is set, the
         # emission, tuning and M-step dispatch to gaussian.hip; the scans are shared.
@@ -247,9 +258,13 @@ class DeviceEM:
         return self.timer(name) if self.timer is not None else _NO_TIMER
 
     # ------------------------------------------------------------------ setup
-    def set_transition(self, tr: BandedTransition):
+    def set_transition(self, tr):
         if tr.L != self.L:
             raise ValueError("transition size mismatch")
+        if isinstance(tr, DenseTransition):
+            self._set_dense(tr)
+            return
+        self.dense = False
         self._tr = tr
         self._invz = torch.as_tensor(tr.invz, device=self.dev)
         c = nat.Transition()
@@ -261,6 +276,37 @@ class DeviceEM:
         A = tr.A.astype(np.float32)
         c.A[0], c.A[1], c.A[2], c.A[3] = float(A[0, 0]), float(A[0, 1]), float(A[1, 0]), float(A[1, 1])
         self._tr_c = c
+
+    def _set_dense(self, tr: DenseTransition):
+        """Dense log-domain scans (dense_scan.hip): logK0 and its transpose on the device."""
+        self.dense = True
+        self._tr = tr
+        lk64 = np.asarray(tr.logK0, dtype=np.float64)
+        lk = lk64.astype(np.float32)
+        with np.errstate(invalid='ignore'):
+            lo = np.where(np.isfinite(lk), lk64 - lk.astype(np.float64), 0.0).astype(np.float32)
+        self._dK = torch.as_tensor(np.ascontiguousarray(lk), device=self.dev)
+        self._dKT = torch.as_tensor(np.ascontiguousarray(lk.T), device=self.dev)
+        self._dKlo = torch.as_tensor(np.ascontiguousarray(lo), device=self.dev)
+        self._dKTlo = torch.as_tensor(np.ascontiguousarray(lo.T), device=self.dev)
+        c = nat.DenseTransition()
+        c.L = self.L
+        c.logK = nat.ptr(self._dK)
+        c.logKT = nat.ptr(self._dKT)
+        c.logK_lo = nat.ptr(self._dKlo)
+        c.logKT_lo = nat.ptr(self._dKTlo)
+        la = tr.logA.astype(np.float32)
+        c.logA[0], c.logA[1], c.logA[2], c.logA[3] = (float(la[0, 0]), float(la[0, 1]), float(la[1, 0]),
+                                                      float(la[1, 1]))
+        self._tr_d = c
+        self.Cd = self.scan.chunk_dense_for(self.T)
+        need = int(self.lib.pmg_dense_workspace_size(self.T, self.L, self.Cd))
+        if need == 0:
+            raise nat.NativeError(f"n_latent_bin={self.L} unsupported by the dense scans (max 1024)")
+        if self.ws_dense is None or self.ws_dense.numel() < need:
+            self.ws_dense = torch.empty(need, dtype=torch.uint8, device=self.dev)
+        if self.log_alpha is None:
+            self.log_alpha = torch.empty((self.T, 2, self.L), dtype=torch.float32, device=self.dev)
 
     def set_ma_latent(self, ma_latent):
         if ma_latent is None:
@@ -413,8 +459,10 @@ class DeviceEM:
         self._rep_evt = None
 
     def ctl_words(self):
-        """The scans' int32 control words (device view; see fb_kernels.h kCtl*)."""
-        return self.ws_fb[:4 * nat.CTL_WORDS].view(torch.int32)
+        """The scans' int32 control words (device view; see fb_kernels.h kCtl*; the dense
+        scans use the same layout in their own workspace)."""
+        ws = self.ws_dense if self.dense else self.ws_fb
+        return ws[:4 * nat.CTL_WORDS].view(torch.int32)
 
     def _snapshot_repairs(self):
         self._rep_host.copy_(self.ctl_words(), non_blocking=True)
@@ -422,6 +470,14 @@ class DeviceEM:
         self._rep_evt.record()
 
     def forward(self, likelihood_scale, logz_out):
+        if self.dense:
+            with self._t('forward_filter'):      # main pass + verify + relaxation + logZ
+                nat.check(self.lib.pmg_dense_forward(
+                    nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.mref), self.T, ctypes.byref(self._tr_d),
+                    float(likelihood_scale), self.Cd, int(self.warm[0]), float(self.scan.tol),
+                    nat.ptr(self.alpha), nat.ptr(self.log_alpha), nat.ptr(self.logc), nat.ptr(logz_out),
+                    nat.ptr(self.ws_dense), self.ws_dense.numel(), nat.stream_handle()), "pmg_dense_forward")
+            return
         self._adapt_warmup()
         sc = self.scan
         args = (nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.mref), self.T, ctypes.byref(self._tr_c),
@@ -433,7 +489,19 @@ class DeviceEM:
         with self._t('forward_repair'):          # verify / relaxation / logZ
             nat.check(self.lib.pmg_forward_filter_phase(*args, 2), "pmg_forward_filter")
 
-    def backward(self, likelihood_scale, P=True, gamma=None, rho=None):
+    def backward(self, likelihood_scale, P=True, gamma=None, rho=None, log_gamma=None):
+        """rho: the joint partner; with the dense scans it is written as log(rho)
+        (see joint_log)."""
+        if self.dense:
+            with self._t('backward_smoother'):
+                nat.check(self.lib.pmg_dense_backward(
+                    nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.log_alpha), self.T, ctypes.byref(self._tr_d),
+                    float(likelihood_scale), self.Cd, int(self.warm[1]), float(self.scan.tol),
+                    nat.ptr(self.P) if P else None, nat.ptr(gamma), nat.ptr(log_gamma), None, nat.ptr(rho),
+                    nat.ptr(self.ws_dense), self.ws_dense.numel(), nat.stream_handle()), "pmg_dense_backward")
+            return
+        if log_gamma is not None:
+            raise ValueError("log_gamma is produced by the dense scans only")
         sc = self.scan
         args = (nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.alpha), self.T, ctypes.byref(self._tr_c),
                 float(likelihood_scale), self.Cb, int(self.warm[1]), float(sc.tol),
@@ -444,10 +512,10 @@ class DeviceEM:
         with self._t('backward_repair'):         # verify / relaxation
             nat.check(self.lib.pmg_backward_smoother_phase(*args, 2), "pmg_backward_smoother")
 
-    def e_step(self, likelihood_scale, logz_out, gamma=None, rho=None):
+    def e_step(self, likelihood_scale, logz_out, gamma=None, rho=None, log_gamma=None):
         self.emission(likelihood_scale)
         self.forward(likelihood_scale, logz_out)
-        self.backward(likelihood_scale, True, gamma, rho)
+        self.backward(likelihood_scale, True, gamma, rho, log_gamma)
         self._snapshot_repairs()
 
     def repairs(self):
@@ -468,6 +536,13 @@ class DeviceEM:
         nat.check(self.lib.pmg_loglik_materialize(nat.ptr(self.delta), nat.ptr(self.rblk), self.T, self.L,
                                                   nat.ptr(ll), nat.stream_handle()), "pmg_loglik_materialize")
         return ll
+
+    def joint_log(self, log_rho):
+        """Dense scans: log S[x,x'] = LSE_t log alpha_t[x] + log rho_{t+1}[x'] (2L x 2L, f64)."""
+        S = torch.empty((2 * self.L, 2 * self.L), dtype=torch.float64, device=self.dev)
+        nat.check(self.lib.pmg_joint_log_accumulate(nat.ptr(self.log_alpha), nat.ptr(log_rho), self.T, self.L,
+                                                    nat.ptr(S), nat.stream_handle()), "pmg_joint_log_accumulate")
+        return S
 
     def joint(self, rho):
         """S[x,x'] = sum_t alpha_t[x] rho_{t+1}[x'] (2L x 2L, f64)."""

@@ -299,6 +299,10 @@ class TimeShardedEM:
         B = np.asarray(basis, np.float32)
         self.L = B.shape[0]
         scan = scan or ScanConfig()
+        from .gp_kernel import DenseTransition
+        if isinstance(transition, DenseTransition):
+            raise NotImplementedError("time-sharded EM runs the banded scans only (the dense log-domain scans "
+                                      "have no carry hand-off yet)")
         self.shards = [ShardEM(lay, y, self.L, B, scan, ma_neuron, device) for lay in self.lays]
         for s in self.shards:
             s.set_transition(transition)

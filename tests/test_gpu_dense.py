@@ -1,0 +1,168 @@
+"""GPU parity of the dense log-domain scans (dense_scan.hip) and of the kernels passed to
+_decode_latent, against the float64 oracle.
+
+The dense scans run the reference's own log-space recursion (decoder.py:151-226) for
+continuous kernels the banded linear-space scans cannot hold: custom_transition_kernel
+(gp_kernel.py:30-34, 61-66), RBF kernels wider than 32 bins, and the latent-only model
+(decoder_latentonly.py), whose far latent moves have weights (exp(-1000)) beyond the
+fp32 / f64 range.  Bars: posteriors rel 1e-5 (atol 1e-12) for the jump model; for the
+latent-only model max abs 1e-5 and < 10 % of the fp32 reference-mimic's deviation
+(test_gpu_parity.latent_only_close); log marginal rel 1e-7; finite log outputs where
+the reference's are finite.
+"""
+import warnings
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import gplvm_oracle as O
+from tests.synth import make
+from tests.test_gpu_parity import argmax_match, close_prob, latent_only_close
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _dev():
+    torch.cuda.set_device(0)
+
+
+def _custom_kernel(L, seed=5):
+    rng = np.random.default_rng(seed)
+    i = np.arange(L)
+    return np.exp(-np.abs(i[:, None] - i[None, :]) / 3.0) + 0.02 * rng.random((L, L))
+
+
+@pytest.mark.parametrize("chunk", [None, 16])
+def test_custom_transition_kernel_decode_vs_oracle(chunk):
+    """Jump model with a dense custom continuous kernel (gp_kernel.py:61-66); chunk 16
+    with no warm-up makes every boundary fail so the relaxation runs."""
+    import poor_man_gplvm_amd as P
+    N, L, T = 30, 80, 700
+    d = make(N, L, T)
+    Kc = _custom_kernel(L)
+    sc = P.ScanConfig(chunk=chunk, warmup=0 if chunk else 48)
+    m = P.PoissonGPLVMJump1D(N, n_latent_bin=L, tuning_lengthscale=10., custom_transition_kernel=Kc,
+                             scan_config=sc)
+    r = m.decode_latent(d['y'], tuning=d['tuning'])
+    ref = O.decode_latent(d['y'], d['tuning'], custom_kernel=Kc)
+    close_prob(r['posterior_all'], ref['posterior_all'])
+    argmax_match(r['posterior_latent_marg'], ref['posterior_latent_marg'])
+    assert abs(r['log_marginal_final'] - ref['log_marginal_final']) <= 1e-7 * abs(ref['log_marginal_final'])
+    np.testing.assert_allclose(r['log_one_step_predictive_marginals_all'],
+                               ref['log_one_step_predictive_marginals_all'], rtol=1e-6, atol=1e-5)
+    lp, lr = r['log_posterior_all'], ref['log_posterior_all']
+    assert np.all(np.isfinite(lp))
+    keep = lr > -60
+    np.testing.assert_allclose(lp[keep], lr[keep], atol=2e-4)
+    np.testing.assert_allclose(r['p_transition_full'], ref['p_transition_full'], rtol=1e-4, atol=1e-7)
+
+
+def test_wide_movement_variance_vs_oracle():
+    """movement_variance = 5 needs a 42-bin band (> 32): the dense scans take it."""
+    import poor_man_gplvm_amd as P
+    N, L, T = 40, 128, 800
+    d = make(N, L, T, mv=5.0)
+    m = P.PoissonGPLVMJump1D(N, n_latent_bin=L, tuning_lengthscale=10., movement_variance=5.0)
+    r = m.decode_latent(d['y'], tuning=d['tuning'])
+    ref = O.decode_latent(d['y'], d['tuning'], movement_variance=5.0)
+    close_prob(r['posterior_all'], ref['posterior_all'])
+    assert abs(r['log_marginal_final'] - ref['log_marginal_final']) <= 1e-7 * abs(ref['log_marginal_final'])
+
+
+@pytest.mark.parametrize("masked", [False, True])
+def test_latent_only_far_moves_exact(masked):
+    """Latent-only model on data sampled WITH jumps (moves of tens of bins): the log
+    marginal includes transitions of weight exp(-1000) (tools/diag_lo_mask.py; round 1's
+    banded scan gave -48336 against the reference's -47881 here)."""
+    import poor_man_gplvm_amd as P
+    N, L, T = 30, 100, 1500
+    d = make(N, L, T)
+    ml = None
+    if masked:
+        ml = np.zeros(L)
+        ml[::3] = 1
+        ml[np.random.default_rng(0).choice(L, 20, replace=False)] = 1
+    _, logK = O.create_transition_prob_latent_1d(L, 1.0)
+    lpa, lz, lca, cs, lj, ll = O.smooth_latent_only(d['y'], d['tuning'], logK, ma_latent=ml)
+    m = P.PoissonGPLVM1D(N, n_latent_bin=L, tuning_lengthscale=10.)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", RuntimeWarning)
+        res = m.decode_latent(d['y'], tuning=d['tuning'], ma_latent=ml)
+    assert abs(res['log_marginal_final'] - lz) <= 1e-7 * abs(lz), (res['log_marginal_final'], lz)
+    # the pairwise joint of a far move (rho ~ e^+1000 against K ~ e^-1000) is accumulated
+    # in log space: finite, and equal to the reference's logaddexp accumulation
+    keep = np.ones(L, bool) if ml is None else ml.astype(bool)
+    for k in ('p_transition_latent', 'p_joint_latent', 'log_joint_latent'):
+        assert not np.isnan(res[k]).any(), k
+    ref = O.compute_transition_posterior_prob_latent(lj)
+    rows = keep & (ref['p_joint_latent'].sum(1) > 1e-6)
+    np.testing.assert_allclose(res['p_transition_latent'][np.ix_(rows, keep)],
+                               ref['p_transition_latent'][np.ix_(rows, keep)], rtol=1e-4, atol=1e-6)
+    latent_only_close(res['posterior_all'], d['y'], d['tuning'], logK, ml)
+    argmax_match(res['posterior_all'], np.exp(lpa))
+    fwd = m.log_marginal_masked(d['y'], (np.ones(L) if ml is None else ml)[None], tuning=d['tuning'])[0]
+    assert abs(fwd - lz) <= 1e-7 * abs(lz)
+
+
+def test_latent_only_private_decode_signature():
+    """PoissonGPLVM1D._decode_latent(y, tuning, hyperparam, log_latent_transition_kernel (L, L),
+    ma_neuron, ...) -> the latent-only 6-tuple (core.py:943-953)."""
+    import poor_man_gplvm_amd as P
+    N, L, T = 20, 60, 400
+    d = make(N, L, T)
+    _, logK = O.create_transition_prob_latent_1d(L, 2.0)      # a kernel other than the model's
+    m = P.PoissonGPLVM1D(N, n_latent_bin=L, tuning_lengthscale=10.)
+    la, lz, lc, cs, lj, ll = m._decode_latent(d['y'], d['tuning'], {}, logK, np.ones(N))
+    rla, rlz, rlc, rcs, rlj, rll = O.smooth_latent_only(d['y'], d['tuning'], logK)
+    assert la.shape == (T, L) and lj.shape == (L, L)
+    latent_only_close(np.exp(la), d['y'], d['tuning'], logK)
+    assert abs(lz - rlz) <= 1e-7 * abs(rlz)
+
+
+@pytest.mark.parametrize("kind", ["banded_other_mv", "dense_custom"])
+def test_decode_latent_uses_passed_kernels(kind):
+    """_decode_latent scans with the kernels it is passed (core.py:777-786), not with the
+    model's own hyper-parameters."""
+    import poor_man_gplvm_amd as P
+    N, L, T = 30, 64, 500
+    d = make(N, L, T)
+    m = P.PoissonGPLVMJump1D(N, n_latent_bin=L, tuning_lengthscale=10., movement_variance=1.0)
+    if kind == "banded_other_mv":
+        _, logK, _, logA = O.create_transition_prob_1d(L, 2.0, 0.05, 0.02)
+    else:
+        _, logK, _, logA = O.create_transition_prob_1d(L, 1.0, 0.01, 0.01, custom_kernel=_custom_kernel(L, 9))
+    la, lz, lc, cs, lj, ll = m._decode_latent(d['y'], d['tuning'], {}, logK, logA, np.ones(N))
+    rla, rlz, rlc, rcs, rlj, rll = O.smooth_all_step_combined_ma_chunk(d['y'], d['tuning'], logK, logA,
+                                                                        with_joint=True)
+    close_prob(np.exp(la), np.exp(rla))
+    assert abs(lz - rlz) <= 1e-7 * abs(rlz)
+    np.testing.assert_allclose(np.exp(lj), np.exp(rlj), rtol=1e-4, atol=1e-5 * np.exp(rlj).max())
+
+
+def test_decode_latent_outputs_finite_with_unvisited_bins():
+    """Strongly tuned neurons leave most latent bins unvisited (their f32 alpha
+    underflows): every decode_latent output must stay finite, with no RuntimeWarning
+    (round 1 returned NaN transition rows here)."""
+    import poor_man_gplvm_amd as P
+    N, L, T = 60, 100, 400
+    d = make(N, L, T)
+    tun = d['tuning'] * 8.0
+    rng = np.random.default_rng(3)
+    y = rng.poisson(tun[d['latent'][:, 1]]).astype(np.float32)
+    m = P.PoissonGPLVMJump1D(N, n_latent_bin=L, tuning_lengthscale=10.)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", RuntimeWarning)
+        r = m.decode_latent(y, tuning=tun)
+    for k, v in r.items():
+        if isinstance(v, np.ndarray):
+            assert not np.isnan(v).any(), k
+    for k in ('log_transition_full', 'log_transition_latent', 'log_joint_full', 'p_transition_full',
+              'p_transition_latent'):
+        assert np.all(np.isfinite(r[k])), k
+    # rows with mass match the oracle; unvisited rows are the prior transition
+    ref = O.decode_latent(y, tun)
+    mass = ref['p_joint_latent'].sum(1) > 1e-6
+    np.testing.assert_allclose(r['p_transition_latent'][mass], ref['p_transition_latent'][mass], rtol=1e-4,
+                               atol=1e-7)

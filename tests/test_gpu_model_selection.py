@@ -59,16 +59,21 @@ def test_log_marginal_masked_vs_oracle(model, N, L, T, frac):
         np.testing.assert_allclose(ds['std'], np.std(ref), rtol=1e-4, atol=1e-6 * abs(np.mean(ref)))
 
 
-def test_latent_only_mask_gap_wider_than_band_raises():
+def test_latent_only_mask_gap_wider_than_band():
+    """Masks whose kept latent bins are further apart than any band: the latent-only
+    model crosses the gap with its log-domain continuous kernel (decoder_latentonly.py),
+    exactly as the reference."""
     import poor_man_gplvm_amd as P
+    from oracle import gplvm_oracle as O
     d = make(10, 60, 100)
     m = P.PoissonGPLVM1D(10, n_latent_bin=60)
     ml = np.zeros(60)
-    ml[[0, 5, 30, 31]] = 1                       # gap of 25 bins > band 9 (mv = 1)
-    with pytest.raises(NotImplementedError):
-        m.log_marginal_masked(d['y'], ml[None], tuning=d['tuning'])
-    with pytest.raises(NotImplementedError):
-        m.decode_latent(d['y'], tuning=d['tuning'], ma_latent=ml)
+    ml[[0, 5, 30, 31]] = 1                       # a gap of 25 bins
+    _, logK = O.create_transition_prob_latent_1d(60, 1.0)
+    lz = O.smooth_latent_only(d['y'], d['tuning'], logK, ma_latent=ml)[1]
+    got = m.log_marginal_masked(d['y'], ml[None], tuning=d['tuning'])[0]
+    assert abs(got - lz) <= 1e-7 * abs(lz)
+    assert abs(m.decode_latent(d['y'], tuning=d['tuning'], ma_latent=ml)['log_marginal_final'] - lz) <= 1e-7 * abs(lz)
 
 
 def test_log_marginal_masked_rejects_bad_masks():

@@ -3,7 +3,7 @@ spike train with halo warm-up and carry rounds must reproduce the unsharded answ
 
 Bars (as tests/test_gpu_parity.py): against the float64 golden fixtures the same
 tolerances as the single-GPU EM; against the single-GPU engine on larger inputs the
-scan tolerance after one EM iteration (Hilbert boundary tol 1e-6 -> probabilities
+scan tolerance after one EM iteration (Hilbert boundary tol 3e-6 -> probabilities
 within rel 2e-5 where P > 1e-12; 1e-5 absolute after two), logZ rel 1e-7 (suff-stat sums are re-associated over shards), identical
 Adam iteration counts.
 Virtual shards (LocalComm) run every shard on cuda:0 in one process; the gloo case
@@ -27,14 +27,15 @@ def _dev():
     torch.cuda.set_device(0)
 
 
-def _sharded_fixture(name, world, chunk, halo):
+def _sharded_fixture(name, world, chunk, halo, scan_tol=None):
     import poor_man_gplvm_amd as P
     from poor_man_gplvm_amd.timeshard import run_em_timesharded
     f = np.load(os.path.join(HERE, 'golden', name))
     L = f['basis'].shape[0]
+    sc = None if scan_tol is None else P.ScanConfig(tol=scan_tol)
     res, info = run_em_timesharded(f['y'].astype(np.float32), f['W0'], f['basis'], f['lp0'],
                                    n_iter=int(f['n_iter']), transition=P.banded_transition(L, float(f['mv'])),
-                                   world=world, chunk=chunk, halo=halo,
+                                   world=world, chunk=chunk, halo=halo, scan=sc,
                                    adam=P.AdamConfig(maxiter=int(f['maxiter']), tol=float(f['tol'])))
     return f, res, info
 
@@ -51,8 +52,10 @@ def test_timesharded_one_iteration_golden(world, chunk, halo):
 
 
 def test_timesharded_fixed_iterations_golden():
-    """Three EM iterations over 4 shards (same bar as test_fit_em_fixed_iterations_golden)."""
-    f, res, info = _sharded_fixture('em_c1_fixed.npz', 4, 16, 32)
+    """Three EM iterations over 4 shards (same bar as test_fit_em_fixed_iterations_golden).
+    The bar (10 % of the fp32 reference-mimic's own deviation, 4.1e-6 here) is tighter than
+    what the default scan tolerance guarantees (2 x 3e-6), so this fixture scans at 1e-6."""
+    f, res, info = _sharded_fixture('em_c1_fixed.npz', 4, 16, 32, scan_tol=1e-6)
     np.testing.assert_allclose(res['tuning'], f['tuning'], rtol=RT)
     exact = f['posterior'].astype(np.float64).sum(1)
     ours = np.asarray(res['posterior_latent_marg'], np.float64)

@@ -43,6 +43,53 @@ def test_band_limit_raises():
         banded_transition(512, 10.0)
 
 
+def test_transition_selection():
+    """Banded scans when the continuous kernel is a <= 32-bin RBF band, dense log-domain
+    scans otherwise; kernels passed as logs are recovered in the same forms."""
+    from poor_man_gplvm_amd.gp_kernel import (DenseTransition, BandedTransition, make_transition,
+                                              transition_from_log_kernels, create_transition_prob_1d)
+    assert isinstance(make_transition(100, 1.0), BandedTransition)
+    assert isinstance(make_transition(100, 10.0), DenseTransition)
+    L = 50
+    Kc = np.exp(-np.abs(np.arange(L)[:, None] - np.arange(L)[None, :]) / 3.0)
+    assert isinstance(make_transition(L, 1.0, custom_kernel=Kc), DenseTransition)
+    _, lk, _, la = create_transition_prob_1d(L, 2.0, 0.05, 0.02)
+    tr = transition_from_log_kernels(lk, la)
+    ref = banded_transition(L, 2.0, 0.05, 0.02)
+    assert isinstance(tr, BandedTransition) and tr.band <= ref.band
+    np.testing.assert_allclose(tr.g, ref.g[:tr.band + 1], rtol=1e-6)
+    assert np.all(ref.g[tr.band + 1:] < 1e-30)
+    np.testing.assert_allclose(tr.invz, ref.invz, rtol=1e-6)
+    np.testing.assert_allclose(tr.A, ref.A, rtol=1e-12)
+    _, lk, _, la = create_transition_prob_1d(L, 1.0, custom_kernel=Kc)
+    assert isinstance(transition_from_log_kernels(lk, la), DenseTransition)
+    assert isinstance(transition_from_log_kernels(*create_transition_prob_1d(L, 1.0)[1::2], force_dense=True),
+                      DenseTransition)
+    lk_bad = lk.copy()
+    lk_bad[1, 0, 0] += 1.0
+    with pytest.raises(NotImplementedError):
+        transition_from_log_kernels(lk_bad, la)
+
+
+def test_log_joint_never_nan():
+    """Underflowed joint counts (unvisited states) keep finite log values and normalise
+    to the prior transition; masked latents keep the -1e20 sentinel sums."""
+    from poor_man_gplvm_amd.core import log_joint_from_counts, compute_transition_posterior_prob
+    L = 6
+    _, logK, _, logA = P.create_transition_prob_1d(L, 1.0)
+    S4 = np.random.default_rng(0).random((2, 2, L, L))
+    S4[0, :, 2, :] = 0.0                  # state (d=0, i=2) never visited
+    lj = log_joint_from_counts(S4, logK, logA)
+    assert np.all(np.isfinite(lj))
+    with np.errstate(invalid='raise', divide='raise'):
+        r = compute_transition_posterior_prob(lj)
+    for k, v in r.items():
+        assert np.all(np.isfinite(v)), k
+    row = r['p_transition_full'][0, :, 2, :].astype(np.float64)
+    prior = np.exp(logA[0][:, None] + logK[:, 2, :])
+    np.testing.assert_allclose(row, prior / prior.sum(), rtol=1e-5)
+
+
 def test_constructor_and_api_without_gpu():
     m = P.PoissonGPLVMJump1D(30, n_latent_bin=100, tuning_lengthscale=10.)
     assert m.tuning_basis.shape == (100, 18)
