@@ -3,7 +3,9 @@
 HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (both reported in KB).  The factor
 2 is the gfx950 correction of MI355X_MICROARCH.md (HBM section): FETCH_SIZE counts
 128-B memory-side read requests as 64 B for wide coalesced streaming reads.
-usage: python tools/pmc_summary.py gpurun_out/pmc1 profiles/r01_pmc_c3.json
+Only the last LAST_ITERS EM iterations' dispatches of each kernel count (steady state:
+the first iterations of a fresh fit run long relaxations and Adam loops).
+usage: python tools/pmc_summary.py gpurun_out/pmc1 profiles/r02_pmc_c3.json [ITERS LAST_ITERS]
 """
 import csv
 import glob
@@ -12,18 +14,25 @@ import sys
 from collections import defaultdict
 
 KEYS = {"k_forward<": "k_forward", "k_backward<": "k_backward", "k_ptb3": "k_ptb3",
-        "k_emission_i8": "k_emission_i8", "k_adam<": "k_adam"}
+        "k_emission_i8": "k_emission_i8", "k_adam<": "k_adam", "k_verify": "k_verify",
+        "k_forward_relax<": "k_forward_relax", "k_backward_relax<": "k_backward_relax"}
 
 
-def main(prefix, out):
+def main(prefix, out, iters=7, last_iters=3):
     vals = defaultdict(lambda: defaultdict(list))
     for tag in ("fetch", "write", "sq", "sq2"):
         files = glob.glob(f"{prefix}_{tag}/**/*counter_collection.csv", recursive=True)
+        per = defaultdict(lambda: defaultdict(list))     # kernel -> counter -> [(dispatch, value)]
         for f in files:
             for r in csv.DictReader(open(f)):
                 for pat, k in KEYS.items():
                     if pat in r["Kernel_Name"]:
-                        vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                        per[k][r["Counter_Name"]].append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
+        for k, cs in per.items():
+            for c, dv in cs.items():
+                dv.sort()
+                keep = max(1, len(dv) // iters) * last_iters
+                vals[k][c].extend(v for _, v in dv[-keep:])
     res = {}
     for k, cs in vals.items():
         mean = {c: sum(v) / len(v) for c, v in cs.items()}
@@ -33,7 +42,8 @@ def main(prefix, out):
             e["hbm_write_bytes_per_launch"] = mean["WRITE_SIZE"] * 1024.0
             e["hbm_bytes_per_launch"] = e["hbm_read_bytes_per_launch"] + e["hbm_write_bytes_per_launch"]
         res[k] = e
-    doc = {"source": f"rocprofv3 --pmc passes, {prefix}_*, bench.py --steps 3 --warmup 3",
+    doc = {"source": f"rocprofv3 --pmc passes, {prefix}_*, bench.py --steps 3 --warmup 3 (+1 pre-warm iteration); "
+                     f"means over the last {last_iters} of {iters} EM iterations' dispatches",
            "note": "FETCH_SIZE doubled (gfx950 correction); values are means over the profiled dispatches",
            "kernels": res}
     with open(out, "w") as fh:
@@ -43,4 +53,4 @@ def main(prefix, out):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], *(int(a) for a in sys.argv[3:5]))
