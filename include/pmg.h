@@ -90,6 +90,13 @@ int pmg_emission_poisson_f64(const float* y, const double* gconst, const double*
                              const float* ma_neuron, int32_t ma_is_2d, const uint8_t* ma_latent,
                              double dt, int64_t T, int32_t L, int32_t N, float* delta,
                              double* rblk, void* workspace, size_t workspace_bytes, void* stream);
+/* Latent mask on an unmasked emission (any of the emissions above, run with ma_latent =   */
+/* NULL): (delta, rblk) = the (delta0, rblk0) those kernels would produce with ma_latent   */
+/* (ll[:, ma_latent == 0] = -1e20, decoder.py:46; block references over kept bins).  Used  */
+/* by log_marginal_masked so that get_downsampled_lml's masks (model_selection_helper.py: */
+/* 243-260) share one emission contraction.  Out of place.                                */
+int pmg_emission_latent_mask(const float* delta0, const double* rblk0, int64_t T, int32_t L,
+                             const uint8_t* ma_latent, float* delta, double* rblk, void* stream);
 /* Per-time reference: m[t] = max_b rblk[t,b], phi[t,b] = f32(s*(rblk[t,b]-m[t])) so that  */
 /* exp(s*ll[t,l] - s*m[t]) = exp(s*delta[t,l] + phi[t,l/32]).                              */
 int pmg_emission_rowref(const double* rblk, int64_t T, int32_t nblk, double likelihood_scale,
@@ -271,6 +278,10 @@ int pmg_suffstats_bf16(const float* P, const uint16_t* ybt, int64_t T, int64_t T
 int pmg_exp(const float* logp, int64_t n, float* p, void* stream);
 /* out = log(x) elementwise (log-space outputs; log(0) = -inf). */
 int pmg_log(const float* x, int64_t n, float* out, void* stream);
+/* out[t, n] = y[(t - shift[n]) mod T, n] for y, out (T, N) row-major f32, shift (N,) int64
+ * (device): every neuron's column rolled by its own shift, the np.roll of
+ * test.circular_shuffle_data (reference poor_man_gplvm/test.py:10-24).  y != out. */
+int pmg_roll_columns(const float* y, int64_t T, int32_t N, const int64_t* shift, float* out, void* stream);
 
 /* ------------------------------------------------------------------ */
 /* Adam M-step -- fit_tuning_helper.make_adam_runner.run                 */

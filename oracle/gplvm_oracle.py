@@ -46,7 +46,7 @@ __all__ = [
     "adam_init", "adam_update", "adam_run", "m_step", "fit_em", "decode_latent",
     "naive_bayes_chunk", "init_latent_posterior_from_uniform", "sample_latent",
     "sample_spikes", "jump_consensus", "downsampled_lml", "loglikelihood_gaussian_all",
-    "gaussian_m_step_analytic", "fit_em_gaussian",
+    "gaussian_m_step_analytic", "fit_em_gaussian", "circular_shuffle_once", "compute_entropy",
 ]
 
 NEG_MASK = -1e20          # decoder.py:46  masked latent log-likelihood
@@ -654,3 +654,23 @@ def downsampled_lml(y, tuning, masks, movement_variance=1.0, p_move_to_jump=0.01
         lml.append(float(logz))
     lml = np.array(lml)
     return lml, lml.mean(), lml.std()
+
+
+def circular_shuffle_once(y, rng_randint=np.random.randint):
+    """test.py:19-24, one shuffle: column j rolled by randint(0, n_time), drawn per
+    neuron in column order.  Returns (shuffled copy, shifts)."""
+    y = np.asarray(y)
+    n_time, n_neuron = y.shape
+    out = y.copy()
+    shifts = np.zeros(n_neuron, dtype=np.int64)
+    for j in range(n_neuron):
+        shifts[j] = rng_randint(0, n_time)
+        out[:, j] = np.roll(y[:, j], shifts[j])
+    return out, shifts
+
+
+def compute_entropy(logp_l, axis=(-1, -2)):
+    """test.py:70-79 with p = 0 states contributing 0."""
+    p = np.exp(np.asarray(logp_l, np.float64))
+    with np.errstate(invalid='ignore', divide='ignore'):
+        return -np.sum(np.where(p > 0, p * np.log(np.where(p > 0, p, 1.0)), 0.0), axis=axis)

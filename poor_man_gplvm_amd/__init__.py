@@ -11,4 +11,4 @@ from .core import (GaussianGPLVM1D, GaussianGPLVMJump1D, PoissonGPLVM1D, Poisson
                    compute_transition_posterior_prob_latent, run_em)
 from .engine import AdamConfig, ScanConfig  # noqa: F401
 from .gp_kernel import banded_transition, create_transition_prob_1d, generate_basis  # noqa: F401
-from . import model_selection_helper  # noqa: F401
+from . import model_selection_helper, test  # noqa: F401

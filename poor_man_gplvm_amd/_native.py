@@ -32,7 +32,7 @@ EXPORTED_SYMBOLS = (
     "pmg_emission_rowref", "pmg_loglik_materialize", "pmg_fwdbwd_workspace_size",
     "pmg_forward_filter", "pmg_backward_smoother", "pmg_fwdbwd_repair_counter_offset",
     "pmg_forward_filter_phase", "pmg_backward_smoother_phase",
-    "pmg_suffstats_workspace_size", "pmg_suffstats", "pmg_exp", "pmg_log",
+    "pmg_suffstats_workspace_size", "pmg_suffstats", "pmg_exp", "pmg_log", "pmg_roll_columns", "pmg_emission_latent_mask",
     "pmg_spikes_bf16t", "pmg_suffstats_bf16_workspace_size", "pmg_suffstats_bf16",
     "pmg_mstep_workspace_size", "pmg_mstep_adam_supported", "pmg_mstep_adam", "pmg_joint_workspace_size",
     "pmg_joint_accumulate", "pmg_fwdbwd_lpad", "pmg_fwdbwd_state",
@@ -105,6 +105,8 @@ _SIGS = {
     "pmg_suffstats_bf16": ([_P, _P, _I64, _I64, _I32, _I32, _I32, _P, _P, _P, _SZ, _P], _I32),
     "pmg_exp": ([_P, _I64, _P, _P], _I32),
     "pmg_log": ([_P, _I64, _P, _P], _I32),
+    "pmg_roll_columns": ([_P, _I64, _I32, _P, _P, _P], _I32),
+    "pmg_emission_latent_mask": ([_P, _P, _I64, _I32, _P, _P, _P, _P], _I32),
     "pmg_mstep_workspace_size": ([_I32, _I32], _SZ),
     "pmg_mstep_adam_supported": ([_I32, _I32, _I32], ctypes.c_int),
     "pmg_mstep_adam": ([_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, ctypes.POINTER(AdamCfg),

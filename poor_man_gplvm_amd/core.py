@@ -212,21 +212,33 @@ class PoissonGPLVMJump1D:
 
     def _run_decode(self, y, tuning, hyperparam, ma_neuron, ma_latent, likelihood_scale, joint=True,
                     logK=None, logA=None):
+        eng = self._decode_engine(y, tuning, hyperparam, ma_neuron, ma_latent, logK, logA)
+        return self._decode_on(eng, hyperparam, ma_latent, likelihood_scale, joint, logK, logA)
+
+    def _decode_engine(self, y, tuning, hyperparam, ma_neuron, ma_latent, logK=None, logA=None):
+        """Device state of a decode: spikes uploaded and prepared, transition, masks and
+        tuning set (reusable across decodes of spike trains of the same shape)."""
         mv = hyperparam.get('movement_variance', self.movement_variance)
         pmj = hyperparam.get('p_move_to_jump', self.p_move_to_jump)
         pjm = hyperparam.get('p_jump_to_move', self.p_jump_to_move)
-        y = np.asarray(y)
         ma = None if ma_neuron is None else np.asarray(ma_neuron, np.float32)
         tr = self._scan_transition(mv, pmj, pjm, logK, logA)
         self._check_latent_mask(tr, ma_latent)
-        sp = SpikeData(y, ma)
+        sp = SpikeData(y if isinstance(y, torch.Tensor) else np.asarray(y), ma)
         eng = DeviceEM(sp, self.n_latent_bin, scan=self.scan_config)
         self._observation(eng, hyperparam)
         eng.set_transition(tr)
         eng.set_ma_latent(ma_latent)
         eng.set_tuning(np.asarray(tuning))
+        return eng
+
+    def _decode_on(self, eng, hyperparam, ma_latent, likelihood_scale, joint=True, logK=None, logA=None):
+        """One smoother pass (emission, forward, backward, joint) over eng's current spikes."""
+        mv = hyperparam.get('movement_variance', self.movement_variance)
+        pmj = hyperparam.get('p_move_to_jump', self.p_move_to_jump)
+        pjm = hyperparam.get('p_jump_to_move', self.p_jump_to_move)
         dev = eng.dev
-        T, L = sp.T, self.n_latent_bin
+        T, L = eng.T, self.n_latent_bin
         logz = torch.zeros(1, dtype=torch.float64, device=dev)
         gamma = torch.empty((T, 2, L), dtype=torch.float32, device=dev)
         rho = torch.zeros((T, 2, L), dtype=torch.float32, device=dev) if joint else None
@@ -275,7 +287,22 @@ class PoissonGPLVMJump1D:
             ma_neuron = self.ma_neuron_default
         if ma_latent is None:
             ma_latent = self.ma_latent_default
-        r = self._run_decode(y, tuning, hyperparam, ma_neuron, ma_latent, likelihood_scale, joint=True)
+        hp, logK, logA = self._dynamics_decode_args(hyperparam)
+        r = self._run_decode(y, tuning, hp, ma_neuron, ma_latent, likelihood_scale, joint=True, logK=logK,
+                             logA=logA)
+        return self._decode_result(r, t_l)
+
+    def _decode_hp(self, hyperparam):
+        """Hook: the hyper-parameters a public decode call adds (the Gaussian model's noise_std)."""
+        return dict(hyperparam)
+
+    def _dynamics_decode_args(self, hyperparam):
+        """Hook: (hyperparam, logK, logA) of decode_latent's smoother; None kernels = the
+        model's own transition for these hyper-parameters."""
+        return dict(hyperparam), None, None
+
+    def _decode_result(self, r, t_l=None):
+        """decode_latent's returned dict from a _decode_on result (core.py:477-497)."""
         posterior_all = r['posterior_all']
         plm = posterior_all.sum(axis=1)
         pdm = posterior_all.sum(axis=2)
@@ -309,15 +336,24 @@ class PoissonGPLVMJump1D:
             ma_neuron = self.ma_neuron_default
         if ma_latent is None:
             ma_latent = self.ma_latent_default
-        y = np.asarray(y)
-        T = y.shape[0]
-        dt = np.broadcast_to(np.asarray(dt_l, np.float64), (T,))
+        eng = self._nb_engine(y, tuning, hyperparam, ma_neuron, ma_latent)
+        return self._nb_on(eng, dt_l, t_l)
+
+    def _nb_engine(self, y, tuning, hyperparam, ma_neuron, ma_latent):
+        """Device state of a naive-Bayes decode (spikes, masks, tuning; no transition)."""
         ma = None if ma_neuron is None else np.asarray(ma_neuron, np.float32)
-        sp = SpikeData(y, ma)
+        sp = SpikeData(y if isinstance(y, torch.Tensor) else np.asarray(y), ma)
         eng = DeviceEM(sp, self.n_latent_bin, scan=self.scan_config)
         self._observation(eng, hyperparam)
         eng.set_ma_latent(ma_latent)
         eng.set_tuning(np.asarray(tuning))
+        return eng
+
+    def _nb_on(self, eng, dt_l, t_l=None):
+        """decode_latent_naive_bayes over eng's current spikes."""
+        sp = eng.sp
+        T = sp.T
+        dt = np.broadcast_to(np.asarray(dt_l, np.float64), (T,))
         dev, L = eng.dev, self.n_latent_bin
         lib, sh = eng.lib, nat.stream_handle()
         if eng.noise_std is not None and not np.all(dt == dt[0]):
@@ -353,10 +389,12 @@ class PoissonGPLVMJump1D:
         This is the inner loop of model_selection_helper.get_downsampled_lml
         (model_selection_helper.py:243-260), which reads nothing from each decode
         but log_marginal_final.  So the spikes are uploaded once, the transition and
-        tuning are set once, and each mask runs only the emission and the forward
-        filter (logZ is the filter's Σ_t c_t, decoder.py:151-187).  The backward
-        pass, the joint and the host copies of (T, D, L) tensors are skipped.
-        Every logZ stays on the device until one copy at the end."""
+        tuning are set once, the emission contraction runs once (unmasked), and each
+        mask runs only pmg_emission_latent_mask (masked bins to -1e20, block
+        references re-derived), the row reference and the forward filter (logZ is
+        the filter's sum_t c_t, decoder.py:151-187).  The backward pass, the joint
+        and the host copies of (T, D, L) tensors are skipped.  Every logZ stays on
+        the device until one copy at the end."""
         if _is_tsd(y):
             y = y.d
         if tuning is None:
@@ -380,9 +418,11 @@ class PoissonGPLVMJump1D:
         eng.set_transition(tr)
         eng.set_tuning(np.asarray(tuning))
         logz = torch.zeros(len(masks), dtype=torch.float64, device=eng.dev)
-        for r, m in enumerate(masks):
-            eng.set_ma_latent(m)
-            eng.emission(likelihood_scale)
+        eng.set_ma_latent(None)
+        delta0, rblk0 = eng.emission_unmasked()
+        mu8 = torch.as_tensor((masks != 0).astype(np.uint8), device=eng.dev)
+        for r in range(len(masks)):
+            eng.emission_from(delta0, rblk0, mu8[r], likelihood_scale)
             eng.forward(likelihood_scale, logz[r:r + 1])
         return _np(logz).astype(np.float64)
 
@@ -710,6 +750,11 @@ class GaussianGPLVMJump1D(PoissonGPLVMJump1D):
         finally:
             self._fit_noise_std = None
 
+    def _decode_hp(self, hyperparam):
+        hp = dict(hyperparam)
+        hp['noise_std'] = hp.get('noise_std', self.noise_std)
+        return hp
+
     def decode_latent(self, y, tuning=None, hyperparam={}, **kwargs):
         """core.py:879-882: noise_std from hyperparam or the model."""
         hp = dict(hyperparam)
@@ -816,11 +861,19 @@ class PoissonGPLVM1D(PoissonGPLVMJump1D):
             ma_neuron = self.ma_neuron_default
         if ma_latent is None:
             ma_latent = self.ma_latent_default
+        hp, logK, logA = self._dynamics_decode_args(hyperparam)
+        r = self._run_decode(y, tuning, hp, ma_neuron, ma_latent, likelihood_scale, joint=True, logK=logK, logA=logA)
+        return self._decode_result(r, t_l)
+
+    def _dynamics_decode_args(self, hyperparam):
         hp = dict(hyperparam)
         hp['p_move_to_jump'], hp['p_jump_to_move'] = 0.0, 1.0
         mv = hp.get('movement_variance', self.movement_variance)
         _, logK, _, logA = create_transition_prob_1d(self.n_latent_bin, mv, 0.0, 1.0, self.custom_transition_kernel)
-        r = self._run_decode(y, tuning, hp, ma_neuron, ma_latent, likelihood_scale, joint=True, logK=logK, logA=logA)
+        return hp, logK, logA
+
+    def _decode_result(self, r, t_l=None):
+        """decode_latent's latent-only dict (core.py:160-177)."""
         posterior_all = r['posterior_all'][:, 0]
         if t_l is not None and nap is not None:
             posterior_all = nap.TsdFrame(d=posterior_all, t=t_l)

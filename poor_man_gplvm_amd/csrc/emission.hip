@@ -272,6 +272,43 @@ __global__ void __launch_bounds__(256) k_emission_f64(
   }
 }
 
+// Latent mask applied to an unmasked emission (delta0, rblk0) in the format above:
+// ll[:, ma_latent == 0] = -1e20 (decoder.py:46) and the 32-latent block references
+// re-derived over the kept bins, exactly as the emission kernels derive them.  Blocks
+// without a masked bin are copied bit for bit; in the others a kept bin's ll is
+// recovered as delta0 + rblk0 in f64 (exact up to delta0's own f32 rounding).  One wave
+// per (time bin, pair of 32-latent blocks); T * L * 8 bytes + rblk traffic per mask, no
+// contraction: this is what lets log_marginal_masked run the emission GEMM once for all
+// its masks (model_selection_helper.get_downsampled_lml, :243-260).
+__global__ void __launch_bounds__(256) k_latent_mask_apply(
+    const float* __restrict__ delta0, const double* __restrict__ rblk0, int64_t T, int L, int nblk,
+    const uint8_t* __restrict__ ma_latent, float* __restrict__ delta, double* __restrict__ rblk) {
+  const int lane = threadIdx.x & 63;
+  const int npair = (nblk + 1) >> 1;
+  const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (w >= T * npair) return;               // uniform per wave
+  const int64_t t = w / npair;
+  const int l = (int)(w - t * npair) * 64 + lane;
+  const int blk = l >> 5;
+  const bool bvalid = blk < nblk;
+  const bool lvalid = l < L;
+  const bool msk = lvalid && ma_latent[l] == 0;
+  const double r0 = bvalid ? rblk0[t * nblk + blk] : 0.0;
+  const float d0 = lvalid ? delta0[t * (int64_t)L + l] : 0.f;
+  double v = msk ? -1e20 : (double)d0 + r0;
+  v = lvalid ? v : -INFINITY;
+  const float anym = half_max32(msk ? 1.f : 0.f);
+  const double mx = (double)half_max32((float)v);
+  if (!bvalid) return;                      // after the cross-lane reductions
+  if (anym > 0.f) {
+    if ((lane & 31) == 0) rblk[t * nblk + blk] = mx;
+    if (lvalid) delta[t * (int64_t)L + l] = (float)(v - mx);
+  } else {
+    if ((lane & 31) == 0) rblk[t * nblk + blk] = r0;
+    if (lvalid) delta[t * (int64_t)L + l] = d0;
+  }
+}
+
 }  // namespace pmg
 
 using namespace pmg;
@@ -328,6 +365,19 @@ int pmg_emission_poisson_f64(const float* y, const double* gconst, const double*
   dim3 grid((unsigned)((T + 15) / 16), (unsigned)((L + 63) / 64));
   hipLaunchKernelGGL(k_emission_f64, grid, dim3(256), 0, as_stream(stream), y, ma_neuron,
                      ma_is_2d, tuning64, dt, gconst, ma_latent, T, L, N, Lp, delta, rblk);
+  PMG_LAUNCH_CHECK();
+  return PMG_OK;
+}
+
+int pmg_emission_latent_mask(const float* delta0, const double* rblk0, int64_t T, int32_t L,
+                             const uint8_t* ma_latent, float* delta, double* rblk, void* stream) {
+  PMG_REQUIRE(T > 0 && L > 0 && delta0 && rblk0 && ma_latent && delta && rblk,
+              "pmg_emission_latent_mask: bad args");
+  PMG_REQUIRE(delta0 != delta && rblk0 != rblk, "pmg_emission_latent_mask: in-place is not supported");
+  const int nblk = (int)(round_up(L, 32) / 32);
+  const int64_t waves = T * ((nblk + 1) / 2);
+  hipLaunchKernelGGL(k_latent_mask_apply, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, as_stream(stream),
+                     delta0, rblk0, T, L, nblk, ma_latent, delta, rblk);
   PMG_LAUNCH_CHECK();
   return PMG_OK;
 }

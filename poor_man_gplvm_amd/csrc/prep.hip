@@ -107,6 +107,23 @@ __global__ void k_log(const float* __restrict__ x, int64_t n, float* __restrict_
   for (; i < n; i += stride) y[i] = logf(x[i]);
 }
 
+// out[t, n] = y[(t - shift[n]) mod T, n]: np.roll of every neuron's column by its own
+// shift (circular_shuffle_data, test.py:20-23).  A block walks rows t; its threads own
+// neuron columns, so each thread's shift is read once and every row write is coalesced.
+__global__ void __launch_bounds__(256) k_roll_columns(const float* __restrict__ y, int64_t T, int N,
+                                                      const int64_t* __restrict__ shift,
+                                                      float* __restrict__ out) {
+  for (int n = threadIdx.x; n < N; n += blockDim.x) {
+    int64_t s = shift[n] % T;
+    if (s < 0) s += T;
+    for (int64_t t = blockIdx.x; t < T; t += gridDim.x) {
+      int64_t src = t - s;
+      src += (src < 0) ? T : 0;
+      out[t * N + n] = y[src * N + n];
+    }
+  }
+}
+
 }  // namespace pmg
 
 using namespace pmg;
@@ -169,6 +186,15 @@ int pmg_exp(const float* logp, int64_t n, float* p, void* stream) {
   if (n == 0) return PMG_OK;
   unsigned blocks = (unsigned)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
   hipLaunchKernelGGL(k_exp, dim3(blocks), dim3(256), 0, as_stream(stream), logp, n, p);
+  PMG_LAUNCH_CHECK();
+  return PMG_OK;
+}
+
+int pmg_roll_columns(const float* y, int64_t T, int32_t N, const int64_t* shift, float* out, void* stream) {
+  PMG_REQUIRE(T > 0 && N > 0 && y && shift && out && y != out, "pmg_roll_columns: bad args");
+  const unsigned threads = (unsigned)(N >= 256 ? 256 : round_up(N, 64));
+  const unsigned blocks = (unsigned)(T < 8192 ? T : 8192);
+  hipLaunchKernelGGL(k_roll_columns, dim3(blocks), dim3(threads), 0, as_stream(stream), y, T, N, shift, out);
   PMG_LAUNCH_CHECK();
   return PMG_OK;
 }

@@ -102,14 +102,19 @@ class SpikeData:
     """Spike counts prepared once per fit (pmg_spikes_prepare)."""
 
     def __init__(self, y, ma_neuron=None, device=None):
-        lib = nat.load()
+        """y: (n_time, n_neuron) host array, or a float32 device tensor (used in place)."""
         dev = device or default_device()
-        y = np.asarray(y)
+        if isinstance(y, torch.Tensor):
+            if y.device.type != 'cuda' or y.dtype != torch.float32 or not y.is_contiguous():
+                raise ValueError("a tensor y must be a contiguous float32 device tensor")
+        else:
+            y = np.asarray(y)
         if y.ndim != 2:
-            raise ValueError(f"y must be (n_time, n_neuron), got {y.shape}")
+            raise ValueError(f"y must be (n_time, n_neuron), got {tuple(y.shape)}")
         self.T, self.N = int(y.shape[0]), int(y.shape[1])
         self.device = dev
-        self.y = torch.as_tensor(np.ascontiguousarray(y, dtype=np.float32), device=dev)
+        self.y = y if isinstance(y, torch.Tensor) else torch.as_tensor(np.ascontiguousarray(y, dtype=np.float32),
+                                                                       device=dev)
         self.Kp = _ru(self.N, 128)
         self.Np = _ru(self.N + 1, 64)
         self.Tp = _ru(self.T, 64)
@@ -128,21 +133,36 @@ class SpikeData:
         self.yq = torch.empty((self.Tp, self.Kp), dtype=torch.int8, device=dev)
         self.gconst = torch.empty(self.T, dtype=torch.float64, device=dev)
         self.yext = torch.empty((self.T, self.Np), dtype=torch.float32, device=dev)
-        flags = torch.zeros(1, dtype=torch.int32, device=dev)
-        nat.check(lib.pmg_spikes_prepare(nat.ptr(self.y), self.T, self.N, nat.ptr(self.ma),
-                                         int(self.ma_2d), nat.ptr(self.yq), self.Kp,
-                                         nat.ptr(self.gconst), nat.ptr(self.yext), self.Np,
-                                         nat.ptr(flags), nat.stream_handle()),
-                  "pmg_spikes_prepare")
-        self.flags = int(flags.item())
+        self._flags = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.ybt = None
+        self._prepare()
+        self.flags = int(self._flags.item())
         # exact int8 path: integer counts in [0,127], 0/1 mask, no per-time mask
         self.int_path = self.flags == 0 and not self.ma_2d
         # integer counts are exact in bf16: suff-stats on the bf16 MFMA (exact products)
-        self.ybt = None
         if not (self.flags & 1):
             self.ybt = torch.empty((self.Np, self.Tp), dtype=torch.int16, device=dev)
-            nat.check(lib.pmg_spikes_bf16t(nat.ptr(self.yext), self.T, self.Np, nat.ptr(self.ybt), self.Tp,
-                                           nat.stream_handle()), "pmg_spikes_bf16t")
+            self._transpose()
+
+    def _prepare(self):
+        nat.check(nat.load().pmg_spikes_prepare(nat.ptr(self.y), self.T, self.N, nat.ptr(self.ma),
+                                                int(self.ma_2d), nat.ptr(self.yq), self.Kp,
+                                                nat.ptr(self.gconst), nat.ptr(self.yext), self.Np,
+                                                nat.ptr(self._flags), nat.stream_handle()),
+                  "pmg_spikes_prepare")
+
+    def _transpose(self):
+        nat.check(nat.load().pmg_spikes_bf16t(nat.ptr(self.yext), self.T, self.Np, nat.ptr(self.ybt), self.Tp,
+                                              nat.stream_handle()), "pmg_spikes_bf16t")
+
+    def refresh(self):
+        """Re-derive the prepared forms after self.y was rewritten in place on the device
+        with the same multiset of counts per neuron (a permutation in time, such as
+        pmg_roll_columns): the int8 / bf16 eligibility flags cannot change, so this
+        stays on the stream without a host sync."""
+        self._prepare()
+        if self.ybt is not None:
+            self._transpose()
 
 
 class KernelTimer:
@@ -416,6 +436,31 @@ class DeviceEM:
         with self._t('emission_rowref'):
           nat.check(self.lib.pmg_emission_rowref(nat.ptr(self.rblk), self.T, self.nblk, float(likelihood_scale),
                                                  nat.ptr(self.phi), nat.ptr(self.mref), sh), "pmg_emission_rowref")
+
+    def emission_unmasked(self, dt=1.0):
+        """The emission contraction without a latent mask into fresh (delta0, rblk0)
+        buffers, to be masked per use by emission_from."""
+        saved, self.ma_latent = self.ma_latent, None
+        try:
+            with self._t('emission'):
+                self._emission_call(self.sp, nat.stream_handle(), dt)
+        finally:
+            self.ma_latent = saved
+        return self.delta.clone(), self.rblk.clone()
+
+    def emission_from(self, delta0, rblk0, ma_latent_u8, likelihood_scale=1.0):
+        """(delta, rblk) = (delta0, rblk0) under the latent mask ma_latent_u8 ((L,) uint8
+        device tensor; pmg_emission_latent_mask), then the row reference."""
+        if tuple(ma_latent_u8.shape) != (self.L,) or ma_latent_u8.dtype != torch.uint8:
+            raise ValueError(f"ma_latent_u8 must be a ({self.L},) uint8 tensor")
+        sh = nat.stream_handle()
+        with self._t('emission_mask'):
+            nat.check(self.lib.pmg_emission_latent_mask(nat.ptr(delta0), nat.ptr(rblk0), self.T, self.L,
+                                                        nat.ptr(ma_latent_u8), nat.ptr(self.delta),
+                                                        nat.ptr(self.rblk), sh), "pmg_emission_latent_mask")
+        with self._t('emission_rowref'):
+            nat.check(self.lib.pmg_emission_rowref(nat.ptr(self.rblk), self.T, self.nblk, float(likelihood_scale),
+                                                   nat.ptr(self.phi), nat.ptr(self.mref), sh), "pmg_emission_rowref")
 
     def _emission_call(self, sp, sh, dt):
         if self.noise_std is not None:

@@ -18,10 +18,7 @@ pytestmark = pytest.mark.gpu
 
 def _smooth_data(N, L, T):
     """Spikes from a latent path without jumps (the latent-only model's own
-    generative process, core.py:919-1019).  The device scan bands the continuous
-    kernel at weights 1e-30 below its centre; a latent-only model decoding data
-    with latent jumps wider than that band differs from the reference's dense
-    log-domain kernel."""
+    generative process, core.py:919-1019)."""
     d = make(N, L, T)
     lat = O.sample_latent(T, L, np.random.default_rng(1), 1.0, 0.0, 1.0)
     d['y'] = O.sample_spikes(d['tuning'], lat[:, 1], np.random.default_rng(2)).astype(np.float32)
@@ -36,14 +33,9 @@ def test_log_marginal_masked_vs_oracle(model, N, L, T, frac):
     d = make(N, L, T) if model == "jump" else _smooth_data(N, L, T)
     cls = P.PoissonGPLVMJump1D if model == "jump" else P.PoissonGPLVM1D
     m = cls(N, n_latent_bin=L, tuning_lengthscale=10.)
+    # random downsampling leaves gaps of many bins between kept latents: the latent-only
+    # model crosses them on the dense log-domain scans with the exact far-move weights
     masks = MS.downsample_latent_masks(L, frac, 4, key=3)
-    if model == "latentonly":
-        # keep the kept bins within the continuous-kernel band of each other (the
-        # device scan's limit for a model without a jump state; see the raise test)
-        masks = np.zeros((4, L))
-        for r in range(4):
-            masks[r, ::3] = 1
-            masks[r, np.random.default_rng(r).choice(L, int(L * frac), replace=False)] = 1
     got = m.log_marginal_masked(d['y'], masks, tuning=d['tuning'])
     if model == "jump":
         ref = O.downsampled_lml(d['y'], d['tuning'], masks)[0]
@@ -51,6 +43,8 @@ def test_log_marginal_masked_vs_oracle(model, N, L, T, frac):
         _, logK = O.create_transition_prob_latent_1d(L, 1.0)
         ref = np.array([O.smooth_latent_only(d['y'], d['tuning'], logK, ma_latent=mk)[1] for mk in masks])
     np.testing.assert_allclose(got, ref, rtol=1e-7)
+    # the batched path (one emission, per-mask pmg_emission_latent_mask) vs one full
+    # masked decode per mask: the same up to delta's f32 rounding
     full = [m.decode_latent(d['y'], tuning=d['tuning'], ma_latent=mk)['log_marginal_final'] for mk in masks]
     np.testing.assert_allclose(got, full, rtol=1e-9)
     if model == "jump":
@@ -105,3 +99,60 @@ def test_model_selection_one_split_end_to_end():
     lz = res['best_model_l'][int(tab['log_marginal_test_best_index'].values[best_row])].decode_latent(y_test)
     np.testing.assert_allclose(tab['log_marginal_test_best_value'].values[best_row], lz['log_marginal_final'],
                                rtol=1e-12)
+
+
+@pytest.mark.parametrize("path", ["int8", "f64", "gaussian", "dt"])
+def test_latent_mask_apply_matches_masked_emission(path):
+    """pmg_emission_latent_mask on the unmasked emission == the emission run with the
+    mask: masked bins -1e20, kept bins' ll to 2 f32 ulps of delta, unmasked blocks
+    bit-identical; includes fully masked 32-bin blocks and a ragged last block."""
+    import torch
+    from poor_man_gplvm_amd import _native as nat
+    from poor_man_gplvm_amd.engine import DeviceEM, SpikeData
+    N, L, T = 37, 150, 900
+    d = make(N, L, T)
+    rng = np.random.default_rng(2)
+    y = d['y'] if path != "gaussian" else (d['y'] + rng.normal(size=d['y'].shape)).astype(np.float32)
+    ma = (rng.random(N) > 0.2).astype(np.float32) * (1.7 if path == "f64" else 1.0)
+    ml = (rng.random(L) > 0.4).astype(np.uint8)
+    ml[32:64] = 0                 # a fully masked block
+    ml[96:128] = 1                # a block without masked bins
+    ml[149] = 0                   # ragged last block (150 = 4 * 32 + 22)
+    eng = DeviceEM(SpikeData(y, ma), L)
+    if path == "gaussian":
+        eng.noise_std = 0.5
+    eng.set_tuning(d['tuning'])
+    sh = nat.stream_handle()
+
+    def emit(mask):
+        eng.set_ma_latent(mask)
+        if path == "dt":
+            dtt = torch.as_tensor(rng.uniform(0.5, 1.5, T), device='cuda')
+            nat.check(eng.lib.pmg_emission_poisson_dt(nat.ptr(eng.sp.y), nat.ptr(eng.sp.gconst),
+                                                      nat.ptr(eng.tuning64), nat.ptr(eng.sp.ma), 0,
+                                                      nat.ptr(eng.ma_latent), nat.ptr(dtt), T, L, N,
+                                                      nat.ptr(eng.delta), nat.ptr(eng.rblk), sh), "dt")
+        else:
+            eng._emission_call(eng.sp, sh, 1.0)
+        return eng.delta.clone(), eng.rblk.clone()
+
+    rng_state = rng.bit_generator.state
+    d0, r0 = emit(None)
+    rng.bit_generator.state = rng_state      # the same per-bin dt for both calls
+    dm, rm = emit(ml)
+    mu8 = torch.as_tensor(ml, device='cuda')
+    da, ra = torch.empty_like(d0), torch.empty_like(r0)
+    nat.check(eng.lib.pmg_emission_latent_mask(nat.ptr(d0), nat.ptr(r0), T, L, nat.ptr(mu8), nat.ptr(da),
+                                               nat.ptr(ra), sh), "pmg_emission_latent_mask")
+    d0, dm, rm, da, ra = (x.cpu().numpy() for x in (d0, dm, rm, da, ra))
+    blk = np.arange(L) // 32
+    llm = dm.astype(np.float64) + rm[:, blk]
+    lla = da.astype(np.float64) + ra[:, blk]
+    keep = ml.astype(bool)
+    assert np.all(lla[:, ~keep] <= -1e19) and np.all(llm[:, ~keep] <= -1e19)
+    # kept bins: d0's own rounding (its block max may have been a masked bin) + delta's
+    ulp = np.spacing(np.maximum(np.abs(d0[:, keep]), np.abs(dm[:, keep])).astype(np.float32)).astype(np.float64)
+    assert np.all(np.abs(lla[:, keep] - llm[:, keep]) <= 1.5 * ulp)
+    clean = np.array([ml[b * 32:(b + 1) * 32].all() for b in range(rm.shape[1])])
+    np.testing.assert_array_equal(ra[:, clean], rm[:, clean])
+    np.testing.assert_array_equal(da[:, np.repeat(clean, 32)[:L]], dm[:, np.repeat(clean, 32)[:L]])
