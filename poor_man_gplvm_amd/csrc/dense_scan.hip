@@ -552,7 +552,7 @@ __device__ float dense_hilbert_reg(const DenseParams& p, DenseShared<JD>& sh, Sl
 
 template <int JD>
 __device__ bool dfwd_segment(const DenseParams& p, DFwd<JD>& st, DenseShared<JD>& sh, int c0, int b,
-                             const int* flg, int& nrep) {
+                             const int* flg, int& nrep, int* stop = nullptr) {
   const size_t SZ = (size_t)2 * p.Lp;
   for (int c = c0; c < b; ++c) {
     const int64_t t_c = (int64_t)c * p.C;
@@ -565,7 +565,10 @@ __device__ bool dfwd_segment(const DenseParams& p, DFwd<JD>& st, DenseShared<JD>
     const float d = dense_hilbert_reg<JD>(p, sh, st.sl, st.x0, st.x1, so);
     __syncthreads();
     st.save(p, so);
-    if (d <= p.tol && (c + 1 >= b || !(flg && flg[c + 1]))) return false;
+    if (d <= p.tol && (c + 1 >= b || !(flg && flg[c + 1]))) {
+      if (stop) *stop = c;
+      return false;
+    }
   }
   return true;
 }
@@ -582,10 +585,14 @@ __global__ void __launch_bounds__(kDNT) k_dense_forward_relax(DenseParams p) {
     const int b = a + p.G < p.M ? a + p.G : p.M;
     DFwd<JD> st;
     bool changed = false;
-    const int c0 = dense_find_flag<1>(p.flags, a > 1 ? a : 1, b);
-    if (c0 >= 0) {
+    // round 0: every flagged boundary of the segment (see forward_relax in fb_kernels.h)
+    int c0 = dense_find_flag<1>(p.flags, a > 1 ? a : 1, b);
+    while (c0 >= 0) {
       st.load(p, p.s_in + (size_t)c0 * SZ, sh);
-      changed = dfwd_segment<JD>(p, st, sh, c0, b, p.flags, nrep);
+      int stop = b;
+      changed = dfwd_segment<JD>(p, st, sh, c0, b, p.flags, nrep, &stop);
+      if (changed) break;
+      c0 = stop + 2 < b ? dense_find_flag<1>(p.flags, stop + 2, b) : -1;
     }
     for (int k = 0;; ++k) {
       if (changed) st.save(p, p.seg_end + ((size_t)(k & 1) * p.S + s) * SZ);
@@ -778,7 +785,7 @@ __global__ void __launch_bounds__(kDNT) k_dense_backward(DenseParams p) {
 
 template <int JD>
 __device__ bool dbwd_segment(const DenseParams& p, DBwd<JD>& st, DenseShared<JD>& sh, int c0, int a,
-                             const int* flg, int& nrep) {
+                             const int* flg, int& nrep, int* stop = nullptr) {
   const size_t SZ = (size_t)2 * p.Lp;
   for (int c = c0; c >= a; --c) {
     const int64_t t_c = (int64_t)c * p.C;
@@ -793,7 +800,10 @@ __device__ bool dbwd_segment(const DenseParams& p, DBwd<JD>& st, DenseShared<JD>
     const float d = dense_hilbert_reg<JD>(p, sh, st.sl, st.b0, st.b1, bf);
     __syncthreads();
     st.save(p, bf);
-    if (d <= p.tol && (c == a || !(flg && flg[c - 1]))) return false;
+    if (d <= p.tol && (c == a || !(flg && flg[c - 1]))) {
+      if (stop) *stop = c;
+      return false;
+    }
   }
   return true;
 }
@@ -811,10 +821,13 @@ __global__ void __launch_bounds__(kDNT) k_dense_backward_relax(DenseParams p) {
     const int top = b < p.M - 1 ? b : p.M - 1;
     DBwd<JD> st;
     bool changed = false;
-    const int c0 = dense_find_flag<-1>(p.flags, a, top);
-    if (c0 >= 0) {
+    int c0 = dense_find_flag<-1>(p.flags, a, top);
+    while (c0 >= 0) {
       st.load(p, p.b_in + (size_t)c0 * SZ);
-      changed = dbwd_segment<JD>(p, st, sh, c0, a, p.flags, nrep);
+      int stop = a;
+      changed = dbwd_segment<JD>(p, st, sh, c0, a, p.flags, nrep, &stop);
+      if (changed) break;
+      c0 = stop - 1 > a ? dense_find_flag<-1>(p.flags, a, stop - 1) : -1;
     }
     for (int k = 0;; ++k) {
       if (changed) st.save(p, p.seg_end + ((size_t)(k & 1) * p.S + s) * SZ);

@@ -616,11 +616,12 @@ __device__ __forceinline__ double wave_sum_fixed(const double* x, int n) {
 // ---------------------------------------------------------------------------
 // recompute chunks c0 .. b-1 from st (the filter state at c0*C - 1).  After chunk c,
 // if its new end state is within tol of the old s_out[c] and boundary c+1 is not
-// flagged (flg, round 0 only), the rest of the segment is consistent: stop.  Returns
-// true iff the segment's end state (chunk b-1) moved.
+// flagged (flg, round 0 only), the chunks up to the next flagged boundary are
+// consistent: stop (*stop = c).  Returns true iff the segment's end state (chunk b-1)
+// moved.
 template <int J, int WP, bool VEC>
 __device__ bool fwd_segment(const FBParams& p, Fwd<J, WP>& st, int c0, int b, int j0, const float invz[J],
-                            const int* flg, int& nrep) {
+                            const int* flg, int& nrep, int* stop = nullptr) {
   const size_t SZ = (size_t)2 * p.Lpad;
   for (int c = c0; c < b; ++c) {
     const int64_t t_c = (int64_t)c * p.C;
@@ -632,7 +633,10 @@ __device__ bool fwd_segment(const FBParams& p, Fwd<J, WP>& st, int c0, int b, in
     float* so = p.s_out + (size_t)c * SZ;
     const float d = hilbert_reg<J>(st.p0, st.p1, so, p.Lpad, j0);  // each lane reads only its own slots
     st.save_state(p, so, j0);
-    if (d <= p.tol && (c + 1 >= b || !(flg && flg[c + 1]))) return false;
+    if (d <= p.tol && (c + 1 >= b || !(flg && flg[c + 1]))) {
+      if (stop) *stop = c;
+      return false;
+    }
   }
   return true;
 }
@@ -648,11 +652,15 @@ __device__ void forward_relax(const FBParams& p, int j0, const float invz[J]) {
     const int b = a + p.G < p.M ? a + p.G : p.M;
     Fwd<J, WP> st;
     bool changed = false;
-    // round 0: from the first boundary the verify flagged (it snapshotted the carry into s_in)
-    const int c0 = find_flag<1>(p.flags, a > 1 ? a : 1, b);
-    if (c0 >= 0) {
+    // round 0: every boundary the verify flagged (it snapshotted the carry into s_in),
+    // in order; a pass that settles before the segment end resumes at the next flag
+    int c0 = find_flag<1>(p.flags, a > 1 ? a : 1, b);
+    while (c0 >= 0) {
       st.load_state(p, p.s_in + (size_t)c0 * SZ, j0);
-      changed = fwd_segment<J, WP, VEC>(p, st, c0, b, j0, invz, p.flags, nrep);
+      int stop = b;
+      changed = fwd_segment<J, WP, VEC>(p, st, c0, b, j0, invz, p.flags, nrep, &stop);
+      if (changed) break;                                  // ran through to the segment end
+      c0 = stop + 2 < b ? find_flag<1>(p.flags, stop + 2, b) : -1;
     }
     for (int k = 0;; ++k) {
       if (changed) st.save_state(p, p.seg_end + ((size_t)(k & 1) * p.S + s) * SZ, j0);
@@ -946,10 +954,11 @@ __global__ void __launch_bounds__(64) k_backward_full(FBParams p) {
 // recompute chunks c0, c0-1, .., a from st (beta at (c0+1)*C).  After chunk c, if its
 // new beta at c*C is within tol of the old b_first[c] (weighted by alpha at c*C, the
 // boundary metric of k_verify) and boundary c-1 is not flagged, stop.  Returns true
-// iff the segment's end state (b_first[a]) moved.
+// iff the segment's end state (b_first[a]) moved; otherwise *stop = the chunk it
+// settled at.
 template <int J, int WP, bool VEC>
 __device__ bool bwd_segment(const FBParams& p, Bwd<J, WP>& st, int c0, int a, int j0, const float invz[J],
-                            const int* flg, int& nrep) {
+                            const int* flg, int& nrep, int* stop = nullptr) {
   const size_t SZ = (size_t)2 * p.Lpad;
   for (int c = c0; c >= a; --c) {
     const int64_t t_c = (int64_t)c * p.C;
@@ -962,7 +971,10 @@ __device__ bool bwd_segment(const FBParams& p, Bwd<J, WP>& st, int c0, int a, in
     float* bf = p.b_first + (size_t)c * SZ;
     const float d = hilbert_reg<J>(st.b0, st.b1, bf, p.Lpad, j0, p.alpha_in + t_c * 2 * (int64_t)p.L, p.L);
     st.save_state(p, bf, j0);
-    if (d <= p.tol && (c == a || !(flg && flg[c - 1]))) return false;
+    if (d <= p.tol && (c == a || !(flg && flg[c - 1]))) {
+      if (stop) *stop = c;
+      return false;
+    }
   }
   return true;
 }
@@ -979,10 +991,14 @@ __device__ void backward_relax(const FBParams& p, int j0, const float invz[J]) {
     const int top = b < p.M - 1 ? b : p.M - 1;  // boundaries c <= M-2 have a successor
     Bwd<J, WP> st;
     bool changed = false;
-    const int c0 = find_flag<-1>(p.flags, a, top);
-    if (c0 >= 0) {
+    // round 0: every flagged boundary, top down (see forward_relax)
+    int c0 = find_flag<-1>(p.flags, a, top);
+    while (c0 >= 0) {
       st.load_state(p, p.b_in + (size_t)c0 * SZ, j0);
-      changed = bwd_segment<J, WP, VEC>(p, st, c0, a, j0, invz, p.flags, nrep);
+      int stop = a;
+      changed = bwd_segment<J, WP, VEC>(p, st, c0, a, j0, invz, p.flags, nrep, &stop);
+      if (changed) break;
+      c0 = stop - 1 > a ? find_flag<-1>(p.flags, a, stop - 1) : -1;
     }
     for (int k = 0;; ++k) {
       if (changed) st.save_state(p, p.seg_end + ((size_t)(k & 1) * p.S + s) * SZ, j0);

@@ -150,9 +150,12 @@ def test_latent_mask_apply_matches_masked_emission(path):
     lla = da.astype(np.float64) + ra[:, blk]
     keep = ml.astype(bool)
     assert np.all(lla[:, ~keep] <= -1e19) and np.all(llm[:, ~keep] <= -1e19)
-    # kept bins: d0's own rounding (its block max may have been a masked bin) + delta's
+    # kept bins: d0's own rounding (its block max may have been a masked bin) + delta's;
+    # the f64 / Gaussian / per-bin-dt emissions keep an exact f64 block max, the mask
+    # pass an f32-rounded one (as the int8 emission): a residual of ~2^-24 ulp_f32(ll)
     ulp = np.spacing(np.maximum(np.abs(d0[:, keep]), np.abs(dm[:, keep])).astype(np.float32)).astype(np.float64)
-    assert np.all(np.abs(lla[:, keep] - llm[:, keep]) <= 1.5 * ulp)
+    err = np.abs(lla[:, keep] - llm[:, keep])
+    assert np.all(err <= 1.5 * ulp + 1e-13 * np.abs(llm[:, keep])), (err / (ulp + 1e-300)).max()
     clean = np.array([ml[b * 32:(b + 1) * 32].all() for b in range(rm.shape[1])])
     np.testing.assert_array_equal(ra[:, clean], rm[:, clean])
     np.testing.assert_array_equal(da[:, np.repeat(clean, 32)[:L]], dm[:, np.repeat(clean, 32)[:L]])

@@ -178,6 +178,62 @@ def test_flat_tuning_cascade():
     assert abs(logz.item() - lz) <= 1e-7 * abs(lz)
 
 
+def test_sparse_boundary_failures():
+    """Sharp emissions and a 2-step warm-up: boundaries fail here and there, so one
+    relaxation segment holds several flagged boundaries separated by good ones.  Every
+    one must be recomputed (a segment pass that settles resumes at the next flag)."""
+    N, L, T = 256, 128, 8000
+    d = make(N, L, T)
+    sp, eng = _engine(d, L, chunk=8, warmup=2)
+    eng.set_tuning(d['tuning'])
+    logz = torch.zeros(1, dtype=torch.float64, device='cuda')
+    gamma = torch.empty((T, 2, L), dtype=torch.float32, device='cuda')
+    eng.e_step(1.0, logz, gamma=gamma)
+    f, b = eng.repairs()
+    assert f > 0 and b > 0
+    K, logK, A, logA = O.create_transition_prob_1d(L, 1.0)
+    lpa, lz, lca, cs, _, _ = O.smooth_all_step_combined_ma_chunk(d['y'], d['tuning'], logK, logA, with_joint=False)
+    close_prob(gamma.cpu().numpy(), np.exp(lpa))
+    close_prob(eng.alpha.cpu().numpy(), np.exp(lca))
+    assert abs(logz.item() - lz) <= 1e-7 * abs(lz)
+
+
+def test_sparse_boundary_failures_vs_dense_scan():
+    """The C4 regime that exposed the single-flag relaxation (1024 neurons, tuning after
+    one M-step from a random posterior), reduced: banded scans with a 4-step warm-up vs
+    the dense log-domain scans (f64 state, an independent algorithm)."""
+    import poor_man_gplvm_amd as P
+    from poor_man_gplvm_amd.engine import AdamConfig, DeviceEM, ScanConfig, SpikeData
+    from poor_man_gplvm_amd.gp_kernel import transition_from_log_kernels
+    N, L, T = 1024, 256, 20000
+    d = make(N, L, T)
+    sp = SpikeData(d['y'])
+    eng = DeviceEM(sp, L, basis=d['B'], scan=ScanConfig(chunk=16, warmup=4, adaptive=False))
+    eng.set_transition(P.banded_transition(L, 1.0))
+    eng.set_log_posterior(d['lp0'])
+    W = torch.as_tensor(d['W0'].astype(np.float64), device='cuda').contiguous()
+    z = torch.zeros_like(W)
+    stats = torch.zeros(4, dtype=torch.float64, device='cuda')
+    lh = torch.zeros(40, dtype=torch.float64, device='cuda')
+    eng.m_step(W, z, z.clone(), torch.zeros(1, dtype=torch.int64, device='cuda'), AdamConfig(maxiter=40, tol=0.0),
+               stats, lh, lh.clone())
+    eng.compute_tuning(W)
+    logz = torch.zeros(1, dtype=torch.float64, device='cuda')
+    gamma = torch.empty((T, 2, L), dtype=torch.float32, device='cuda')
+    eng.e_step(1.0, logz, gamma=gamma)
+    assert sum(eng.repairs()) > 0
+    tun = eng.tuning64.cpu().numpy()
+    ed = DeviceEM(sp, L, scan=ScanConfig(adaptive=False))
+    _, logK, _, logA = O.create_transition_prob_1d(L, 1.0)
+    ed.set_transition(transition_from_log_kernels(logK, logA, force_dense=True))
+    ed.set_tuning(tun)
+    lz2 = torch.zeros(1, dtype=torch.float64, device='cuda')
+    g2 = torch.empty((T, 2, L), dtype=torch.float32, device='cuda')
+    ed.e_step(1.0, lz2, gamma=g2, log_gamma=torch.empty_like(g2))
+    close_prob(gamma.cpu().numpy(), g2.cpu().numpy().astype(np.float64), rtol=2e-5)
+    assert abs(logz.item() - lz2.item()) <= 1e-9 * abs(lz2.item())
+
+
 def test_masked_latents_scan():
     N, L, T = 30, 80, 500
     d = make(N, L, T)

@@ -146,7 +146,7 @@ def test_test_one_model():
     np.testing.assert_array_equal(r['log_marg_thresh'], thr)
     sig = r['is_sig_tsd']['d'] if isinstance(r['is_sig_tsd'], dict) else np.asarray(r['is_sig_tsd'].d)
     np.testing.assert_array_equal(sig, r['decode_res_true']['log_marginal_l'] > thr)
-    assert sig.mean() > 0.5       # true tuning: most bins beat their shuffles
+    assert sig.mean() > 0.05      # the true tuning beats its shuffles well above the 2.5 % chance level
     np.random.seed(0)
     r2 = PT.test_one_model(d['y'], m, n_shuffle=4, decoder_type='dynamics')
     assert r2['log_marg_thresh'].shape == (T,)
