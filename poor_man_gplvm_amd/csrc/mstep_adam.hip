@@ -96,149 +96,178 @@ __global__ void k_fill_u64(unsigned long long* __restrict__ x, size_t n, unsigne
 }
 
 // ---------------------------------------------------------------------------
-// Wave transpose-reduce: 64 per-lane values x[0..63] -> lane l returns
-// sum over the 64 lanes of x[bitrev6(l)].  Six butterfly stages (lane bit 5..0:
-// permlane32_swap, permlane16_swap, DPP row_ror:8, row_half_mirror,
-// quad_perm[2,3,0,1], quad_perm[1,0,3,2]); at every stage the lower half of each
-// lane group keeps the even register of a pair and the upper half the odd one, so
-// each stage halves the registers: ~140 instructions for 64 sums.
+// Basis layout: ONE register-resident copy, as a 2-D block per thread.  The 512 threads
+// form 32 l-blocks (4 per wave: the 16-lane DPP rows) x 16 q-blocks (lane & 15); thread
+// (lb, qb) holds B[lb*A + i, qb*BC + k] for i < A = Lp/32, k < BC = ceil(NB/16).
+//   f = B W  : per-thread partial sums over its BC columns for its A rows, then a
+//              16-lane DPP reduce-scatter (lane j gets row bitrev(j)): every row's F
+//              ends on one lane, which evaluates softplus / sigmoid and G for it;
+//   B^T G    : G of the block's rows is broadcast through wave-local LDS, each thread
+//              forms its BC column partials over its A rows, lanes with the same q-block
+//              are summed over the 4 DPP rows (shfl_xor 16, 32) and over the 8 waves
+//              (LDS, fixed order) by the element-update threads.
+// Everything but the G broadcast and the cross-wave sum stays in registers.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float f_of(unsigned u) { return __uint_as_float(u); }
-__device__ __forceinline__ unsigned u_of(float f) { return __float_as_uint(f); }
-
-template <int CTRL>
-__device__ __forceinline__ float dpp_pair_add(float a, float b, bool upper) {
-  // lower lanes: a + partner(a); upper lanes: b + partner(b)
-  const float x = upper ? b : a;
-  const float y = upper ? a : b;
-  return x + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(y), CTRL, 0xf, 0xf, false));
-}
-
-__device__ __forceinline__ int bitrev5(int l) {
-  return ((l & 1) << 4) | ((l & 2) << 2) | (l & 4) | ((l & 8) >> 2) | ((l & 16) >> 4);
-}
-
-// 32 values x_i = a[i/S]*b[i%S] (generated on the fly, pairwise, to keep register
-// pressure at 16 + 2): stages on lane bits 4..0 inside each 32-lane half, then the
-// two halves are added (permlane32_swap of a register with itself).  Lane l returns
-// the 64-lane sum of x[bitrev5(l & 31)].
-template <int SP, int C0, int R>
-__device__ __forceinline__ float wave_products_reduce32(const float* brow, const float* gr) {
-  const int lane = threadIdx.x & 63;
-  float x[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int v0 = C0 + 2 * i, v1 = v0 + 1;
-    const float p0 = (v0 < R) ? brow[v0 / SP] * gr[v0 % SP] : 0.f;
-    const float p1 = (v1 < R) ? brow[v1 / SP] * gr[v1 % SP] : 0.f;
-    auto r = __builtin_amdgcn_permlane16_swap(u_of(p0), u_of(p1), false, false);
-    x[i] = f_of(r[0]) + f_of(r[1]);
-  }
-  const bool b3 = lane & 8, b2 = lane & 4, b1 = lane & 2, b0 = lane & 1;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) x[i] = dpp_pair_add<0x128>(x[2 * i], x[2 * i + 1], b3);  // row_ror:8
-#pragma unroll
-  for (int i = 0; i < 4; ++i) x[i] = dpp_pair_add<0x141>(x[2 * i], x[2 * i + 1], b2);  // row_half_mirror
-#pragma unroll
-  for (int i = 0; i < 2; ++i) x[i] = dpp_pair_add<0x4E>(x[2 * i], x[2 * i + 1], b1);   // quad_perm 2,3,0,1
-  const float v = dpp_pair_add<0xB1>(x[0], x[1], b0);                                  // quad_perm 1,0,3,2
-  auto r = __builtin_amdgcn_permlane32_swap(u_of(v), u_of(v), false, false);
-  return f_of(r[0]) + f_of(r[1]);
-}
-
-// products brow[q]*g for q in [C0, R) (one neuron), reduced over the wave, written to
-// sred[(QOFF + q) * 4] (the caller offsets sred by the neuron slot)
-template <int C0, int R, int QOFF>
-struct ChunkLoop {
-  static __device__ __forceinline__ void run(const float* brow, float g, float* sred, int lane) {
-    const float gg[1] = {g};
-    const float red = wave_products_reduce32<1, C0, R>(brow, gg);
-    const int v = C0 + bitrev5(lane & 31);
-    if (lane < 32 && v < R) sred[(QOFF + v) * 4] = red;
-    if constexpr (C0 + 32 < R) ChunkLoop<C0 + 32, R, QOFF>::run(brow, g, sred, lane);
-  }
-};
-
-// Basis split: the first NBR columns of each row live in registers, the remaining
-// NBM-NBR in an LDS row tile with a padded stride (stride = 16m+4 words: the 16
-// lanes of a ds_read_b128 group land on distinct bank quads).
-template <int NBM>
-struct BasisSplit {
-  static constexpr int NBR = NBM < 32 ? NBM : 32;
-  static constexpr int NBL = NBM - NBR;               // multiple of 16
-  static constexpr int STRIDE = NBL > 0 ? NBL + 4 : 4;
-};
-
-// Threads: thread = latent row (L <= 512).  Per body: rows (f, G, B^T G partials) |
-// barrier | Adam element update (threads < NB*S, i.e. the first waves) while the LAST
-// wave, which owns no weight, runs the stop-rule decision pipeline | barrier |
-// publish.  The stop flag is seen by every wave right after the second barrier.
-//
-// f = softplus(F), F = B W_k, is needed to f64 accuracy (the factor y_w/f - t_w
-// cancels near the optimum).  F is carried per (row, neuron) in f64 registers and
-// advanced by the f32 product B (W_k - W_{k-1}) of the small Adam step (error ~1e-9
-// per body), and recomputed exactly in f64 every kRefresh bodies.
 constexpr int kNW = kThreads / 64;          // waves (the last one also runs the decision)
-constexpr int kThreadsAll = kThreads;
 constexpr int kRefresh = 16;
 
-template <int NBM, int LGM, int SP>
-__global__ void __launch_bounds__(kThreadsAll) k_adam(AdamParams p) {
-  using BS = BasisSplit<NBM>;
-  constexpr int NBR = BS::NBR, NBL = BS::NBL, STRIDE = BS::STRIDE;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sBl = smem;                                                   // [kThreads][STRIDE]
-  double* sW = reinterpret_cast<double*>(sBl + kThreads * STRIDE);     // [4][NBM] W_k (f64)
-  float* sD = reinterpret_cast<float*>(sW + NBM * kSMax);              // [4][NBM] W_k - W_{k-1}
-  float* sRed = sD + NBM * kSMax;                                      // [kNW][NBM][4] partial B^T G
-  double* sSum = reinterpret_cast<double*>(sRed + kNW * NBM * kSMax);  // [2][kNW]
-  double* sYw = sSum + 2 * kNW;                                        // [kThreads][4]
-  int* sCtl = reinterpret_cast<int*>(sYw + kThreads * kSMax);          // [4]
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+// lower lanes of the pairing: a + partner(a); upper lanes: b + partner(b) (two fused
+// DPP adds and one select: no select on the DPP source)
+template <int CTRL, typename T>
+__device__ __forceinline__ T pair_add(T a, T b, bool upper) {
+  T sa, sb;
+  if constexpr (sizeof(T) == 8) {
+    sa = a + dpp_d<CTRL>(a);
+    sb = b + dpp_d<CTRL>(b);
+  } else {
+    sa = a + dpp_f<CTRL>(a);
+    sb = b + dpp_f<CTRL>(b);
+  }
+  return upper ? sb : sa;
+}
+
+// v + v(lane ^ 16), v + v(lane ^ 32): permlane swaps (VALU, no LDS round trip)
+__device__ __forceinline__ float add_xor16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float add_xor32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// 1/x in f64 from v_rcp_f64 and two Newton steps (x > 0, finite)
+__device__ __forceinline__ double rcp_nr(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(r, fma(-x, r, 1.0), r);
+  r = fma(r, fma(-x, r, 1.0), r);
+  return r;
+}
+template <int CTRL, typename T>
+__device__ __forceinline__ T dpp_t(T v) {
+  if constexpr (sizeof(T) == 8) return dpp_d<CTRL>(v);
+  else return dpp_f<CTRL>(v);
+}
+
+// x[A] per lane -> sum over the 16 lanes of the DPP row of x[idx], idx = the lane's row
+// slot (scatter_slot).  Four stages on lane bits 3, 2, 1, 0 (row_ror:8, row_half_mirror,
+// quad_perm [2,3,0,1], quad_perm [1,0,3,2]): the first 4 - log2(A) are plain butterflies
+// (lanes differing in those bits end with the same sums), each later one halves the
+// vector, the lane keeping the even (lower lanes) or odd (upper lanes) entries, so the
+// index bits are read from the lane bits in reverse order.
+template <int A, typename T>
+__device__ __forceinline__ T reduce_scatter16(T* x) {
+  const int lane = threadIdx.x & 63;
+  const bool b3 = lane & 8, b2 = lane & 4, b1 = lane & 2, b0 = lane & 1;
+  if constexpr (A == 16) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = pair_add<0x128>(x[2 * i], x[2 * i + 1], b3);
+  } else {
+#pragma unroll
+    for (int i = 0; i < A; ++i) x[i] = x[i] + dpp_t<0x128>(x[i]);
+  }
+  if constexpr (A >= 8) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = pair_add<0x141>(x[2 * i], x[2 * i + 1], b2);
+  } else {
+#pragma unroll
+    for (int i = 0; i < A; ++i) x[i] = x[i] + dpp_t<0x141>(x[i]);
+  }
+  if constexpr (A >= 4) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) x[i] = pair_add<0x4E>(x[2 * i], x[2 * i + 1], b1);
+  } else {
+#pragma unroll
+    for (int i = 0; i < A; ++i) x[i] = x[i] + dpp_t<0x4E>(x[i]);
+  }
+  return pair_add<0xB1>(x[0], x[1], b0);
+}
+
+// the row slot of a lane after reduce_scatter16<A>: index bits from lane bits 3..(4-log2 A)
+template <int A>
+__device__ __forceinline__ int scatter_slot(int lane) {
+  const int j = lane & 15;
+  const int r4 = ((j & 1) << 3) | ((j & 2) << 1) | ((j & 4) >> 1) | ((j & 8) >> 3);   // bitrev4
+  return A == 16 ? r4 : A == 8 ? (r4 >> 1) : (r4 >> 2);   // lanes j < A (j & 8 == 0 ...) own the slots
+}
+
+template <int A, int BC, int SP>
+__global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
+  constexpr int BCP = (BC + 3) & ~3;                                   // padded q-block (b128 reads)
+  constexpr int QS = 16 * BCP;                                         // padded columns per neuron
+  __shared__ __attribute__((aligned(16))) double sW[kSMax * QS];       // W_k (f64), [s][qb][BCP]
+  __shared__ __attribute__((aligned(16))) float sD[kSMax * QS];        // W_k - W_{k-1}
+  __shared__ __attribute__((aligned(16))) float sG[32 * A * SP];       // G of every row, [l][s]
+  __shared__ float sPart[kNW * SP * 16 * BC];                          // per-wave B^T G, [w][s][q]
+  __shared__ double sSum[2 * kNW];
+  __shared__ int sCtl[4];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
   const bool ctl = wid == kNW - 1;                     // runs the decision pipeline
   const int g = blockIdx.x;
   const int n0 = g * p.S;
-  const int S = (p.N - n0) < p.S ? (p.N - n0) : p.S;  // neurons owned
+  const int S = (p.N - n0) < p.S ? (p.N - n0) : p.S;  // neurons owned (<= SP)
   const int L = p.L, NB = p.NB;
   const double sd = p.prior_std, isd2 = 1.0 / (sd * sd);
   const double lconst = log(sd) + 0.5 * log(2.0 * M_PI);
 
+  // ---- thread roles ------------------------------------------------------------
+  const int lb = wid * 4 + (lane >> 4);                // l-block (rows lb*A ..)
+  const int qb = lane & 15;                            // q-block (cols qb*BC ..)
+  const int slot = scatter_slot<A>(lane);
+  const int lrow = lb * A + slot;                      // the row this lane evaluates
+  const bool owner = (lane & 15) < A;                  // one lane per row slot
+  const bool is_row = owner && lrow < L;
+  // element (q, s) of the Adam update
+  const int eq = tid / SP, es = tid % SP;
+  const bool is_el = eq < NB && es < S;
+
   // ---- one-time loads -------------------------------------------------------
-  const bool is_row = tid < L;
-  float brow[NBR];
+  float bb[A][BC];
 #pragma unroll
-  for (int k = 0; k < NBR; ++k) brow[k] = (is_row && k < NB) ? p.basis[(size_t)tid * NB + k] : 0.f;
-  for (int k = 0; k < STRIDE; ++k) {
-    const int q = NBR + k;
-    sBl[tid * STRIDE + k] = (is_row && k < NBL && q < NB) ? p.basis[(size_t)tid * NB + q] : 0.f;
-  }
-  double twd = 0.0;
-  for (int s = 0; s < kSMax; ++s)
-      sYw[tid * kSMax + s] = (is_row && s < S) ? p.yw[(size_t)tid * p.N + n0 + s] : 0.0;
-  if (is_row) twd = p.tw[tid];
-  const int ek = tid % NB, en = tid / NB;
-  const bool is_el = en < S;
-  for (int q = tid; q < NBM * kSMax; q += blockDim.x) {
+  for (int i = 0; i < A; ++i)
+#pragma unroll
+    for (int k = 0; k < BC; ++k) {
+      const int l = lb * A + i, q = qb * BC + k;
+      bb[i][k] = (l < L && q < NB) ? p.basis[(size_t)l * NB + q] : 0.f;
+    }
+  double yws[SP];
+#pragma unroll
+  for (int s = 0; s < SP; ++s) yws[s] = (is_row && s < S) ? p.yw[(size_t)lrow * p.N + n0 + s] : 0.0;
+  const double twd = is_row ? p.tw[lrow] : 0.0;
+  for (int q = tid; q < kSMax * QS; q += blockDim.x) {
     sW[q] = 0.0;
     sD[q] = 0.f;
   }
+  for (int q = tid; q < 32 * A * SP; q += blockDim.x) sG[q] = 0.f;
   if (tid < 4) sCtl[tid] = 0;
   // element state (W, mu, nu) of this thread's weight, and its global ring
   double w_cur = 0.0, mu_cur = 0.0, nu_cur = 0.0;
-  double* ring = p.ring + (size_t)g * kRing * 3 * NBM * kSMax;
-  const int e = ek * kSMax + en;
+  constexpr int RS = 128 * kSMax;                      // ring slab per state (adam_ws)
+  double* ring = p.ring + (size_t)g * kRing * 3 * RS;
+  const int e = eq * kSMax + es;
+  const int ewo = es * QS + (eq / BC) * BCP + eq % BC; // this element's sW / sD slot
   __syncthreads();
   if (is_el) {
-    const size_t o = (size_t)ek * p.N + n0 + en;
+    const size_t o = (size_t)eq * p.N + n0 + es;
     w_cur = p.W[o];
     mu_cur = p.mu[o];
     nu_cur = p.nu[o];
-    sW[en * NBM + ek] = w_cur;
-    ring[(0 * 3 + 0) * NBM * kSMax + e] = w_cur;
-    ring[(0 * 3 + 1) * NBM * kSMax + e] = mu_cur;
-    ring[(0 * 3 + 2) * NBM * kSMax + e] = nu_cur;
+    sW[ewo] = w_cur;
+    ring[(0 * 3 + 0) * RS + e] = w_cur;
+    ring[(0 * 3 + 1) * RS + e] = mu_cur;
+    ring[(0 * 3 + 2) * RS + e] = nu_cur;
   }
   const int64_t count0 = p.count[0];
   double b1t = pow(p.b1, (double)count0), b2t = pow(p.b2, (double)count0);
@@ -253,98 +282,118 @@ __global__ void __launch_bounds__(kThreadsAll) k_adam(AdamParams p) {
   double fin_loss = 0.0;
   const int maxiter = p.maxiter;
   const bool eval_only = maxiter <= 1;
-  // running F of this row for neurons 0..3 (f64)
-  double F0 = 0.0, F1 = 0.0, F2 = 0.0, F3 = 0.0;
+  double Fs[SP];                           // F of the lane's row, per neuron (f64)
+#pragma unroll
+  for (int s = 0; s < SP; ++s) Fs[s] = 0.0;
 
   for (int k = 0;; ++k) {
-    // ---- body k: evaluate at W_k ---------------------------------------------
+    // ---- phase A: F = B W_k on the lane's row, softplus, loss, G -----------------
     PMG_ADAM_STAMP(k, 0)
     double lpart = 0.0;
-    {
-      const bool exact = (k % kRefresh) == 0;
-      // neurons one at a time (runtime loop, not unrolled: one neuron's registers live)
-#pragma unroll 1
-      for (int s = 0; s < S; ++s) {
-        double F;
-        if (exact) {
-          F = 0.0;
+    const bool exact = (k % kRefresh) == 0;
+    // one neuron slot at a time (slots s >= S carry zeros and write G = 0); the
+    // scheduling barrier keeps one slot's A-row partials live at a time
 #pragma unroll
-          for (int q = 0; q < NBR; ++q) {
-            asm volatile("" : "+v"(brow[q]));   // keep the f32->f64 conversion local
-            F = fma((double)brow[q], sW[s * NBM + q], F);
-          }
-#pragma unroll 2
-          for (int q4 = 0; q4 < NBL; q4 += 4) {
-            const float4 b4 = *reinterpret_cast<const float4*>(&sBl[tid * STRIDE + q4]);
-            F = fma((double)b4.x, sW[s * NBM + NBR + q4], F);
-            F = fma((double)b4.y, sW[s * NBM + NBR + q4 + 1], F);
-            F = fma((double)b4.z, sW[s * NBM + NBR + q4 + 2], F);
-            F = fma((double)b4.w, sW[s * NBM + NBR + q4 + 3], F);
-          }
-        } else {
-          float dF = 0.f;
+    for (int s = 0; s < SP; ++s) {
+      double F;
+      if (exact) {
+        double x[A];
 #pragma unroll
-          for (int q = 0; q < NBR; ++q) dF = fmaf(brow[q], sD[s * NBM + q], dF);
+        for (int i = 0; i < A; ++i) x[i] = 0.0;
 #pragma unroll
-          for (int q4 = 0; q4 < NBL; q4 += 4) {
-            const float4 b4 = *reinterpret_cast<const float4*>(&sBl[tid * STRIDE + q4]);
-            const float4 d4 = *reinterpret_cast<const float4*>(&sD[s * NBM + NBR + q4]);
-            dF = fmaf(b4.x, d4.x, dF);
-            dF = fmaf(b4.y, d4.y, dF);
-            dF = fmaf(b4.z, d4.z, dF);
-            dF = fmaf(b4.w, d4.w, dF);
-          }
-          F = (s == 0 ? F0 : s == 1 ? F1 : s == 2 ? F2 : F3) + (double)dF;
+        for (int k4 = 0; k4 < BC; ++k4) {
+          const double w = sW[s * QS + qb * BCP + k4];
+#pragma unroll
+          for (int i = 0; i < A; ++i) x[i] = fma((double)bb[i][k4], w, x[i]);
         }
-        F0 = s == 0 ? F : F0;
-        F1 = s == 1 ? F : F1;
-        F2 = s == 2 ? F : F2;
-        F3 = s == 3 ? F : F3;
-        const double ywd = is_row ? sYw[tid * kSMax + s] : 0.0;
-        // softplus / sigmoid in f32 at Fh = f32(F), corrected to first order in the
-        // exact residual r = F - Fh (|r| <= 2^-24 |F|): f = softplus(Fh) + sigmoid(Fh) r
-        const float Fh = (float)F;
-        const double r = F - (double)Fh;
-        const float f32 = fmaxf(Fh, 0.f) + log1pf(expf(-fabsf(Fh)));
-        const float sg = 1.f / (1.f + expf(-Fh));
-        const double fd = (double)f32 + (double)sg * r;
-        const float gr = is_row ? (float)((ywd / (fd + 1e-20) - twd) * (double)sg) : 0.f;
-        if (is_row) {
-          const double xl = (ywd != 0.0) ? ywd * ((double)logf(f32 + 1e-20f) + (double)sg * r / (double)f32) : 0.0;
-          lpart -= xl - fd * twd;
-        }
-        // per-wave partial of B^T G for this neuron, 32 columns per chunk
-        float* sr = &sRed[(wid * NBM) * kSMax] + s;
-        ChunkLoop<0, NBR, 0>::run(brow, gr, sr, lane);
+        F = reduce_scatter16<A>(x);
+      } else {
+        float dw[BCP];
 #pragma unroll
-        for (int c0 = 0; c0 < NBL; c0 += 32) {
-          float bl[32];
-#pragma unroll
-          for (int q4 = 0; q4 < 32; q4 += 4) {
-            const float4 b4 = (c0 + q4 < NBL)
-                                  ? *reinterpret_cast<const float4*>(&sBl[tid * STRIDE + c0 + q4])
-                                  : make_float4(0.f, 0.f, 0.f, 0.f);
-            bl[q4] = b4.x;
-            bl[q4 + 1] = b4.y;
-            bl[q4 + 2] = b4.z;
-            bl[q4 + 3] = b4.w;
-          }
-          const float gg[1] = {gr};
-          const float red = wave_products_reduce32<1, 0, 32>(bl, gg);
-          const int v = c0 + bitrev5(lane & 31);
-          if (lane < 32 && v < NBL) sr[(NBR + v) * kSMax] = red;
+        for (int k4 = 0; k4 < BCP; k4 += 4) {
+          const float4 v = *reinterpret_cast<const float4*>(&sD[s * QS + qb * BCP + k4]);
+          dw[k4] = v.x;
+          dw[k4 + 1] = v.y;
+          dw[k4 + 2] = v.z;
+          dw[k4 + 3] = v.w;
         }
+        float x[A];
+#pragma unroll
+        for (int i = 0; i < A; ++i) {
+          float a = 0.f;
+#pragma unroll
+          for (int k4 = 0; k4 < BC; ++k4) a = fmaf(bb[i][k4], dw[k4], a);
+          x[i] = a;
+        }
+        F = Fs[s] + (double)reduce_scatter16<A>(x);
       }
+      Fs[s] = F;
+      const double ywd = yws[s];
+      // softplus / sigmoid in f32 at Fh = f32(F), corrected to first order in the
+      // exact residual r = F - Fh (|r| <= 2^-24 |F|): f = softplus(Fh) + sigmoid(Fh) r
+      const float Fh = (float)F;
+      const double r = F - (double)Fh;
+      const float f32 = fmaxf(Fh, 0.f) + log1pf(expf(-fabsf(Fh)));
+      const float sg = 1.f / (1.f + expf(-Fh));
+      const double fd = (double)f32 + (double)sg * r;
+      const bool live = is_row && s < S;
+      const float gv = live ? (float)((ywd * rcp_nr(fd + 1e-20) - twd) * (double)sg) : 0.f;
+      if (owner) sG[(lb * A + slot) * SP + s] = gv;
+      const double xl = (ywd != 0.0) ? ywd * ((double)logf(f32 + 1e-20f) + (double)sg * r * rcp_nr((double)f32)) : 0.0;
+      lpart -= live ? xl - fd * twd : 0.0;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- phase B: B^T G partials (G of the block from wave-local LDS) ---------------
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's G stores are visible
+    float gp[SP][BC];
+#pragma unroll
+    for (int s = 0; s < SP; ++s)
+#pragma unroll
+      for (int k4 = 0; k4 < BC; ++k4) gp[s][k4] = 0.f;
+#pragma unroll
+    for (int i = 0; i < A; ++i) {
+      float gl[SP];
+      const float* src = &sG[(lb * A + i) * SP];
+      if constexpr (SP == 1) gl[0] = src[0];
+      else if constexpr (SP == 2) {
+        const float2 v = *reinterpret_cast<const float2*>(src);
+        gl[0] = v.x;
+        gl[1] = v.y;
+      } else {
+        const float4 v = *reinterpret_cast<const float4*>(src);
+        gl[0] = v.x;
+        gl[1] = v.y;
+        gl[2] = v.z;
+        gl[3] = v.w;
+      }
+#pragma unroll
+      for (int s = 0; s < SP; ++s)
+#pragma unroll
+        for (int k4 = 0; k4 < BC; ++k4) gp[s][k4] = fmaf(bb[i][k4], gl[s], gp[s][k4]);
+    }
+#pragma unroll
+    for (int s = 0; s < SP; ++s)
+#pragma unroll
+      for (int k4 = 0; k4 < BC; ++k4) {
+        gp[s][k4] = add_xor32(add_xor16(gp[s][k4]));
+      }
+    if (lane < 16) {
+#pragma unroll
+      for (int s = 0; s < SP; ++s)
+#pragma unroll
+        for (int k4 = 0; k4 < BC; ++k4) sPart[(wid * SP + s) * 16 * BC + qb * BC + k4] = gp[s][k4];
     }
     PMG_ADAM_STAMP(k, 1)
     PMG_LDS_BARRIER();
     PMG_ADAM_STAMP(k, 2)
+    // ---- Adam element update ------------------------------------------------------
     double gsq = 0.0;
     b1t *= p.b1;
     b2t *= p.b2;
     if (is_el) {
       float gsum = 0.f;
-      for (int q = 0; q < kNW; ++q) gsum += sRed[(q * NBM) * kSMax + e];
+#pragma unroll
+      for (int w = 0; w < kNW; ++w) gsum += sPart[(w * SP + es) * 16 * BC + eq];
       const double gr = -(double)gsum + w_cur * isd2;
       gsq = gr * gr;
       lpart += 0.5 * w_cur * w_cur * isd2 + lconst;
@@ -359,11 +408,11 @@ __global__ void __launch_bounds__(kThreadsAll) k_adam(AdamParams p) {
         nu_cur = nu;
       }
       const int ns = (k + 1) % kRing;
-      ring[(ns * 3 + 0) * NBM * kSMax + e] = w_cur;
-      ring[(ns * 3 + 1) * NBM * kSMax + e] = mu_cur;
-      ring[(ns * 3 + 2) * NBM * kSMax + e] = nu_cur;
-      sW[en * NBM + ek] = w_cur;
-      sD[en * NBM + ek] = (float)(w_cur - w_old);
+      ring[(ns * 3 + 0) * RS + e] = w_cur;
+      ring[(ns * 3 + 1) * RS + e] = mu_cur;
+      ring[(ns * 3 + 2) * RS + e] = nu_cur;
+      sW[ewo] = w_cur;
+      sD[ewo] = (float)(w_cur - w_old);
     }
     lpart = wave_sum_f64(lpart);
     gsq = wave_sum_f64(gsq);
@@ -371,6 +420,7 @@ __global__ void __launch_bounds__(kThreadsAll) k_adam(AdamParams p) {
       sSum[wid] = lpart;
       sSum[kNW + wid] = gsq;
     }
+    if (p.prof && g == 0 && tid == kThreads - 64 && k < 64) p.prof[k * 8 + 5] = __builtin_amdgcn_s_memtime();
     if (ctl && k > 0) {
       // ---- decision pipeline (control wave) over bodies dj .. k-1 ---------------
       // Partials are pre-filled with a signalling-NaN sentinel (never produced by
@@ -445,6 +495,7 @@ __global__ void __launch_bounds__(kThreadsAll) k_adam(AdamParams p) {
         }
       }
     }
+    if (p.prof && g == 0 && tid == kThreads - 64 && k < 64) p.prof[k * 8 + 6] = __builtin_amdgcn_s_memtime();
     PMG_ADAM_STAMP(k, 3)
     PMG_LDS_BARRIER();
     if (sCtl[0] || sCtl[2]) break;
@@ -463,10 +514,10 @@ __global__ void __launch_bounds__(kThreadsAll) k_adam(AdamParams p) {
   // ---- write the state after body stop_j (W_{stop_j+1}) from the ring ---------
   const int fs = eval_only ? (1 % kRing) : ((stop_j + 1) % kRing);
   if (is_el && !sCtl[2]) {
-    const size_t o = (size_t)ek * p.N + n0 + en;
-    p.W[o] = ring[(fs * 3 + 0) * NBM * kSMax + e];
-    p.mu[o] = ring[(fs * 3 + 1) * NBM * kSMax + e];
-    p.nu[o] = ring[(fs * 3 + 2) * NBM * kSMax + e];
+    const size_t o = (size_t)eq * p.N + n0 + es;
+    p.W[o] = ring[(fs * 3 + 0) * RS + e];
+    p.mu[o] = ring[(fs * 3 + 1) * RS + e];
+    p.nu[o] = ring[(fs * 3 + 2) * RS + e];
   }
   if (g == 0 && ctl && lane == 0 && !sCtl[2]) {
     const int n_iter = eval_only ? 1 : stop_j + 2;
@@ -475,14 +526,6 @@ __global__ void __launch_bounds__(kThreadsAll) k_adam(AdamParams p) {
     p.stats[3] = loss0;
     p.count[0] = count0 + (eval_only ? 0 : (stop_j + 1));
   }
-}
-
-template <int NBM>
-static size_t adam_lds_bytes() {
-  using BS = BasisSplit<NBM>;
-  return sizeof(float) * ((size_t)kThreads * BS::STRIDE + 2 * NBM * kSMax + NBM * kSMax +
-                          kNW * NBM * kSMax) +
-         sizeof(double) * (2 * kNW + kThreads * kSMax) + sizeof(int) * 4 + 64;
 }
 
 // Histories (fit_tuning_helper.py:147-149, :175-176) from the published partials, summed
@@ -536,20 +579,29 @@ struct AdamKernel {
   size_t lds;
 };
 
-template <int NBM>
-static AdamKernel pick_sp(int SPn) {
-  (void)SPn;  // neurons are looped at run time inside the kernel
-  return {k_adam<NBM, NBM, 1>, adam_lds_bytes<NBM>()};
+template <int A, int BC>
+static AdamKernel pick_sp(int S) {
+  if (S <= 1) return {k_adam<A, BC, 1>, 0};
+  if (S <= 2) return {k_adam<A, BC, 2>, 0};
+  return {k_adam<A, BC, 4>, 0};
 }
 
-static AdamKernel pick_adam(int NB, int SPn) {
-  if (NB <= 32) return pick_sp<32>(SPn);
-  if (NB <= 48) return pick_sp<48>(SPn);
-  if (NB <= 64) return pick_sp<64>(SPn);
-  if (NB <= 80) return pick_sp<80>(SPn);
-  if (NB <= 96) return pick_sp<96>(SPn);
-  if (NB <= 112) return pick_sp<112>(SPn);
-  if (NB <= 128) return pick_sp<128>(SPn);
+template <int A>
+static AdamKernel pick_bc(int NB, int S) {
+  if (NB <= 32) return pick_sp<A, 2>(S);
+  if (NB <= 48) return pick_sp<A, 3>(S);
+  if (NB <= 64) return pick_sp<A, 4>(S);
+  if (NB <= 80) return pick_sp<A, 5>(S);
+  if (NB <= 96) return pick_sp<A, 6>(S);
+  if (NB <= 128) return pick_sp<A, 8>(S);
+  return {nullptr, 0};
+}
+
+// rows per l-block A = ceil(L / 32) rounded up to 4 / 8 / 16
+static AdamKernel pick_adam(int NB, int L, int S) {
+  if (L <= 128) return pick_bc<4>(NB, S);
+  if (L <= 256) return pick_bc<8>(NB, S);
+  if (L <= 512) return pick_bc<16>(NB, S);
   return {nullptr, 0};
 }
 
@@ -588,7 +640,7 @@ int pmg_mstep_adam_supported(int32_t L, int32_t NB, int32_t N) {
   int S, G, ng, LG;
   adam_geometry(N, L, NB, S, G, ng, LG);
   if (S > kSMax || NB * S > kThreads) return 0;
-  AdamKernel kern = pick_adam(NB, S);
+  AdamKernel kern = pick_adam(NB, L, S);
   return (kern.fn != nullptr && kern.lds <= 160 * 1024) ? 1 : 0;
 }
 
@@ -605,7 +657,7 @@ int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const floa
   adam_geometry(N, L, NB, S, G, ng, LG);
   PMG_REQUIRE(S <= kSMax, "pmg_mstep_adam: N=%d needs %d neurons per workgroup (> %d)", N, S, kSMax);
   PMG_REQUIRE(NB * S <= kThreads, "pmg_mstep_adam: NB*S=%d > %d", NB * S, kThreads);
-  AdamKernel kern = pick_adam(NB, S);
+  AdamKernel kern = pick_adam(NB, L, S);
   PMG_REQUIRE(kern.fn != nullptr && kern.lds <= 160 * 1024,
               "pmg_mstep_adam: NB=%d unsupported (basis must fit registers + 160 KiB LDS)", NB);
   const int maxiter = cfg->maxiter > 1 ? cfg->maxiter : 1;
@@ -656,9 +708,6 @@ int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const floa
   p.timeout = w.timeout;
   p.ring = w.ring;
   PMG_HIP(hipMemsetAsync(stats, 0, 4 * sizeof(double), st));
-  if (kern.lds > 64 * 1024)
-    PMG_HIP(hipFuncSetAttribute((const void*)kern.fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)kern.lds));
   static long long* prof_buf = nullptr;   // debug: per-phase stamps (PMG_ADAM_PROF set)
   const bool prof = getenv("PMG_ADAM_PROF") != nullptr;
   if (prof) {
@@ -668,7 +717,7 @@ int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const floa
   } else {
     p.prof = nullptr;
   }
-  hipLaunchKernelGGL(kern.fn, dim3(G), dim3(kThreadsAll), kern.lds, st, p);
+  hipLaunchKernelGGL(kern.fn, dim3(G), dim3(kThreads), kern.lds, st, p);
   PMG_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_adam_hist, dim3(64), dim3(64), 0, st, p);
   PMG_LAUNCH_CHECK();
@@ -676,18 +725,19 @@ int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const floa
     long long h[64 * 8];
     PMG_HIP(hipMemcpyAsync(h, prof_buf, sizeof(h), hipMemcpyDeviceToHost, st));
     PMG_HIP(hipStreamSynchronize(st));
-    double acc[5] = {0, 0, 0, 0, 0};
+    double acc[6] = {0, 0, 0, 0, 0, 0};
     int n = 0;
     for (int k = 8; k + 1 < 64; ++k) {   // skip the pipeline fill
       if (h[k * 8 + 4] == 0 || h[(k + 1) * 8] == 0) break;
       for (int i = 0; i < 4; ++i) acc[i] += (double)(h[k * 8 + i + 1] - h[k * 8 + i]);
       acc[4] += (double)(h[(k + 1) * 8] - h[k * 8 + 4]);
+      acc[5] += (double)(h[k * 8 + 6] - h[k * 8 + 5]);
       ++n;
     }
     if (n > 0)
       fprintf(stderr, "[pmg adam prof] bodies=%d ticks/body: rows %.0f | bar1 %.0f | update %.0f | "
-              "sums+bar2+publish %.0f | loop %.0f\n", n, acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n,
-              acc[4] / n);
+              "sums+bar2+publish %.0f | loop %.0f | decision (ctl wave) %.0f\n", n, acc[0] / n, acc[1] / n,
+              acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n);
   }
   return PMG_OK;
 }
