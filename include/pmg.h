@@ -130,6 +130,11 @@ int pmg_tuning_linear(const float* basis, const double* W, int32_t L, int32_t NB
 int pmg_emission_gaussian(const float* y, const double* tuning64, const float* ma_neuron, int32_t ma_is_2d,
                           const uint8_t* ma_latent, double noise_std, double dt, int64_t T, int32_t L,
                           int32_t N, float* delta, double* rblk, void* stream);
+/* Per-time-bin dt (decoder.get_loglikelihood_ma_all_changing_dt with the Gaussian
+ * observation model, decoder.py:73-85 -> :50-57): mu = tuning * dt_t[t]; dt_t (T) f64. */
+int pmg_emission_gaussian_dt(const float* y, const double* tuning64, const float* ma_neuron, int32_t ma_is_2d,
+                             const uint8_t* ma_latent, double noise_std, const double* dt_t, int64_t T, int32_t L,
+                             int32_t N, float* delta, double* rblk, void* stream);
 /* Analytic M-step, fit_tuning_helper.gaussian_m_step_analytic (:44-61):          */
 /* W (NB,N) f64 = solve(B^T diag(t_w) B / s^2 + I / p^2, B^T y_w / s^2), Cholesky */
 /* in f64 (H is SPD).  status (device int32) = 1 if a pivot was not positive.      */

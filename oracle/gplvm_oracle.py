@@ -251,16 +251,19 @@ def smooth_all_step(causal_post, causal_prior, logK, logA, carry_init=None, with
 
 def loglikelihood_gaussian_all(y, tuning, noise_std, ma_neuron=None, ma_latent=None, dt=1.0):
     """decoder.py:50-57 vmapped over time: ll[t,l] = sum_n m[t,n] *
-    norm.logpdf(y[t,n], tuning[l,n]*dt, noise_std); ll[:, ~ma_latent] = -1e20."""
+    norm.logpdf(y[t,n], tuning[l,n]*dt, noise_std); ll[:, ~ma_latent] = -1e20.
+    dt may be a per-time-bin array (decoder.py:73-85, get_loglikelihood_ma_all_changing_dt)."""
     y = np.asarray(y, _F)
-    mu = np.asarray(tuning, _F) * dt
+    tun = np.asarray(tuning, _F)
     T, N = y.shape
+    dt_t = np.broadcast_to(np.asarray(dt, _F), (T,))[:, None]
     m = np.ones((T, N), _F) if ma_neuron is None else np.broadcast_to(np.asarray(ma_neuron, _F), (T, N))
     s = float(noise_std)
     c0 = -math.log(s) - 0.5 * math.log(2 * math.pi)
-    # sum_n m*(c0 - (y - mu)^2 / (2 s^2)), expanded into matrix products
+    # sum_n m*(c0 - (y - tuning dt_t)^2 / (2 s^2)), expanded into matrix products
     ll = (c0 * m.sum(1, keepdims=True) - 0.5 / s ** 2 * ((m * y * y).sum(1, keepdims=True)
-                                                         - 2.0 * (m * y) @ mu.T + m @ (mu * mu).T))
+                                                         - 2.0 * dt_t * ((m * y) @ tun.T)
+                                                         + dt_t ** 2 * (m @ (tun * tun).T)))
     if ma_latent is not None:
         ml = np.asarray(ma_latent).astype(bool)
         ll = np.where(ml[None, :], ll, NEG_MASK)

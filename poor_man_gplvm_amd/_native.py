@@ -32,7 +32,8 @@ EXPORTED_SYMBOLS = (
     "pmg_emission_rowref", "pmg_loglik_materialize", "pmg_fwdbwd_workspace_size",
     "pmg_forward_filter", "pmg_backward_smoother", "pmg_fwdbwd_repair_counter_offset",
     "pmg_forward_filter_phase", "pmg_backward_smoother_phase",
-    "pmg_suffstats_workspace_size", "pmg_suffstats", "pmg_exp", "pmg_log", "pmg_roll_columns", "pmg_emission_latent_mask",
+    "pmg_suffstats_workspace_size", "pmg_suffstats", "pmg_exp", "pmg_log", "pmg_roll_columns",
+    "pmg_emission_latent_mask", "pmg_emission_gaussian_dt",
     "pmg_spikes_bf16t", "pmg_suffstats_bf16_workspace_size", "pmg_suffstats_bf16",
     "pmg_mstep_workspace_size", "pmg_mstep_adam_supported", "pmg_mstep_adam", "pmg_joint_workspace_size",
     "pmg_joint_accumulate", "pmg_fwdbwd_lpad", "pmg_fwdbwd_state",
@@ -117,6 +118,7 @@ _SIGS = {
     "pmg_tuning_linear": ([_P, _P, _I32, _I32, _I32, _P, _P, _P], _I32),
     "pmg_emission_gaussian": ([_P, _P, _P, _I32, _P, ctypes.c_double, ctypes.c_double, _I64, _I32, _I32,
                                _P, _P, _P], _I32),
+    "pmg_emission_gaussian_dt": ([_P, _P, _P, _I32, _P, ctypes.c_double, _P, _I64, _I32, _I32, _P, _P, _P], _I32),
     "pmg_gaussian_mstep_workspace_size": ([_I32, _I32], _SZ),
     "pmg_gaussian_mstep": ([_P, _P, _P, _I32, _I32, _I32, ctypes.c_double, ctypes.c_double, _P, _P, _P, _SZ,
                             _P], _I32),

@@ -356,10 +356,14 @@ class PoissonGPLVMJump1D:
         dt = np.broadcast_to(np.asarray(dt_l, np.float64), (T,))
         dev, L = eng.dev, self.n_latent_bin
         lib, sh = eng.lib, nat.stream_handle()
-        if eng.noise_std is not None and not np.all(dt == dt[0]):
-            raise NotImplementedError("Gaussian naive-Bayes decoding with a per-time-bin dt_l is not implemented")
         if np.all(dt == dt[0]):
             eng._emission_call(sp, sh, float(dt[0]))
+        elif eng.noise_std is not None:
+            dtt = torch.as_tensor(np.array(dt, dtype=np.float64), device=dev)
+            nat.check(lib.pmg_emission_gaussian_dt(nat.ptr(sp.y), nat.ptr(eng.tuning64), nat.ptr(sp.ma),
+                                                   int(sp.ma_2d), nat.ptr(eng.ma_latent), float(eng.noise_std),
+                                                   nat.ptr(dtt), T, L, sp.N, nat.ptr(eng.delta), nat.ptr(eng.rblk),
+                                                   sh), "pmg_emission_gaussian_dt")
         else:
             dtt = torch.as_tensor(np.array(dt, dtype=np.float64), device=dev)
             nat.check(lib.pmg_emission_poisson_dt(nat.ptr(sp.y), nat.ptr(sp.gconst), nat.ptr(eng.tuning64),

@@ -39,8 +39,8 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 __global__ void __launch_bounds__(256) k_emission_gaussian(
     const float* __restrict__ y, const float* __restrict__ ma, int ma_2d, const double* __restrict__ tuning,
-    const uint8_t* __restrict__ ma_latent, double inv_s, double c0, double dt, int64_t T, int L, int N, int Lp,
-    float* __restrict__ delta, double* __restrict__ rblk) {
+    const uint8_t* __restrict__ ma_latent, double inv_s, double c0, double dt, const double* __restrict__ dt_t,
+    int64_t T, int L, int N, int Lp, float* __restrict__ delta, double* __restrict__ rblk) {
   __shared__ float sY[64][33];     // y and m stay f32 (their f64 product is exact)
   __shared__ float sM[64][33];
   __shared__ double sTu[32][65];   // mu = tuning * dt (f64); mu^2 is formed at use
@@ -115,7 +115,10 @@ __global__ void __launch_bounds__(256) k_emission_gaussian(
         const int l = l0 + 16 * s + (lane & 15);
         double x = -INFINITY;
         if (l < L && t < T) {
-          x = q[r] + inv_s2 * acc_a[s][r] - 0.5 * inv_s2 * acc_b[s][r];
+          // per-time-bin dt (decoder.py:73-85): mu = tuning dt_t, so the contractions (run
+          // with dt = 1) scale by dt_t and dt_t^2
+          const double d = dt_t ? dt_t[t] : 1.0;
+          x = q[r] + inv_s2 * d * acc_a[s][r] - 0.5 * inv_s2 * (d * d) * acc_b[s][r];
           if (ma_latent && ma_latent[l] == 0) x = -1e20;
         }
         v[u] = x;
@@ -255,7 +258,22 @@ int pmg_emission_gaussian(const float* y, const double* tuning64, const float* m
   const double c0 = -log(noise_std) - 0.5 * log(2.0 * M_PI);
   dim3 grid((unsigned)((T + 63) / 64), (unsigned)((L + 63) / 64));
   hipLaunchKernelGGL(k_emission_gaussian, grid, dim3(256), 0, as_stream(stream), y, ma_neuron, ma_is_2d, tuning64,
-                     ma_latent, 1.0 / noise_std, c0, dt, T, L, N, Lp, delta, rblk);
+                     ma_latent, 1.0 / noise_std, c0, dt, nullptr, T, L, N, Lp, delta, rblk);
+  PMG_LAUNCH_CHECK();
+  return PMG_OK;
+}
+
+int pmg_emission_gaussian_dt(const float* y, const double* tuning64, const float* ma_neuron, int32_t ma_is_2d,
+                             const uint8_t* ma_latent, double noise_std, const double* dt_t, int64_t T, int32_t L,
+                             int32_t N, float* delta, double* rblk, void* stream) {
+  PMG_REQUIRE(T > 0 && L > 0 && N > 0 && y && tuning64 && dt_t && delta && rblk,
+              "pmg_emission_gaussian_dt: bad args");
+  PMG_REQUIRE(noise_std > 0.0, "pmg_emission_gaussian_dt: noise_std must be > 0");
+  const int Lp = (int)round_up(L, 32);
+  const double c0 = -log(noise_std) - 0.5 * log(2.0 * M_PI);
+  dim3 grid((unsigned)((T + 63) / 64), (unsigned)((L + 63) / 64));
+  hipLaunchKernelGGL(k_emission_gaussian, grid, dim3(256), 0, as_stream(stream), y, ma_neuron, ma_is_2d, tuning64,
+                     ma_latent, 1.0 / noise_std, c0, 1.0, dt_t, T, L, N, Lp, delta, rblk);
   PMG_LAUNCH_CHECK();
   return PMG_OK;
 }

@@ -390,6 +390,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
     double gsq = 0.0;
     b1t *= p.b1;
     b2t *= p.b2;
+    const double c1 = 1.0 / (1.0 - b1t), c2 = 1.0 / (1.0 - b2t);   // bias corrections (uniform)
     if (is_el) {
       float gsum = 0.f;
 #pragma unroll
@@ -401,9 +402,9 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
       if (!eval_only) {  // optax 0.2.2 scale_by_adam + scale(-lr)
         const double mu = (1.0 - p.b1) * gr + p.b1 * mu_cur;
         const double nu = (1.0 - p.b2) * gr * gr + p.b2 * nu_cur;
-        const double mh = mu / (1.0 - b1t);
-        const double nh = nu / (1.0 - b2t);
-        w_cur = w_cur - p.lr * (mh / (sqrt(nh + p.eps_root) + p.eps));
+        const double mh = mu * c1;
+        const double nh = nu * c2;
+        w_cur = w_cur - p.lr * (mh * rcp_nr(sqrt(nh + p.eps_root) + p.eps));
         mu_cur = mu;
         nu_cur = nu;
       }
@@ -445,6 +446,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
 #pragma unroll
             for (int q = 0; q < kPartPerLane; ++q) ok &= (lv0[q] != kSentinel);
             ok = __all(ok);
+            if (p.prof && g == 0 && lane == 0 && k < 64) p.prof[k * 8 + 7] += 1;
             if (++spins > (1u << 24)) {
               if (lane == 0) {
                 atomicOr(p.timeout, 1);
@@ -726,18 +728,20 @@ int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const floa
     PMG_HIP(hipMemcpyAsync(h, prof_buf, sizeof(h), hipMemcpyDeviceToHost, st));
     PMG_HIP(hipStreamSynchronize(st));
     double acc[6] = {0, 0, 0, 0, 0, 0};
+    long long spins = 0;
     int n = 0;
     for (int k = 8; k + 1 < 64; ++k) {   // skip the pipeline fill
       if (h[k * 8 + 4] == 0 || h[(k + 1) * 8] == 0) break;
       for (int i = 0; i < 4; ++i) acc[i] += (double)(h[k * 8 + i + 1] - h[k * 8 + i]);
       acc[4] += (double)(h[(k + 1) * 8] - h[k * 8 + 4]);
       acc[5] += (double)(h[k * 8 + 6] - h[k * 8 + 5]);
+      spins += h[k * 8 + 7];
       ++n;
     }
     if (n > 0)
       fprintf(stderr, "[pmg adam prof] bodies=%d ticks/body: rows %.0f | bar1 %.0f | update %.0f | "
-              "sums+bar2+publish %.0f | loop %.0f | decision (ctl wave) %.0f\n", n, acc[0] / n, acc[1] / n,
-              acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n);
+              "sums+bar2+publish %.0f | loop %.0f | decision (ctl wave) %.0f, blocking polls %lld\n", n,
+              acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n, spins);
   }
   return PMG_OK;
 }

@@ -137,5 +137,12 @@ def test_gaussian_naive_bayes_vs_oracle(masked):
     lml = logsumexp(ll, axis=1)
     np.testing.assert_allclose(r['log_marginal_l'], lml, rtol=1e-6)
     close_prob(r['posterior_latent'], np.exp(ll - lml[:, None]), rtol=1e-4, atol=1e-9)
-    with pytest.raises(NotImplementedError):
-        m.decode_latent_naive_bayes(d['y'], tuning=d['tuning'], dt_l=np.linspace(0.5, 1.5, T))
+    # per-time-bin dt (decoder.py:73-85): pmg_emission_gaussian_dt
+    dt = np.linspace(0.5, 1.5, T)
+    r = m.decode_latent_naive_bayes(d['y'], tuning=d['tuning'], ma_latent=ml, dt_l=dt)
+    ll = O.loglikelihood_gaussian_all(d['y'], d['tuning'], SIG, None, ml, dt=dt)
+    lml = logsumexp(ll, axis=1)
+    np.testing.assert_allclose(r['log_marginal_l'], lml, rtol=1e-6)
+    close_prob(r['posterior_latent'], np.exp(ll - lml[:, None]), rtol=1e-4, atol=1e-9)
+    np.testing.assert_allclose(r['ll_per_pos_l'][:, ml.astype(bool) if masked else slice(None)],
+                               ll[:, ml.astype(bool) if masked else slice(None)], rtol=1e-6, atol=1e-3)
