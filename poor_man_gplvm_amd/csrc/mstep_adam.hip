@@ -50,6 +50,7 @@ struct AdamParams {
   double* stats;
   double* loss_hist;
   double* err_hist;
+  const double* bias;         // [2][maxiter] 1/(1 - b1^(count0+k+1)), 1/(1 - b2^(count0+k+1))
   unsigned long long* lpart;  // [maxiter + kLag + 2][G] f64 bits, pre-filled with kSentinel
   unsigned long long* gpart;  // [..][G]
   double* ring;               // [G][kRing][3][NBM*4] (W, mu, nu) after each body
@@ -93,6 +94,26 @@ __global__ void k_fill_u64(unsigned long long* __restrict__ x, size_t n, unsigne
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (; i < n; i += stride) x[i] = v;
+}
+
+// Launch prologue: sentinel-fill both partial arrays and tabulate the bias corrections
+// of every body from the Adam step count, c_k = 1 / (1 - b^(count0 + k + 1)).  A closed
+// form per body (not a running product) gives the same bits however the loop is split
+// into launches (the speculative batches of the neuron-sharded M-step).
+__global__ void k_adam_prologue(unsigned long long* __restrict__ lpart, unsigned long long* __restrict__ gpart,
+                                size_t n, const int64_t* __restrict__ count, double b1, double b2, int maxiter,
+                                double* __restrict__ bias) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t q = i; q < n; q += stride) {
+    lpart[q] = kSentinel;
+    gpart[q] = kSentinel;
+  }
+  const double c0 = (double)count[0];
+  for (size_t k = i; k < (size_t)maxiter; k += stride) {
+    bias[k] = 1.0 / (1.0 - pow(b1, c0 + (double)k + 1.0));
+    bias[maxiter + k] = 1.0 / (1.0 - pow(b2, c0 + (double)k + 1.0));
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -270,7 +291,6 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
     ring[(0 * 3 + 2) * RS + e] = nu_cur;
   }
   const int64_t count0 = p.count[0];
-  double b1t = pow(p.b1, (double)count0), b2t = pow(p.b2, (double)count0);
   __syncthreads();
 
   // control-wave state
@@ -388,10 +408,11 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
     PMG_ADAM_STAMP(k, 2)
     // ---- Adam element update ------------------------------------------------------
     double gsq = 0.0;
-    b1t *= p.b1;
-    b2t *= p.b2;
-    const double c1 = 1.0 / (1.0 - b1t), c2 = 1.0 / (1.0 - b2t);   // bias corrections (uniform)
     if (is_el) {
+      // bias corrections (uniform); bodies run ahead of the decision past maxiter are discarded
+      const int mi = p.maxiter > 1 ? p.maxiter : 1;
+      const int kb = k < mi ? k : mi - 1;
+      const double c1 = p.bias[kb], c2 = p.bias[mi + kb];
       float gsum = 0.f;
 #pragma unroll
       for (int w = 0; w < kNW; ++w) gsum += sPart[(w * SP + es) * 16 * BC + eq];
@@ -560,6 +581,7 @@ struct AdamWork {
   double* ring;
   unsigned long long* lpart;
   unsigned long long* gpart;
+  double* bias;
   int* timeout;
 };
 
@@ -570,6 +592,7 @@ static size_t adam_ws(int G, int maxiter, AdamWork* w, void* base) {
   ww.ring = c.take<double>((size_t)G * kRing * 3 * 128 * kSMax);
   ww.lpart = c.take<unsigned long long>(((size_t)maxiter + kLag + 2) * G);
   ww.gpart = c.take<unsigned long long>(((size_t)maxiter + kLag + 2) * G);
+  ww.bias = c.take<double>(2 * (size_t)maxiter);
   if (w) *w = ww;
   return c.off + 256;
 }
@@ -670,9 +693,8 @@ int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const floa
   adam_ws(G, maxiter, &w, workspace);
   {
     const size_t n = ((size_t)maxiter + kLag + 2) * G;
-    hipLaunchKernelGGL(k_fill_u64, dim3(256), dim3(256), 0, st, w.lpart, n, kSentinel);
-    PMG_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_fill_u64, dim3(256), dim3(256), 0, st, w.gpart, n, kSentinel);
+    hipLaunchKernelGGL(k_adam_prologue, dim3(256), dim3(256), 0, st, w.lpart, w.gpart, n, (const int64_t*)count,
+                       cfg->b1, cfg->b2, maxiter, w.bias);
     PMG_LAUNCH_CHECK();
   }
   PMG_HIP(hipMemsetAsync(w.timeout, 0, sizeof(int), st));
@@ -709,6 +731,7 @@ int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const floa
   p.gpart = w.gpart;
   p.timeout = w.timeout;
   p.ring = w.ring;
+  p.bias = w.bias;
   PMG_HIP(hipMemsetAsync(stats, 0, 4 * sizeof(double), st));
   static long long* prof_buf = nullptr;   // debug: per-phase stamps (PMG_ADAM_PROF set)
   const bool prof = getenv("PMG_ADAM_PROF") != nullptr;

@@ -390,21 +390,28 @@ class DeviceEM:
     # basis row in registers + LDS); larger ones use the tiled per-body kernels
     PERSISTENT_MAX_L, PERSISTENT_MAX_NB = 512, 128
 
-    def adam(self, W, mu, nu, count, cfg: AdamConfig, stats_out, lh_out, eh_out):
+    def adam(self, W, mu, nu, count, cfg: AdamConfig, stats_out, lh_out, eh_out, yw=None):
+        """The Adam loop on W (NB, n) f64 with sufficient statistics yw (L, n) (default:
+        this engine's y_w, n = N); a column slice of the neurons when given (the
+        neuron-sharded M-step of timeshard.py)."""
         if self.basis is None:
             raise ValueError("no basis")
+        yw = self.yw if yw is None else yw
+        n = int(W.shape[1])
+        if tuple(yw.shape) != (self.L, n) or not yw.is_contiguous() or not W.is_contiguous():
+            raise ValueError(f"adam: W {tuple(W.shape)} / yw {tuple(yw.shape)} mismatch")
         tiled = (self.L > self.PERSISTENT_MAX_L or self.NB > self.PERSISTENT_MAX_NB
-                 or not self.lib.pmg_mstep_adam_supported(self.L, self.NB, self.N))
-        need = int(self.lib.pmg_mstep_tiled_workspace_size(self.L, self.NB, self.N) if tiled
-                   else self.lib.pmg_mstep_workspace_size(self.N, int(cfg.maxiter)))
+                 or not self.lib.pmg_mstep_adam_supported(self.L, self.NB, n))
+        need = int(self.lib.pmg_mstep_tiled_workspace_size(self.L, self.NB, n) if tiled
+                   else self.lib.pmg_mstep_workspace_size(n, int(cfg.maxiter)))
         if self.ws_ad is None or self.ws_ad.numel() < need:
             self.ws_ad = torch.empty(need, dtype=torch.uint8, device=self.dev)
         c = cfg.to_c()
         fn = self.lib.pmg_mstep_adam_tiled if tiled else self.lib.pmg_mstep_adam
         with self._t('mstep_adam'):
           nat.check(fn(nat.ptr(W), nat.ptr(mu), nat.ptr(nu), nat.ptr(count),
-                       nat.ptr(self.basis), nat.ptr(self.yw), nat.ptr(self.tw),
-                       self.L, self.NB, self.N, ctypes.byref(c), nat.ptr(stats_out),
+                       nat.ptr(self.basis), nat.ptr(yw), nat.ptr(self.tw),
+                       self.L, self.NB, n, ctypes.byref(c), nat.ptr(stats_out),
                        nat.ptr(lh_out), nat.ptr(eh_out), nat.ptr(self.ws_ad),
                        self.ws_ad.numel(), nat.stream_handle()),
                     "pmg_mstep_adam_tiled" if tiled else "pmg_mstep_adam")

@@ -147,6 +147,25 @@ class LocalComm:
     def gather_rank0(self, parts):
         return [p.cpu() for p in parts]
 
+    def allreduce_process_sum(self, x):
+        """x is already summed over this process's shards, i.e. over all ranks."""
+        return np.asarray(x, np.float64)
+
+    def allreduce_np(self, per_shard):
+        """Sum of host arrays over shards (rank order); the same array for every shard."""
+        acc = np.array(per_shard[0], dtype=np.float64, copy=True)
+        for a in per_shard[1:]:
+            acc = acc + a
+        return acc
+
+    def allgather_cols(self, slices, fulls, bounds):
+        """slices[i]: (rows, b-a) device tensor of local shard i (neuron block
+        bounds[rank]); every full (rows, N) tensor receives every block."""
+        for i, r in enumerate(self.ranks):
+            a, b = bounds[r]
+            for f in fulls:
+                f[:, a:b].copy_(slices[i])
+
 
 class DistComm:
     """One shard per process over torch.distributed: backend "nccl" (= RCCL over xGMI
@@ -193,6 +212,29 @@ class DistComm:
         if staged is not None and staged is not rcv:
             rcv.copy_(staged)
 
+    def allreduce_process_sum(self, x):
+        return self.allreduce_np([x])
+
+    def allreduce_np(self, per_shard):
+        (a,) = per_shard
+        dev = torch.device("cpu") if self.host else torch.device("cuda", torch.cuda.current_device())
+        t = torch.as_tensor(np.asarray(a, np.float64), device=dev).contiguous()
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+        return t.cpu().numpy()
+
+    def allgather_cols(self, slices, fulls, bounds):
+        (mine,) = slices
+        wmax = max(b - a for a, b in bounds)
+        buf = torch.zeros((mine.shape[0], wmax), dtype=mine.dtype, device=mine.device)
+        buf[:, :mine.shape[1]].copy_(mine)
+        src = self._stage(buf)
+        parts = [torch.empty_like(src) for _ in range(self.world)]
+        self.dist.all_gather(parts, src, group=self.group)
+        for r, (a, b) in enumerate(bounds):
+            blk = parts[r][:, :b - a].to(mine.device)
+            for f in fulls:
+                f[:, a:b].copy_(blk)
+
     def gather_rank0(self, parts):
         """Variable-length slices to rank 0 (host tensors there; [] elsewhere)."""
         (mine,) = parts
@@ -210,6 +252,81 @@ class DistComm:
             return out
         self.dist.send(self._stage(mine.contiguous()), dst=0, group=self.group)
         return []
+
+
+# --------------------------------------------------------------------------- Adam
+def neuron_bounds(N: int, world: int):
+    """Contiguous neuron blocks of the neuron-sharded M-step, one per rank."""
+    edges = [round(r * N / world) for r in range(world + 1)]
+    return [(edges[r], edges[r + 1]) for r in range(world)]
+
+
+def adam_stop_body(losses, j0, maxiter, tol, state):
+    """The while-loop rule of fit_tuning_helper.make_adam_runner.run (:154-164) over the
+    global losses of bodies j0, j0+1, ... (losses[i] is computed at W_{j0+i}, before that
+    body's update).  state carries loss_prev across calls.  Returns the body after whose
+    update the loop stops, or None if it runs past these bodies.  The same rule as the
+    persistent kernel's decision pipeline (mstep_adam.hip)."""
+    for i, loss in enumerate(losses):
+        j = j0 + i
+        loss = float(loss)
+        if j == 0:
+            state['prev'] = loss
+        rel = abs(loss - state['prev']) / max(abs(loss), 1e-8)
+        cont = (j + 1 < maxiter - 1) and ((j + 1 < 5) or (rel > tol))
+        state['prev'] = loss
+        if not cont:
+            return j
+    return None
+
+
+def speculative_adam(run, snapshot, restore, allreduce, maxiter, tol, batch=16):
+    """Neuron-sharded Adam loop with the reference's global stop rule.
+
+    Every rank runs its own neuron slice (the loss and the gradient norm are sums over
+    neurons plus per-weight prior terms), `batch` bodies per launch with tol = 0, then
+    ONE all-reduce of the batch's per-body loss / squared-gradient partials decides on
+    the global sums, in the same order on every rank.  A stop inside the batch restores
+    the batch-start snapshot and re-runs the bodies up to the stopping one, so every rank
+    ends with exactly the state the unsharded loop reaches (batch = 16 keeps the
+    persistent kernel's exact-F refresh, every 16 bodies, on the same bodies).
+
+      run(kmax) -> list over local slices of (n_iter, loss_hist, err_hist) host arrays
+                   (the kernel's outputs for maxiter = kmax, tol = 0)
+      snapshot() / restore(): all local slices' (W, mu, nu, count)
+      allreduce(x) -> sum over ranks of the local sum x (host float64 arrays)
+    Returns dict(n_iter, final_loss, final_error, loss_history, error_history, loss0)."""
+    if maxiter <= 1:   # eval only: the loss at W_0, no update
+        outs = run(1)
+        loc = np.array([[o[1][0] for o in outs], [o[2][0] ** 2 for o in outs]]).sum(axis=1)
+        g = allreduce(loc)
+        return dict(n_iter=1, final_loss=float(g[0]), final_error=float(np.sqrt(g[1])),
+                    loss_history=np.array([g[0]]), error_history=np.array([np.sqrt(g[1])]), loss0=float(g[0]))
+    j0, st = 0, {}
+    lh, eh = [], []
+    while True:
+        snap = snapshot()
+        outs = run(batch + 1)
+        nb = min(int(o[0]) for o in outs) - 1          # bodies this launch ran (batch unless rel == 0)
+        loc = np.zeros((2, nb))
+        for n_iter, lhist, ehist in outs:
+            loc[0] += np.asarray(lhist[1:nb + 1], np.float64)
+            loc[1] += np.asarray(ehist[1:nb + 1], np.float64) ** 2
+        g = allreduce(loc)
+        losses, errs = g[0], np.sqrt(g[1])
+        j = adam_stop_body(losses, j0, maxiter, tol, st)
+        stop_at = nb - 1 if j is None else j - j0
+        lh.extend(losses[:stop_at + 1])
+        eh.extend(errs[:stop_at + 1])
+        if j is not None:
+            if stop_at < nb - 1:       # the stop lies inside the batch: replay up to it
+                restore(snap)
+                run(stop_at + 2)
+            hist_l = np.array([lh[0]] + lh)
+            hist_e = np.array([eh[0]] + eh)
+            return dict(n_iter=j + 2, final_loss=float(lh[-1]), final_error=float(eh[-1]),
+                        loss_history=hist_l, error_history=hist_e, loss0=float(lh[0]))
+        j0 += nb
 
 
 # --------------------------------------------------------------------------- shard
@@ -292,7 +409,7 @@ class TimeShardedEM:
     """The EM loop of core.py:650-676 over time shards (see the module docstring)."""
 
     def __init__(self, y, basis, transition, comm, layouts, scan: ScanConfig | None = None,
-                 ma_neuron=None, ma_latent=None, device=None):
+                 ma_neuron=None, ma_latent=None, device=None, neuron_sharded=False):
         self.comm = comm
         self.lays = [layouts[r] for r in comm.ranks]
         self.world = comm.world
@@ -309,6 +426,9 @@ class TimeShardedEM:
             s.set_ma_latent(ma_latent)
         self.dev = self.shards[0].dev
         self.carry_rounds = [0, 0]     # carry rounds of the last E-step (forward, backward)
+        # neuron-sharded Adam (one neuron block per rank) instead of the replicated loop
+        self.neuron_sharded = bool(neuron_sharded) and self.world > 1
+        self._slices = None
 
     def set_timer(self, timer):
         for s in self.shards:
@@ -367,20 +487,78 @@ class TimeShardedEM:
         for s in self.shards:
             s.suffstats_own()
         self.comm.allreduce_sum([[s.yw, s.tw] for s in self.shards])
-        for s, W, mu, nu, c in zip(self.shards, Ws, mus, nus, cnts):
-            s.adam(W, mu, nu, c, cfg, stats, lh, eh)
+        if self.neuron_sharded:
+            self._adam_neuron_sharded(Ws, mus, nus, cnts, cfg, stats, lh, eh)
+        else:
+            for s, W, mu, nu, c in zip(self.shards, Ws, mus, nus, cnts):
+                s.adam(W, mu, nu, c, cfg, stats, lh, eh)
+        for s, W in zip(self.shards, Ws):
             s.compute_tuning(W)
+
+    def _adam_neuron_sharded(self, Ws, mus, nus, cnts, cfg: AdamConfig, stats, lh, eh):
+        """Rank r runs Adam on neuron block bounds[r] only (speculative_adam); W is then
+        all-gathered so every rank holds the full W for the tuning.  mu / nu of a block
+        live on its rank only (the unused columns of mus / nus are not maintained)."""
+        N = Ws[0].shape[1]
+        bounds = neuron_bounds(N, self.world)
+        if self._slices is None:
+            self._slices = []
+            for s, r, mu, nu in zip(self.shards, self.comm.ranks, mus, nus):
+                a, b = bounds[r]
+                self._slices.append({'mu': mu[:, a:b].contiguous(), 'nu': nu[:, a:b].contiguous()})
+        sl = []
+        for s, r, W, c, d in zip(self.shards, self.comm.ranks, Ws, cnts, self._slices):
+            a, b = bounds[r]
+            d['W'] = W[:, a:b].contiguous()
+            d['yw'] = s.yw[:, a:b].contiguous()
+            d['count'] = c
+            sl.append(d)
+        mi = max(int(cfg.maxiter), 1)
+        st_dev = torch.zeros(4, dtype=torch.float64, device=self.dev)
+        lh_dev = torch.zeros(mi + 1, dtype=torch.float64, device=self.dev)
+        eh_dev = torch.zeros_like(lh_dev)
+
+        def run(kmax):
+            c = AdamConfig(lr=cfg.lr, maxiter=kmax, tol=0.0, prior_std=cfg.prior_std, b1=cfg.b1, b2=cfg.b2,
+                           eps=cfg.eps, eps_root=cfg.eps_root)
+            outs = []
+            for s, d in zip(self.shards, sl):
+                s.adam(d['W'], d['mu'], d['nu'], d['count'], c, st_dev, lh_dev, eh_dev, yw=d['yw'])
+                n = int(st_dev[0].item())
+                outs.append((n, lh_dev[:n].cpu().numpy(), eh_dev[:n].cpu().numpy()))
+            return outs
+
+        def snapshot():
+            return [(d['W'].clone(), d['mu'].clone(), d['nu'].clone(), d['count'].clone()) for d in sl]
+
+        def restore(snap):
+            for d, (W, mu, nu, c) in zip(sl, snap):
+                d['W'].copy_(W)
+                d['mu'].copy_(mu)
+                d['nu'].copy_(nu)
+                d['count'].copy_(c)
+
+        res = speculative_adam(run, snapshot, restore, self.comm.allreduce_process_sum, int(cfg.maxiter),
+                               float(cfg.tol))
+        self.comm.allgather_cols([d['W'] for d in sl], Ws, bounds)
+        n = res['n_iter']
+        stats.copy_(torch.tensor([n, res['final_loss'], res['final_error'], res['loss0']], dtype=torch.float64))
+        k = min(n, lh.shape[0])
+        lh[:k].copy_(torch.as_tensor(res['loss_history'][:k]))
+        eh[:k].copy_(torch.as_tensor(res['error_history'][:k]))
 
 
 def run_em_timesharded(y, params, basis, log_posterior_init, n_iter, transition, comm=None, world=None,
                        ma_neuron=None, ma_latent=None, likelihood_scale=1.0, adam: AdamConfig | None = None,
                        scan: ScanConfig | None = None, halo=512, chunk=None, timing=None, gather=True,
-                       timer=None):
+                       timer=None, neuron_sharded=False):
     """Time-sharded counterpart of core.run_em.  `comm`: DistComm (one shard per
     rank), or None for `world` virtual shards on this device (LocalComm).  Returns
     (res, info); res has run_em's per-fit keys with the per-time outputs concatenated
     over shards.  With DistComm and `gather` they are gathered on rank 0 and the other
-    ranks get res=None; without `gather` every rank returns its own slice."""
+    ranks get res=None; without `gather` every rank returns its own slice.
+    neuron_sharded: each rank runs the Adam M-step on its own neuron block
+    (speculative_adam) instead of the whole replicated loop."""
     adam = adam or AdamConfig()
     if comm is None:
         comm = LocalComm(int(world or 1))
@@ -388,7 +566,8 @@ def run_em_timesharded(y, params, basis, log_posterior_init, n_iter, transition,
         y = np.asarray(y)
     T = int(y.shape[0])
     lays = shard_layout(T, comm.world, chunk=chunk, halo=halo, scan=scan)
-    eng = TimeShardedEM(y, basis, transition, comm, lays, scan, ma_neuron, ma_latent)
+    eng = TimeShardedEM(y, basis, transition, comm, lays, scan, ma_neuron, ma_latent,
+                        neuron_sharded=neuron_sharded)
     if timer is not None:
         eng.set_timer(timer)
     dev = eng.dev

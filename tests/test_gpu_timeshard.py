@@ -137,7 +137,31 @@ def _free_port():
     return p
 
 
-def _gloo_worker(rank, world, port, out):
+@pytest.mark.parametrize("world,N,L,T,maxiter,tol", [(3, 48, 128, 6000, 1000, 1e-6), (2, 40, 100, 4000, 40, 0.0),
+                                                     (4, 64, 600, 3000, 30, 0.0)])
+def test_neuron_sharded_adam_bit_identical(world, N, L, T, maxiter, tol):
+    """Neuron-sharded Adam (speculative batches of 16 bodies, one reduce of the loss
+    partials per batch, replay to the global stop) vs the replicated loop: identical
+    iteration counts and bit-identical W, hence identical tuning and posteriors.
+    L = 600 runs the tiled Adam kernels, the others the persistent kernel."""
+    import poor_man_gplvm_amd as P
+    from poor_man_gplvm_amd.timeshard import run_em_timesharded
+    d = make(N, L, T)
+    kw = dict(n_iter=2, transition=P.banded_transition(L, 1.0), world=world,
+              adam=P.AdamConfig(maxiter=maxiter, tol=tol), chunk=32, halo=256)
+    a, ia = run_em_timesharded(d['y'], d['W0'], d['B'], d['lp0'], **kw)
+    b, ib = run_em_timesharded(d['y'], d['W0'], d['B'], d['lp0'], neuron_sharded=True, **kw)
+    assert a['m_step_res_l']['n_iter'] == b['m_step_res_l']['n_iter']
+    np.testing.assert_array_equal(ia['params64'], ib['params64'])
+    np.testing.assert_array_equal(a['tuning'], b['tuning'])
+    np.testing.assert_array_equal(a['posterior'], b['posterior'])
+    for k in ('final_loss', 'final_error'):
+        np.testing.assert_allclose(a['m_step_res_l'][k], b['m_step_res_l'][k], rtol=1e-12)
+    for x, y in zip(a['m_step_res_l']['loss_history'], b['m_step_res_l']['loss_history']):
+        np.testing.assert_allclose(x, y, rtol=1e-12)
+
+
+def _gloo_worker(rank, world, port, out, neuron_sharded=False):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
@@ -148,9 +172,10 @@ def _gloo_worker(rank, world, port, out):
     L = f['basis'].shape[0]
     res, info = run_em_timesharded(f['y'].astype(np.float32), f['W0'], f['basis'], f['lp0'],
                                    n_iter=int(f['n_iter']), transition=P.banded_transition(L, float(f['mv'])),
-                                   comm=DistComm(), chunk=16, halo=32,
+                                   comm=DistComm(), chunk=16, halo=32, neuron_sharded=neuron_sharded,
                                    adam=P.AdamConfig(maxiter=int(f['maxiter']), tol=float(f['tol'])))
-    out[rank] = None if res is None else (res['posterior_latent_marg'], res['tuning'], res['log_marginal_l'])
+    out[rank] = (info['params64'] if res is None else
+                 (res['posterior_latent_marg'], res['tuning'], res['log_marginal_l'], info['params64']))
     dist.destroy_process_group()
 
 
@@ -160,8 +185,28 @@ def test_timesharded_gloo_two_ranks():
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_gloo_worker, args=(2, _free_port(), out), nprocs=2, join=True)
-    assert out[1] is None
-    plm, tun, lz = out[0]
+    plm, tun, lz, W = out[0]
     np.testing.assert_allclose(tun, f['tuning'], rtol=RT)
     close_prob(plm, f['posterior'].astype(np.float64).sum(1))
     np.testing.assert_allclose(lz, f['log_marginal_l'], rtol=1e-7)
+
+
+def test_timesharded_gloo_two_ranks_neuron_sharded_adam():
+    """Two real ranks (gloo, both on cuda:0), each running Adam on its own neuron block:
+    W on both ranks bit-identical to the replicated single-process run."""
+    import torch.multiprocessing as mp
+    import poor_man_gplvm_amd as P
+    from poor_man_gplvm_amd.timeshard import run_em_timesharded
+    f = np.load(os.path.join(HERE, 'golden', 'em_c1_one.npz'))
+    L = f['basis'].shape[0]
+    ref, info = run_em_timesharded(f['y'].astype(np.float32), f['W0'], f['basis'], f['lp0'],
+                                   n_iter=int(f['n_iter']), transition=P.banded_transition(L, float(f['mv'])),
+                                   world=2, chunk=16, halo=32,
+                                   adam=P.AdamConfig(maxiter=int(f['maxiter']), tol=float(f['tol'])))
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_gloo_worker, args=(2, _free_port(), out, True), nprocs=2, join=True)
+    plm, tun, lz, W0 = out[0]
+    np.testing.assert_array_equal(W0, info['params64'])
+    np.testing.assert_array_equal(out[1], info['params64'])
+    np.testing.assert_array_equal(tun, ref['tuning'])

@@ -101,3 +101,70 @@ def test_distcomm_gloo_matches_localcomm():
     g0 = out[0][4]
     assert len(g0) == 2 and out[1][4] == []
     np.testing.assert_array_equal(g0[1], np.arange(4, dtype=np.float32) + 10)
+
+
+# ---------------------------------------------------------------- neuron-sharded Adam
+def _kernel_mimic(W, mu, nu, count, kmax, tol, a, c, lr=0.01, b1=0.9, b2=0.999, eps=1e-8):
+    """The persistent kernel's loop semantics on a separable objective
+    f(W) = sum_n 0.5 a_n (w_n - c_n)^2 (stop rule of fit_tuning_helper.py:154-164;
+    loss_hist[0] = loss_0, loss_hist[j+1] = loss_j; W after the stopping body)."""
+    def loss_grad(w):
+        return 0.5 * np.sum(a * (w - c) ** 2), a * (w - c)
+    lh, eh = [], []
+    if kmax <= 1:
+        l0, g0 = loss_grad(W)
+        return 1, np.array([l0]), np.array([np.sqrt(np.sum(g0 ** 2))])
+    prev = None
+    for j in range(10 ** 6):
+        loss, g = loss_grad(W)
+        lh.append(loss)
+        eh.append(np.sqrt(np.sum(g ** 2)))
+        count[0] += 1
+        mu[:] = (1 - b1) * g + b1 * mu
+        nu[:] = (1 - b2) * g * g + b2 * nu
+        mh = mu / (1 - b1 ** count[0])
+        nh = nu / (1 - b2 ** count[0])
+        W[:] = W - lr * mh / (np.sqrt(nh) + eps)
+        if j == 0:
+            prev = loss
+        rel = abs(loss - prev) / max(abs(loss), 1e-8)
+        cont = (j + 1 < kmax - 1) and ((j + 1 < 5) or (rel > tol))
+        prev = loss
+        if not cont:
+            return j + 2, np.array([lh[0]] + lh), np.array([eh[0]] + eh)
+
+
+@pytest.mark.parametrize("maxiter,tol,world", [(1000, 1e-6, 3), (40, 0.0, 2), (23, 0.0, 4), (1, 1e-6, 2),
+                                               (7, 1e-6, 3)])
+def test_speculative_adam_matches_unsharded(maxiter, tol, world):
+    from poor_man_gplvm_amd.timeshard import neuron_bounds, speculative_adam
+    rng = np.random.default_rng(0)
+    N = 37
+    a = rng.uniform(0.5, 2.0, N)
+    c = rng.normal(size=N)
+    W0 = rng.normal(size=N)
+    # unsharded loop
+    W, mu, nu, cnt = W0.copy(), np.zeros(N), np.zeros(N), [5]
+    n_ref, lh_ref, eh_ref = _kernel_mimic(W, mu, nu, cnt, maxiter, tol, a, c)
+    # neuron-sharded speculative loop (all ranks in this process: the reduce is the identity)
+    bnd = neuron_bounds(N, world)
+    sl = [dict(W=W0[x:y].copy(), mu=np.zeros(y - x), nu=np.zeros(y - x), cnt=[5], a=a[x:y], c=c[x:y])
+          for x, y in bnd]
+
+    def run(kmax):
+        return [_kernel_mimic(d['W'], d['mu'], d['nu'], d['cnt'], kmax, 0.0, d['a'], d['c']) for d in sl]
+
+    def snapshot():
+        return [(d['W'].copy(), d['mu'].copy(), d['nu'].copy(), list(d['cnt'])) for d in sl]
+
+    def restore(snap):
+        for d, (w, m, v, k) in zip(sl, snap):
+            d['W'][:], d['mu'][:], d['nu'][:], d['cnt'][:] = w, m, v, k
+
+    res = speculative_adam(run, snapshot, restore, lambda x: x, maxiter, tol)
+    assert res['n_iter'] == n_ref
+    np.testing.assert_array_equal(np.concatenate([d['W'] for d in sl]), W)
+    assert all(d['cnt'][0] == cnt[0] for d in sl)
+    np.testing.assert_allclose(res['loss_history'], lh_ref, rtol=1e-13)
+    np.testing.assert_allclose(res['error_history'], eh_ref, rtol=1e-13)
+    assert res['final_loss'] == pytest.approx(lh_ref[-1], rel=1e-13)
