@@ -239,7 +239,8 @@ def bench_timeshard(args):
     comm = DistComm() if world > 1 else LocalComm(args.virtual)
     scan = ScanConfig(chunk=args.chunk or None, warmup=args.warm_steps)
     lays = shard_layout(T, comm.world, chunk=args.chunk or None, halo=args.halo, scan=scan)
-    eng = TimeShardedEM(y, B, banded_transition(L, 1.0, 0.01, 0.01), comm, lays, scan)
+    eng = TimeShardedEM(y, B, banded_transition(L, 1.0, 0.01, 0.01), comm, lays, scan,
+                        neuron_sharded=not args.replicated_adam)
     for s in eng.shards:
         s.set_log_posterior(np.asarray(lp0[s.lay.ext_start:s.lay.ext_stop]))
         if args.warm_fb:
@@ -307,7 +308,8 @@ def bench_timeshard(args):
                                f"time-sharded over {comm.world} shard(s) ({n} per process), halo {args.halo}; "
                                f"one EM iteration per step",
                    "n_neuron": N, "n_time": T, "n_latent_bin": L,
-                   "parallelism": f"time shards x{comm.world} (RCCL all-reduce of y_w/t_w + carry send/recv)"},
+                   "parallelism": f"time shards x{comm.world} (RCCL all-reduce of y_w/t_w + carry send/recv"
+                                  + (", neuron-sharded Adam)" if eng.neuron_sharded else ")")},
         "roofline": roof_dom,
         "rooflines": rooflines,
         "kernels_ms": {k: round(v[1], 4) for k, v in summ.items()},
@@ -341,6 +343,8 @@ def main():
                          "recording (strong scaling, RCCL suff-stat all-reduce + carry hand-off)")
     ap.add_argument("--virtual", type=int, default=1, help="time shards per process (single-GPU rehearsal)")
     ap.add_argument("--halo", type=int, default=512, help="time-shard halo (steps)")
+    ap.add_argument("--replicated-adam", action="store_true",
+                    help="time shards: run the whole Adam loop on every rank instead of one neuron block each")
     args = ap.parse_args()
     if args.shard == "time":
         return bench_timeshard(args)
