@@ -131,6 +131,7 @@ __global__ void k_adam_prologue(unsigned long long* __restrict__ lpart, unsigned
 // ---------------------------------------------------------------------------
 constexpr int kNW = kThreads / 64;          // waves (the last one also runs the decision)
 constexpr int kRefresh = 16;
+typedef float f2v __attribute__((ext_vector_type(2)));   // row pairs: v_pk_fma_f32 operands
 
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double v) {
@@ -255,13 +256,16 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
   const bool is_el = eq < NB && es < S;
 
   // ---- one-time loads -------------------------------------------------------
-  float bb[A][BC];
+  // the thread's basis block as row pairs (rows 2i, 2i+1): both contractions run on
+  // packed FMAs (v_pk_fma_f32), two rows per instruction
+  f2v bb[A / 2][BC];
 #pragma unroll
-  for (int i = 0; i < A; ++i)
+  for (int i = 0; i < A / 2; ++i)
 #pragma unroll
     for (int k = 0; k < BC; ++k) {
-      const int l = lb * A + i, q = qb * BC + k;
-      bb[i][k] = (l < L && q < NB) ? p.basis[(size_t)l * NB + q] : 0.f;
+      const int l = lb * A + 2 * i, q = qb * BC + k;
+      bb[i][k].x = (l < L && q < NB) ? p.basis[(size_t)l * NB + q] : 0.f;
+      bb[i][k].y = (l + 1 < L && q < NB) ? p.basis[(size_t)(l + 1) * NB + q] : 0.f;
     }
   double yws[SP];
 #pragma unroll
@@ -324,7 +328,10 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
         for (int k4 = 0; k4 < BC; ++k4) {
           const double w = sW[s * QS + qb * BCP + k4];
 #pragma unroll
-          for (int i = 0; i < A; ++i) x[i] = fma((double)bb[i][k4], w, x[i]);
+          for (int i = 0; i < A / 2; ++i) {
+            x[2 * i] = fma((double)bb[i][k4].x, w, x[2 * i]);
+            x[2 * i + 1] = fma((double)bb[i][k4].y, w, x[2 * i + 1]);
+          }
         }
         F = reduce_scatter16<A>(x);
       } else {
@@ -339,11 +346,12 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
         }
         float x[A];
 #pragma unroll
-        for (int i = 0; i < A; ++i) {
-          float a = 0.f;
+        for (int i = 0; i < A / 2; ++i) {
+          f2v a = {0.f, 0.f};
 #pragma unroll
-          for (int k4 = 0; k4 < BC; ++k4) a = fmaf(bb[i][k4], dw[k4], a);
-          x[i] = a;
+          for (int k4 = 0; k4 < BC; ++k4) a = __builtin_elementwise_fma(bb[i][k4], (f2v){dw[k4], dw[k4]}, a);
+          x[2 * i] = a.x;
+          x[2 * i + 1] = a.y;
         }
         F = Fs[s] + (double)reduce_scatter16<A>(x);
       }
@@ -365,32 +373,41 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
     }
     // ---- phase B: B^T G partials (G of the block from wave-local LDS) ---------------
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's G stores are visible
-    float gp[SP][BC];
+    // packed over row pairs: acc.x sums the even rows, acc.y the odd ones
+    f2v gacc[SP][BC];
 #pragma unroll
     for (int s = 0; s < SP; ++s)
 #pragma unroll
-      for (int k4 = 0; k4 < BC; ++k4) gp[s][k4] = 0.f;
+      for (int k4 = 0; k4 < BC; ++k4) gacc[s][k4] = (f2v){0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < A; ++i) {
-      float gl[SP];
-      const float* src = &sG[(lb * A + i) * SP];
-      if constexpr (SP == 1) gl[0] = src[0];
-      else if constexpr (SP == 2) {
+    for (int i = 0; i < A / 2; ++i) {
+      f2v gl[SP];                                      // (G[2i][s], G[2i+1][s])
+      const float* src = &sG[(lb * A + 2 * i) * SP];
+      if constexpr (SP == 1) {
         const float2 v = *reinterpret_cast<const float2*>(src);
-        gl[0] = v.x;
-        gl[1] = v.y;
-      } else {
+        gl[0] = (f2v){v.x, v.y};
+      } else if constexpr (SP == 2) {
         const float4 v = *reinterpret_cast<const float4*>(src);
-        gl[0] = v.x;
-        gl[1] = v.y;
-        gl[2] = v.z;
-        gl[3] = v.w;
+        gl[0] = (f2v){v.x, v.z};
+        gl[1] = (f2v){v.y, v.w};
+      } else {
+        const float4 v0 = *reinterpret_cast<const float4*>(src);
+        const float4 v1 = *reinterpret_cast<const float4*>(src + 4);
+        gl[0] = (f2v){v0.x, v1.x};
+        gl[1] = (f2v){v0.y, v1.y};
+        gl[2] = (f2v){v0.z, v1.z};
+        gl[3] = (f2v){v0.w, v1.w};
       }
 #pragma unroll
       for (int s = 0; s < SP; ++s)
 #pragma unroll
-        for (int k4 = 0; k4 < BC; ++k4) gp[s][k4] = fmaf(bb[i][k4], gl[s], gp[s][k4]);
+        for (int k4 = 0; k4 < BC; ++k4) gacc[s][k4] = __builtin_elementwise_fma(bb[i][k4], gl[s], gacc[s][k4]);
     }
+    float gp[SP][BC];
+#pragma unroll
+    for (int s = 0; s < SP; ++s)
+#pragma unroll
+      for (int k4 = 0; k4 < BC; ++k4) gp[s][k4] = gacc[s][k4].x + gacc[s][k4].y;
 #pragma unroll
     for (int s = 0; s < SP; ++s)
 #pragma unroll
