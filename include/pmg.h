@@ -137,7 +137,9 @@ int pmg_emission_gaussian_dt(const float* y, const double* tuning64, const float
                              int32_t N, float* delta, double* rblk, void* stream);
 /* Analytic M-step, fit_tuning_helper.gaussian_m_step_analytic (:44-61):          */
 /* W (NB,N) f64 = solve(B^T diag(t_w) B / s^2 + I / p^2, B^T y_w / s^2), Cholesky */
-/* in f64 (H is SPD).  status (device int32) = 1 if a pivot was not positive.      */
+/* in f64 (H is SPD).  status (device int32) is sticky: set to 1 when a pivot was  */
+/* not positive (W is then NaN), never cleared -- the caller zeroes it, e.g. once   */
+/* per fit, and checks it after the last M-step.                                   */
 size_t pmg_gaussian_mstep_workspace_size(int32_t NB, int32_t N);
 int pmg_gaussian_mstep(const float* basis, const double* yw, const double* tw, int32_t L, int32_t NB, int32_t N,
                        double noise_std, double prior_std, double* W, int32_t* status, void* workspace,
@@ -177,6 +179,10 @@ int pmg_forward_filter(const float* delta, const float* phi, const double* m, in
 /* (:313-326), in the equivalent alpha-beta form                          */
 /*   gamma_t = alpha_t * beta_t / sum,  beta_{T-1} = 1,                   */
 /*   beta_t = Trans (e_{t+1} * beta_{t+1}).                               */
+/* The call must run on the workspace of the forward call that produced   */
+/* alpha: it reads only alpha's d = 0 rows and rebuilds the d = 1 rows     */
+/* (jump * e_t / S_t, bit-exact) from per-step scalars that forward left   */
+/* in the workspace.                                                       */
 /* outputs (either may be NULL): P (T,L) f32 = sum_d gamma (the dynamics  */
 /* marginal of core.py:668, exponentiated); gamma (T,2,L) f32.            */
 /* rho (T,2,L) f32 (NULL = skip): rho_t = e_t*beta_t/N_{t-1} with         */
@@ -189,6 +195,10 @@ int pmg_backward_smoother(const float* delta, const float* phi, const float* alp
 /* The same two calls split in phases (1 = the chunk-parallel main pass,   */
 /* 2 = boundary verification, repair rounds and, forward, the logZ sum;    */
 /* 3 = both = the calls above).  Lets a caller time the main kernel alone. */
+/* Forward only: OR PMG_PHASE_NO_JUMP_ROWS into phase to leave alpha's    */
+/* d = 1 rows unwritten (their values are jump_t * e_t / S_t; the backward */
+/* rebuilds them), for callers that read only P / logZ (an EM iteration). */
+#define PMG_PHASE_NO_JUMP_ROWS 4
 int pmg_forward_filter_phase(const float* delta, const float* phi, const double* m, int64_t T,
                              const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                              int32_t warmup, double tol, float* alpha, double* logc, double* logz,

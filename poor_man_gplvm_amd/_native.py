@@ -23,6 +23,8 @@ STATE_FWD_IN, STATE_FWD_OUT, STATE_BWD_IN, STATE_BWD_FIRST = 0, 1, 2, 3
 # a forward block and a backward block, each {chunks recomputed, relaxation rounds, timeout}
 CTL_WORDS, CTL_FWD, CTL_BWD = 32, 0, 16
 CTL_REPAIRS, CTL_ROUNDS, CTL_ERR = 0, 1, 2
+# pmg_forward_filter_phase flag: alpha's d = 1 rows are not written (PMG_PHASE_NO_JUMP_ROWS)
+PHASE_NO_JUMP_ROWS = 4
 ABI_VERSION = 1
 
 # every symbol the header declares (checked by tests/test_capi_symbols.py)

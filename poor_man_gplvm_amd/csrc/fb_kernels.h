@@ -97,8 +97,13 @@ struct FBParams {
   double* logz;
   float* s_in;
   float* s_out;
+  // per step (jump mass, 1/S) of the forward (T x 2 f32, in the workspace): alpha's d = 1
+  // row is jump * e_t / S, so the backward rebuilds it bit-exactly from e_t and these
+  float* jsc;
+  uint32_t a1_bytes;  // bytes of alpha's d = 1 rows the forward stores (4 L, or 0: omitted)
   // backward
-  const float* alpha_in;
+  const float* alpha_in;  // only the d = 0 rows are read
+  float* w_first;         // per chunk: alpha at its first step, (2, Lpad) (boundary weights)
   float* P;
   float* gamma;
   float* rho;
@@ -204,7 +209,8 @@ __device__ __forceinline__ float chain_sum(float a) { return wave_sum(a); }
 // Hilbert projective distance between two non-negative (2, Lpad) states.
 // Unweighted (state space): components below 1e-30 of the max on both sides are
 // ignored, a component above 1e-20 on one side only counts as a failure.  Weighted by
-// w (the alpha row in its (2, L) layout; backward boundaries compare the POSTERIOR,
+// w (alpha at the boundary in a (2, Lw) layout -- the scans pass the (2, Lpad) rows of
+// w_first, entries past L zero; backward boundaries compare the POSTERIOR,
 // |posterior| <= 1): components below 1e-14 move no output by more than 1e-14
 // absolute (parity atol 1e-12); above it the ratio spread bounds the relative error.
 // ---------------------------------------------------------------------------
@@ -266,9 +272,9 @@ __device__ __forceinline__ float hilbert_dist(const float* __restrict__ x, const
 }
 
 // same metric, x held in registers in the (2, Lpad) lane layout, y in memory;
-// optional weights w in the (2, L) alpha-row layout
+// optional weights w in a (2, L) layout (L = Lpad for w_first rows)
 template <int J>
-__device__ float hilbert_reg(const float x0[J], const float x1[J], const float* __restrict__ y, int Lpad, int j0,
+__device__ __forceinline__ float hilbert_reg(const float x0[J], const float x1[J], const float* __restrict__ y, int Lpad, int j0,
                              const float* __restrict__ w = nullptr, int L = 0) {
   float a[2 * J], b[2 * J];
 #pragma unroll
@@ -317,6 +323,7 @@ template <int J, int WP>
 struct Fwd {
   float p0[J], p1[J];
   float P0, P1;  // sum of p0, p1 (wave-uniform)
+  float jmp, iS; // the last step's jump mass and 1/S: p1 = (jmp * e) * iS
 
   __device__ void init_uniform(const FBParams& p, int j0) {
     const float u = 0.5f * p.invL;
@@ -383,6 +390,8 @@ struct Fwd {
     }
     P0 = U0 * inv;
     P1 = U1 * inv;
+    jmp = jump;
+    iS = inv;
     return S;
   }
 };
@@ -419,9 +428,10 @@ __device__ __forceinline__ void bload_row(const float* row, int L, int j0, float
   }
 }
 
+// bytes: the row's extent (lanes past it drop their stores; 0 = the row is not written)
 template <int J, bool VEC>
-__device__ __forceinline__ void bstore_row(float* row, int L, int j0, const float v[J]) {
-  const __amdgpu_buffer_rsrc_t rs = rsrc_of(row, (uint32_t)L * 4u);
+__device__ __forceinline__ void bstore_row_n(float* row, uint32_t bytes, int j0, const float v[J]) {
+  const __amdgpu_buffer_rsrc_t rs = rsrc_of(row, bytes);
   if constexpr (VEC) {
 #pragma unroll
     for (int j = 0; j < J; j += 4) {
@@ -436,6 +446,19 @@ __device__ __forceinline__ void bstore_row(float* row, int L, int j0, const floa
 #pragma unroll
     for (int j = 0; j < J; ++j) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[j]), rs, (j0 + j) * 4, 0, 0);
   }
+}
+
+template <int J, bool VEC>
+__device__ __forceinline__ void bstore_row(float* row, int L, int j0, const float v[J]) {
+  bstore_row_n<J, VEC>(row, (uint32_t)L * 4u, j0, v);
+}
+
+// two f32 per step (x at 2t, y at 2t + 1) written by lane 0 only
+__device__ __forceinline__ void bstore_pair_lane0(float* base, int64_t t, float x, float y) {
+  const __amdgpu_buffer_rsrc_t rs = rsrc_of(base + 2 * t, 8u);
+  const int off = (threadIdx.x & 63) == 0 ? 0 : 64;
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), rs, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y), rs, off + 4, 0, 0);
 }
 
 // one f64 per step written by lane 0 only (the other lanes' offsets are out of range)
@@ -483,7 +506,8 @@ __device__ __forceinline__ double fwd_stream(const FBParams& p, Fwd<J, WP>& st, 
     if constexpr (OUT) {
       float* arow = p.alpha + t * 2 * (int64_t)p.L;
       bstore_row<J, VEC>(arow, p.L, j0, st.p0);
-      bstore_row<J, VEC>(arow + p.L, p.L, j0, st.p1);
+      bstore_row_n<J, VEC>(arow + p.L, p.a1_bytes, j0, st.p1);
+      bstore_pair_lane0(p.jsc, t, st.jmp, st.iS);
       const double lc = (double)__logf(S) + p.s_d * mt;
       bstore_f64_lane0(p.logc, t, lc);
       logz += lc;
@@ -620,7 +644,7 @@ __device__ __forceinline__ double wave_sum_fixed(const double* x, int n) {
 // consistent: stop (*stop = c).  Returns true iff the segment's end state (chunk b-1)
 // moved.
 template <int J, int WP, bool VEC>
-__device__ bool fwd_segment(const FBParams& p, Fwd<J, WP>& st, int c0, int b, int j0, const float invz[J],
+__device__ __forceinline__ bool fwd_segment(const FBParams& p, Fwd<J, WP>& st, int c0, int b, int j0, const float invz[J],
                             const int* flg, int& nrep, int* stop = nullptr) {
   const size_t SZ = (size_t)2 * p.Lpad;
   for (int c = c0; c < b; ++c) {
@@ -642,7 +666,7 @@ __device__ bool fwd_segment(const FBParams& p, Fwd<J, WP>& st, int c0, int b, in
 }
 
 template <int J, int WP, bool VEC>
-__device__ void forward_relax(const FBParams& p, int j0, const float invz[J]) {
+__device__ __forceinline__ void forward_relax(const FBParams& p, int j0, const float invz[J]) {
   const size_t SZ = (size_t)2 * p.Lpad;
   const int s = blockIdx.x;
   const int lane = threadIdx.x & 63;
@@ -809,15 +833,42 @@ __device__ __forceinline__ void bwd_stream_warm(const FBParams& p, Bwd<J, WP>& s
 template <int J>
 struct BRow {
   EmRaw<J> em;
-  float a0[J], a1[J];
+  float a0[J];
+  float js, ji;  // the forward's (jump, 1/S) of this step
 };
 
 template <int J, bool VEC>
 __device__ __forceinline__ void brow_load(const FBParams& p, int64_t t, int j0, BRow<J>& r) {
   bem_load<J, VEC>(p, t, j0, r.em);
-  const float* arow = p.alpha_in + t * 2 * (int64_t)p.L;
-  bload_row<J, VEC>(arow, p.L, j0, r.a0);
-  bload_row<J, VEC>(arow + p.L, p.L, j0, r.a1);
+  bload_row<J, VEC>(p.alpha_in + t * 2 * (int64_t)p.L, p.L, j0, r.a0);
+  const __amdgpu_buffer_rsrc_t rs = rsrc_of(p.jsc + 2 * t, 8u);
+  r.js = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, 0, 0, 0));
+  r.ji = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, 4, 0, 0));
+}
+
+// alpha_t's d = 1 row as the forward formed it: (jump * e) * (1/S)
+template <int J>
+__device__ __forceinline__ void alpha1_row(float js, float ji, const float e[J], float a1[J]) {
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    a1[j] = js * e[j];
+    a1[j] *= ji;
+  }
+}
+
+// the boundary weights of chunk c: alpha at its first step t_c, (2, Lpad) layout
+template <int J, bool VEC>
+__device__ __forceinline__ void store_weights(const FBParams& p, int64_t t_c, int j0, float* dst) {
+  BRow<J> r;
+  brow_load<J, VEC>(p, t_c, j0, r);
+  float e[J], a1[J];
+  em_exp<J>(p, j0, r.em, e);
+  alpha1_row<J>(r.js, r.ji, e, a1);
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    dst[j0 + j] = r.a0[j];
+    dst[p.Lpad + j0 + j] = a1[j];
+  }
 }
 
 // output steps t = t_e-1 .. t_c; on entry st = beta_{t_e-1} and (vp0, vp1) the v that
@@ -834,12 +885,10 @@ __device__ __forceinline__ void bwd_stream_out(const FBParams& p, Bwd<J, WP>& st
   for (int q = 0; q < PF; ++q) brow_load<J, VEC>(p, t_e - 1 - q > t_c ? t_e - 1 - q : t_c, j0, ring[q]);
   auto body = [&](int q, int64_t t, bool refill) {
     float a0[J], a1[J], e[J];
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      a0[j] = ring[q].a0[j];
-      a1[j] = ring[q].a1[j];
-    }
     em_exp<J>(p, j0, ring[q].em, e);
+#pragma unroll
+    for (int j = 0; j < J; ++j) a0[j] = ring[q].a0[j];
+    alpha1_row<J>(ring[q].js, ring[q].ji, e, a1);
     if (refill) brow_load<J, VEC>(p, t - PF > t_c ? t - PF : t_c, j0, ring[q]);
     float G = 0.f, V0 = 0.f, V1 = 0.f;
 #pragma unroll
@@ -916,6 +965,7 @@ __device__ __forceinline__ void backward_chunk(const FBParams& p, int c, int j0,
   }
   bwd_stream_out<J, WP, kPfBwdOut, VEC, MODE>(p, st, j0, invz, t_c, t_e, vp0, vp1, has_prev);
   st.save_state(p, p.b_first + (size_t)c * SZ, j0);
+  store_weights<J, VEC>(p, t_c, j0, p.w_first + (size_t)c * SZ);
 }
 
 #define PMG_BWD_DISPATCH(MODE)                                          \
@@ -957,7 +1007,7 @@ __global__ void __launch_bounds__(64) k_backward_full(FBParams p) {
 // iff the segment's end state (b_first[a]) moved; otherwise *stop = the chunk it
 // settled at.
 template <int J, int WP, bool VEC>
-__device__ bool bwd_segment(const FBParams& p, Bwd<J, WP>& st, int c0, int a, int j0, const float invz[J],
+__device__ __forceinline__ bool bwd_segment(const FBParams& p, Bwd<J, WP>& st, int c0, int a, int j0, const float invz[J],
                             const int* flg, int& nrep, int* stop = nullptr) {
   const size_t SZ = (size_t)2 * p.Lpad;
   for (int c = c0; c >= a; --c) {
@@ -969,7 +1019,7 @@ __device__ bool bwd_segment(const FBParams& p, Bwd<J, WP>& st, int c0, int a, in
     bwd_stream_out<J, WP, pf_relax_bwd<J>(), VEC, 1>(p, st, j0, invz, t_c, t_e, vp0, vp1, true);
     ++nrep;
     float* bf = p.b_first + (size_t)c * SZ;
-    const float d = hilbert_reg<J>(st.b0, st.b1, bf, p.Lpad, j0, p.alpha_in + t_c * 2 * (int64_t)p.L, p.L);
+    const float d = hilbert_reg<J>(st.b0, st.b1, bf, p.Lpad, j0, p.w_first + (size_t)c * SZ, p.Lpad);
     st.save_state(p, bf, j0);
     if (d <= p.tol && (c == a || !(flg && flg[c - 1]))) {
       if (stop) *stop = c;
@@ -980,7 +1030,7 @@ __device__ bool bwd_segment(const FBParams& p, Bwd<J, WP>& st, int c0, int a, in
 }
 
 template <int J, int WP, bool VEC>
-__device__ void backward_relax(const FBParams& p, int j0, const float invz[J]) {
+__device__ __forceinline__ void backward_relax(const FBParams& p, int j0, const float invz[J]) {
   const size_t SZ = (size_t)2 * p.Lpad;
   const int s = blockIdx.x;
   const int lane = threadIdx.x & 63;
@@ -1009,8 +1059,8 @@ __device__ void backward_relax(const FBParams& p, int j0, const float invz[J]) {
       changed = false;
       if (s + 1 < p.S && p.seg_chg[(k & 1) * p.S + s + 1]) {
         const float* X = p.seg_end + ((size_t)(k & 1) * p.S + s + 1) * SZ;
-        const float* w = p.alpha_in + (int64_t)b * p.C * 2 * (int64_t)p.L;
-        const float d = hilbert_dist(p.b_in + (size_t)(b - 1) * SZ, X, (int)SZ, w, p.L, p.Lpad);
+        const float* w = p.w_first + (size_t)b * SZ;
+        const float d = hilbert_dist(p.b_in + (size_t)(b - 1) * SZ, X, (int)SZ, w, p.Lpad, p.Lpad);
         if (!(d <= p.tol)) {
           st.load_state(p, X, j0);
           changed = bwd_segment<J, WP, VEC>(p, st, b - 1, a, j0, invz, nullptr, nrep);

@@ -9,21 +9,22 @@ namespace pmg {
 // boundary also snapshots y[c + off] into x[c] (the restart state of the relaxation)
 // and counts itself in *pending.
 // Backward (w != nullptr): both betas are weighted by alpha at the boundary time
-// t_e = (c+1) C, i.e. the POSTERIOR at t_e is compared.  An error of beta_{t_e}(j)
+// t_e = (c+1) C (w[c+1], the (2, Lpad) w_first slot of chunk c+1), i.e. the POSTERIOR at
+// t_e is compared.  An error of beta_{t_e}(j)
 // reaches gamma_t(i), t < t_e, only through the joint P(x_t = i, x_{t_e} = j) <=
 // gamma_{t_e}(j), so components with negligible posterior cannot move any output
 // above ~1e-18 probability, while they are exactly the ones the chain forgets slowly.
 __global__ void __launch_bounds__(256) k_verify(float* __restrict__ x, const float* __restrict__ y,
                                                 int first, int last, int off, int SZ, float tol,
                                                 int* __restrict__ flags, const float* __restrict__ w,
-                                                int C, int L, int Lpad, int* __restrict__ pending) {
+                                                int Lpad, int* __restrict__ pending) {
   const int wv = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int c = first + wv;
   if (c > last) return;
   const float* yc = y + (size_t)(c + off) * SZ;
   float* xc = x + (size_t)c * SZ;
-  const float* wc = w ? w + (size_t)(c + 1) * C * 2 * L : nullptr;
-  const float d = hilbert_dist(xc, yc, SZ, wc, L, Lpad);
+  const float* wc = w ? w + (size_t)(c + 1) * SZ : nullptr;
+  const float d = hilbert_dist(xc, yc, SZ, wc, Lpad, Lpad);
   const bool bad = !(d <= tol);
   if ((threadIdx.x & 63) == 0) {
     flags[c] = bad ? 1 : 0;
@@ -38,20 +39,24 @@ __global__ void __launch_bounds__(256) k_verify(float* __restrict__ x, const flo
 // ---------------------------------------------------------------------------
 struct FBWork {
   int* ctl;       // control words: forward block at 0, backward at kCtlStride
-  float *s_in, *s_out, *b_in, *b_first;
+  float* jsc;     // (T, 2) the forward's per-step (jump, 1/S)
+  float *s_in, *s_out, *b_in, *b_first, *w_first;
   double* chunk_logz;
   int* flags;
   float* seg_end;  // [2][kRelaxMaxSeg][2*Lpad]
   int* seg_chg;    // [2][kRelaxMaxSeg]
 };
 
-// workspace layout (the Python diagnostics mirror it): ctl[64] | s_in | s_out | b_in |
-// b_first (M x 2 x Lpad f32 each) | chunk_logz[M] | flags[M] | seg_end | seg_chg
+// workspace layout (the Python diagnostics mirror it): ctl[64] | jsc[2T] | s_in | s_out |
+// b_in | b_first (M x 2 x Lpad f32 each) | chunk_logz[M] | flags[M] | seg_end | seg_chg |
+// w_first (M x 2 x Lpad).  ctl and jsc sit before anything sized by the chunk, so the
+// forward (chunk C) and the backward (chunk Cb) agree on them.
 static FBWork carve_fb(void* ws, int64_t T, int Lpad, int C, size_t* total = nullptr) {
   const int64_t M = (T + C - 1) / C;
   Carver c(ws);
   FBWork w;
   w.ctl = c.take<int>(64);
+  w.jsc = c.take<float>((size_t)2 * T);
   w.s_in = c.take<float>((size_t)M * 2 * Lpad);
   w.s_out = c.take<float>((size_t)M * 2 * Lpad);
   w.b_in = c.take<float>((size_t)M * 2 * Lpad);
@@ -60,6 +65,7 @@ static FBWork carve_fb(void* ws, int64_t T, int Lpad, int C, size_t* total = nul
   w.flags = c.take<int>(M);
   w.seg_end = c.take<float>((size_t)2 * kRelaxMaxSeg * 2 * Lpad);
   w.seg_chg = c.take<int>(2 * kRelaxMaxSeg);
+  w.w_first = c.take<float>((size_t)M * 2 * Lpad);
   if (total) *total = c.off + 256;
   return w;
 }
@@ -209,6 +215,8 @@ static int forward_impl(const float* delta, const float* phi, const double* m, i
   p.logc = logc;
   p.logz = logz;
   p.chunk_logz = w.chunk_logz;
+  p.jsc = w.jsc;
+  p.a1_bytes = (phase & 4) ? 0u : (uint32_t)p.L * 4u;
   p.s_in = w.s_in;
   p.s_out = w.s_out;
   p.flags = w.flags;
@@ -232,7 +240,7 @@ static int forward_impl(const float* delta, const float* phi, const double* m, i
       int* pend = getenv("PMG_DEBUG_NO_REPAIR") ? p.ctl + kCtlStride - 1 : p.ctl + kCtlPending;
       const int nver = p.M - 1;
       hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4), dim3(256), 0, st, w.s_in, (const float*)w.s_out, 1,
-                         p.M - 1, -1, 2 * p.Lpad, p.tol, w.flags, (const float*)nullptr, 0, 0, 0, pend);
+                         p.M - 1, -1, 2 * p.Lpad, p.tol, w.flags, (const float*)nullptr, p.Lpad, pend);
       PMG_LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(ks.forward_relax, dim3(p.S), dim3(64), 0, st, p);  // also sums logZ
@@ -253,7 +261,7 @@ int pmg_forward_filter_phase(const float* delta, const float* phi, const double*
                              const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                              int32_t warmup, double tol, float* alpha, double* logc, double* logz,
                              void* workspace, size_t workspace_bytes, void* stream, int32_t phase) {
-  PMG_REQUIRE(phase >= 1 && phase <= 3, "pmg_forward_filter_phase: phase %d", phase);
+  PMG_REQUIRE((phase & 3) != 0 && (phase & ~7) == 0, "pmg_forward_filter_phase: phase %d", phase);
   return forward_impl(delta, phi, m, T, tr, likelihood_scale, chunk, warmup, tol, alpha, logc, logz,
                       workspace, workspace_bytes, stream, phase);
 }
@@ -273,6 +281,8 @@ static int backward_impl(const float* delta, const float* phi, const float* alph
   p.delta = delta;
   p.phi = phi;
   p.alpha_in = alpha;
+  p.jsc = w.jsc;
+  p.w_first = w.w_first;
   p.P = P;
   p.gamma = gamma;
   p.rho = rho;
@@ -298,7 +308,7 @@ static int backward_impl(const float* delta, const float* phi, const float* alph
     int* pend = getenv("PMG_DEBUG_NO_REPAIR") ? p.ctl + kCtlStride - 1 : p.ctl + kCtlPending;
     const int nver = p.M - 1;
     hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4), dim3(256), 0, st, w.b_in, (const float*)w.b_first, 0,
-                       p.M - 2, 1, 2 * p.Lpad, p.tol, w.flags, alpha, p.C, p.L, p.Lpad, pend);
+                       p.M - 2, 1, 2 * p.Lpad, p.tol, w.flags, (const float*)w.w_first, p.Lpad, pend);
     PMG_LAUNCH_CHECK();
     hipLaunchKernelGGL(ks.backward_relax, dim3(p.S), dim3(64), 0, st, p);
     PMG_LAUNCH_CHECK();

@@ -168,7 +168,9 @@ __device__ __forceinline__ int tri(int i, int j) { return i * (i + 1) / 2 + j; }
 // Cholesky of H (packed lower triangle in LDS, f64), then Linv = L^{-1} (row-major NB x NB,
 // zero above the diagonal) by one column solve per thread.  One workgroup: NB^3/6 flops for
 // the factor and NB^3/6 for the inverse, with no dependency chain longer than NB^2 per
-// thread.  A non-positive pivot sets the status word (the host raises) and skips Linv.
+// thread.  A non-positive pivot sets the (sticky) status word, which the host checks
+// once per fit, and fills Linv with NaN, so W = NaN: a failed solve never leaves a
+// plausible W built from an older inverse.
 __global__ void __launch_bounds__(256) k_gauss_chol_inv(const double* __restrict__ ws, int NB, int N,
                                                         double* __restrict__ Linv, int* __restrict__ status,
                                                         int x_in_lds) {
@@ -183,9 +185,10 @@ __global__ void __launch_bounds__(256) k_gauss_chol_inv(const double* __restrict
   for (int k = 0; k < NB; ++k) {
     const double piv = sA[tri(k, k)];
     __syncthreads();
-    if (!(piv > 0.0)) {
+    if (!(piv > 0.0)) {   // uniform across the workgroup: every thread read the same pivot
       if (tid == 0) status[0] = 1;
-      return;   // uniform across the workgroup: every thread read the same pivot
+      for (int e = tid; e < NB * NB; e += 256) Linv[e] = __builtin_nan("");
+      return;
     }
     const double r = sqrt(piv);
     for (int i = k + 1 + tid; i < NB; i += 256) sA[tri(i, k)] /= r;
@@ -294,7 +297,6 @@ int pmg_gaussian_mstep(const float* basis, const double* yw, const double* tw, i
   PMG_REQUIRE(workspace_bytes >= pmg_gaussian_mstep_workspace_size(NB, N), "pmg_gaussian_mstep: workspace too small");
   hipStream_t st = as_stream(stream);
   double* ws = reinterpret_cast<double*>(workspace);
-  PMG_HIP(hipMemsetAsync(status, 0, sizeof(int32_t), st));
   hipLaunchKernelGGL(k_gauss_normal_eq, dim3((unsigned)((N + NB + 255) / 256), (unsigned)NB), dim3(256), 0, st,
                      basis, yw, tw, L, NB, N, 1.0 / (noise_std * noise_std), 1.0 / (prior_std * prior_std), ws);
   PMG_LAUNCH_CHECK();

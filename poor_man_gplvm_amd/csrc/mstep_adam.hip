@@ -11,8 +11,8 @@
 //
 // MI355X design: the objective separates over neurons except for the scalar loss
 // the stop rule reads.  Workgroups own disjoint neuron columns (one workgroup per
-// CU, all co-resident), keep the basis in registers twice (row-major for f = B W,
-// column groups for B^T G), run Adam on their own columns in f64 and publish a
+// CU, all co-resident), keep the basis in registers once (a 2-D block per thread,
+// see "Basis layout" below), run Adam on their own columns in f64 and publish a
 // f64 partial loss / squared gradient norm per iteration.  Instead of a grid
 // barrier per iteration, every workgroup runs LAG iterations ahead and decides
 // "stop after body j" from the globally summed partials of iteration j (summed in

@@ -266,6 +266,7 @@ class DeviceEM:
         self.dense = False          # transition held by the dense log-domain scans
         self.ws_dense = None
         self.log_alpha = None       # (T, 2, L) log filter state (dense scans)
+        self.alpha_bits = 0         # phase bits of the last forward (PHASE_NO_JUMP_ROWS or 0)
         self.ma_latent = None
         # Gaussian observation model (GaussianGPLVMJump1D): when noise_std is set, the
         # emission, tuning and M-step dispatch to gaussian.hip; the scans are shared.
@@ -368,8 +369,8 @@ class DeviceEM:
 
     def gaussian_m_step(self, W):
         """Analytic M-step of the Gaussian model (fit_tuning_helper.py:44-61) from the
-        current y_w, t_w; W (NB, N) f64 overwritten.  A non-SPD system sets the status
-        word, checked by gaussian_status() (no host sync here)."""
+        current y_w, t_w; W (NB, N) f64 overwritten.  A non-SPD system sets the sticky
+        status word (and W = NaN), checked by gaussian_status() (no host sync here)."""
         need = int(self.lib.pmg_gaussian_mstep_workspace_size(self.NB, self.N))
         if self._ws_gm is None or self._ws_gm.numel() < need:
             self._ws_gm = torch.empty(need, dtype=torch.uint8, device=self.dev)
@@ -382,9 +383,13 @@ class DeviceEM:
                                                 self._ws_gm.numel(), nat.stream_handle()), "pmg_gaussian_mstep")
 
     def gaussian_status(self):
-        """Raise if the last Gaussian M-step met a non-positive pivot (device read: syncs)."""
-        if self._gstatus is not None and int(self._gstatus.item()) != 0:
-            raise nat.NativeError("pmg_gaussian_mstep: normal-equation matrix is not positive definite")
+        """Raise if any Gaussian M-step since the last check met a non-positive pivot
+        (device read: syncs); the sticky word is cleared for the next fit."""
+        if self._gstatus is not None:
+            bad = int(self._gstatus.item()) != 0
+            self._gstatus.zero_()
+            if bad:
+                raise nat.NativeError("pmg_gaussian_mstep: normal-equation matrix is not positive definite")
 
     # shapes the persistent one-launch Adam kernel holds (a latent row per thread, the
     # basis row in registers + LDS); larger ones use the tiled per-body kernels
@@ -521,7 +526,9 @@ class DeviceEM:
         self._rep_evt = torch.cuda.Event()
         self._rep_evt.record()
 
-    def forward(self, likelihood_scale, logz_out):
+    def forward(self, likelihood_scale, logz_out, keep_alpha=True):
+        """keep_alpha False: alpha's d = 1 rows are not written (the backward call rebuilds
+        them from per-step scalars; callers that read only P / logZ skip 4 T L bytes)."""
         if self.dense:
             with self._t('forward_filter'):      # main pass + verify + relaxation + logZ
                 nat.check(self.lib.pmg_dense_forward(
@@ -536,10 +543,11 @@ class DeviceEM:
                 float(likelihood_scale), self.C, int(self.warm[0]), float(sc.tol), nat.ptr(self.alpha),
                 nat.ptr(self.logc), nat.ptr(logz_out), nat.ptr(self.ws_fb), self.ws_fb.numel(),
                 nat.stream_handle())
+        self.alpha_bits = 0 if keep_alpha else nat.PHASE_NO_JUMP_ROWS
         with self._t('forward_filter'):          # main chunk-parallel pass (k_forward)
-            nat.check(self.lib.pmg_forward_filter_phase(*args, 1), "pmg_forward_filter")
+            nat.check(self.lib.pmg_forward_filter_phase(*args, 1 | self.alpha_bits), "pmg_forward_filter")
         with self._t('forward_repair'):          # verify / relaxation / logZ
-            nat.check(self.lib.pmg_forward_filter_phase(*args, 2), "pmg_forward_filter")
+            nat.check(self.lib.pmg_forward_filter_phase(*args, 2 | self.alpha_bits), "pmg_forward_filter")
 
     def backward(self, likelihood_scale, P=True, gamma=None, rho=None, log_gamma=None):
         """rho: the joint partner; with the dense scans it is written as log(rho)
@@ -564,9 +572,12 @@ class DeviceEM:
         with self._t('backward_repair'):         # verify / relaxation
             nat.check(self.lib.pmg_backward_smoother_phase(*args, 2), "pmg_backward_smoother")
 
-    def e_step(self, likelihood_scale, logz_out, gamma=None, rho=None, log_gamma=None):
+    def e_step(self, likelihood_scale, logz_out, gamma=None, rho=None, log_gamma=None, keep_alpha=None):
+        """keep_alpha (default: whenever a posterior output is requested): write alpha in full."""
+        if keep_alpha is None:
+            keep_alpha = gamma is not None or rho is not None or log_gamma is not None
         self.emission(likelihood_scale)
-        self.forward(likelihood_scale, logz_out)
+        self.forward(likelihood_scale, logz_out, keep_alpha)
         self.backward(likelihood_scale, True, gamma, rho, log_gamma)
         self._snapshot_repairs()
 

@@ -386,7 +386,7 @@ class ShardEM(DeviceEM):
                 nat.ptr(self.logc), nat.ptr(logz_scratch), nat.ptr(self.ws_fb), self.ws_fb.numel(),
                 nat.stream_handle())
         with self._t('forward_carry'):
-            nat.check(self.lib.pmg_forward_filter_phase(*args, 2), "pmg_forward_filter")
+            nat.check(self.lib.pmg_forward_filter_phase(*args, 2 | self.alpha_bits), "pmg_forward_filter")
 
     def backward_phase2(self, likelihood_scale, P=True, gamma=None):
         args = (nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.alpha), self.T, ctypes.byref(self._tr_c),
@@ -469,7 +469,7 @@ class TimeShardedEM:
         scratch = torch.empty(1, dtype=torch.float64, device=self.dev)
         for s in self.shards:
             s.emission(likelihood_scale)
-            s.forward(likelihood_scale, scratch)
+            s.forward(likelihood_scale, scratch, keep_alpha=gamma is not None)
         self.carry_rounds[0] = self._carry(0, likelihood_scale, scratch)
         parts = []
         for s in self.shards:

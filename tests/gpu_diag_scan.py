@@ -18,6 +18,7 @@ def carve(ws, T, Lpad, C):
         out[name] = ws[off:off + nbytes].view(dt)
         off += nbytes
     take('repairs', 64, np.int32)
+    take('jsc', 2 * T, np.float32)
     for k in ['s_in', 's_out', 'b_in', 'b_first']:
         take(k, M * 2 * Lpad, np.float32)
     return out, M

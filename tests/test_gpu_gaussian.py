@@ -72,6 +72,40 @@ def test_gaussian_m_step_vs_oracle(N, L, ls):
     np.testing.assert_allclose(tun, m.tuning_basis.astype(np.float64) @ ref, rtol=1e-6, atol=1e-6)
 
 
+def test_gaussian_m_step_failure_is_sticky_and_nan():
+    """A non-positive pivot (here: NaN t_w) sets the status word and makes W NaN; a later
+    good solve neither clears the word nor reuses the failed inverse."""
+    import torch
+    from poor_man_gplvm_amd import _native as nat
+    lib = nat.load()
+    L, NB, N = 64, 12, 40
+    rng = np.random.default_rng(4)
+    dev = torch.device('cuda:0')
+    B = torch.as_tensor(rng.random((L, NB)).astype(np.float32), device=dev)
+    yw = torch.as_tensor(rng.random((L, N)), device=dev)
+    tw_good = torch.as_tensor(rng.random(L) + 1.0, device=dev)
+    tw_bad = tw_good.clone()
+    tw_bad[3] = float('nan')
+    W = torch.zeros((NB, N), dtype=torch.float64, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    ws = torch.empty(int(lib.pmg_gaussian_mstep_workspace_size(NB, N)), dtype=torch.uint8, device=dev)
+
+    def solve(tw):
+        nat.check(lib.pmg_gaussian_mstep(nat.ptr(B), nat.ptr(yw), nat.ptr(tw), L, NB, N, SIG, 1.0, nat.ptr(W),
+                                         nat.ptr(status), nat.ptr(ws), ws.numel(), nat.stream_handle()),
+                  "pmg_gaussian_mstep")
+        torch.cuda.synchronize()
+        return W.cpu().numpy().copy(), int(status.item())
+
+    w0, s0 = solve(tw_good)
+    assert s0 == 0 and np.isfinite(w0).all()
+    w1, s1 = solve(tw_bad)
+    assert s1 == 1 and np.isnan(w1).all()
+    w2, s2 = solve(tw_good)
+    assert s2 == 1, "status must stay set until the caller clears it"
+    np.testing.assert_array_equal(w2, w0)
+
+
 def test_gaussian_decode_vs_oracle():
     import poor_man_gplvm_amd as P
     N, L, T = 30, 100, 1500
