@@ -169,6 +169,9 @@ typedef struct pmg_transition {
 /* outputs: alpha (T,2,L) f32 normalised filter posteriors;              */
 /*          logc (T) f64 one-step predictive marginals (decoder.py:167); */
 /*          logz (1) f64 = sum_t logc (decoder.py:169).                  */
+/* The workspace must be ZERO-FILLED before its first use (one hipMemset);   */
+/* the kernels keep its control words and counters zero between calls, so    */
+/* the scans issue no memsets of their own.                                   */
 size_t pmg_fwdbwd_workspace_size(int64_t T, int32_t L, int32_t chunk);
 int pmg_forward_filter(const float* delta, const float* phi, const double* m, int64_t T,
                        const pmg_transition* tr, double likelihood_scale, int32_t chunk,

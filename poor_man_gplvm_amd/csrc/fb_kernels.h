@@ -59,9 +59,11 @@ template <int J> constexpr int pf_relax_bwd() { return J >= 16 ? 2 : (J >= 8 ? 4
 
 // Control words at the start of the scan workspace (int32), one block per direction
 // (forward at word 0, backward at word kCtlStride):
-//   +0 chunks recomputed, +1 relaxation rounds, +2 timeout flag      (zeroed by phase 1)
-//   +4 boundaries flagged by the verify, +5 barrier arrivals,
-//   +6..+8 segment-end changes of rounds k % 3                       (zeroed by phase 2)
+//   +0 chunks recomputed, +1 relaxation rounds, +2 timeout flag   (zeroed by the main pass)
+//   +4 boundaries flagged by k_verify, +5 barrier arrivals,
+//   +6..+8 segment-end changes of rounds k % 3, +9 relaxation exits
+// Words 4..9 are zero between calls: the workspace starts zero-filled and the last
+// relaxation wave to exit clears them, so no call needs a host memset.
 enum {
   kCtlRepairs = 0,
   kCtlRounds = 1,
@@ -69,9 +71,9 @@ enum {
   kCtlPending = 4,
   kCtlArrive = 5,
   kCtlChanged = 6,
+  kCtlExit = 9,
   kCtlStride = 16,
 };
-constexpr int kCtlPhase2Words = 12;                    // words 4 .. 15 of a block
 constexpr uint64_t kSpinTicks = 200000000ull;          // 2 s of the 100 MHz real-time clock
 constexpr int kRelaxMaxSeg = 512;                      // segment-state slots in the workspace
 
@@ -222,31 +224,43 @@ __device__ __forceinline__ float hilbert_finish(float lo, float hi, int bad) {
   return hi - lo;
 }
 
-// both states in memory, lane-strided (one wave)
+// both states in memory (one wave), n = 2 Lpad floats, optional weights w[i] in the same
+// (2, Lpad) layout.  Every operand is fetched up front with branch-free 16-byte buffer
+// loads (lanes past n read 0), so the wave pays one memory round trip: the predicated
+// scalar loads this replaces were serialised by their branches (k_verify spent 80 % of
+// its ~20 us waiting on memory).
 __device__ __forceinline__ float hilbert_dist(const float* __restrict__ x, const float* __restrict__ y, int n,
-                                              const float* __restrict__ w = nullptr, int L = 0, int Lpad = 0) {
+                                              const float* __restrict__ w = nullptr) {
   const int lane = threadIdx.x & 63;
-  // every operand is fetched up front (n = 2*Lpad <= 2048: at most 32 per lane) so the
-  // wave pays one memory round trip, not one per strided pass
-  constexpr int kMaxPer = 2 * 1024 / 64;
-  float xv[kMaxPer], yv[kMaxPer];
+  constexpr int kQ = 2 * 1024 / 256;  // float4 loads per lane for n <= 2048
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), (short)0, n * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(y), (short)0, n * 4, 0x00020000);
+  const bool weighted = w != nullptr;
+  const __amdgpu_buffer_rsrc_t rw =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(weighted ? w : x), (short)0, n * 4, 0x00020000);
+  float xv[4 * kQ], yv[4 * kQ];
 #pragma unroll
-  for (int q = 0; q < kMaxPer; ++q) {
-    const int i = lane + 64 * q;
-    float wi = 0.f;
-    if (i < n) {
-      wi = 1.f;
-      if (w) {  // state index i = d*Lpad + j
-        const int d = i >= Lpad ? 1 : 0, j = i - d * Lpad;
-        wi = j < L ? w[d * L + j] : 0.f;
-      }
+  for (int q = 0; q < kQ; ++q) {
+    const int off = (lane + 64 * q) * 16;
+    const u4 a = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
+    const u4 b = __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, 0);
+    xv[4 * q] = __uint_as_float(a.x); xv[4 * q + 1] = __uint_as_float(a.y);
+    xv[4 * q + 2] = __uint_as_float(a.z); xv[4 * q + 3] = __uint_as_float(a.w);
+    yv[4 * q] = __uint_as_float(b.x); yv[4 * q + 1] = __uint_as_float(b.y);
+    yv[4 * q + 2] = __uint_as_float(b.z); yv[4 * q + 3] = __uint_as_float(b.w);
+    const u4 c = __builtin_amdgcn_raw_buffer_load_b128(rw, off, 0, 0);  // no branch: selects below
+    const float wc[4] = {__uint_as_float(c.x), __uint_as_float(c.y), __uint_as_float(c.z), __uint_as_float(c.w)};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float f = weighted ? wc[k] : 1.f;
+      xv[4 * q + k] *= f;
+      yv[4 * q + k] *= f;
     }
-    xv[q] = i < n ? x[i] * wi : 0.f;
-    yv[q] = i < n ? y[i] * wi : 0.f;
   }
   float xm = 0.f, ym = 0.f;
 #pragma unroll
-  for (int q = 0; q < kMaxPer; ++q) {
+  for (int q = 0; q < 4 * kQ; ++q) {
     xm = fmaxf(xm, xv[q]);
     ym = fmaxf(ym, yv[q]);
   }
@@ -254,11 +268,11 @@ __device__ __forceinline__ float hilbert_dist(const float* __restrict__ x, const
   ym = wave_max_shfl(ym);
   if (!(xm > 0.f) || !(ym > 0.f)) return INFINITY;
   const float ix = 1.f / xm, iy = 1.f / ym;
-  const float lo_thr = w ? 1e-14f : 1e-30f, hi_thr = w ? 1e-12f : 1e-20f;
+  const float lo_thr = weighted ? 1e-14f : 1e-30f, hi_thr = weighted ? 1e-12f : 1e-20f;
   float lo = INFINITY, hi = -INFINITY;
   int bad = 0;
 #pragma unroll
-  for (int q = 0; q < kMaxPer; ++q) {
+  for (int q = 0; q < 4 * kQ; ++q) {
     const float a = xv[q] * ix, b = yv[q] * iy;
     if (a > lo_thr && b > lo_thr) {
       const float r = __logf(a) - __logf(b);
@@ -541,16 +555,26 @@ __device__ __forceinline__ void forward_chunk(const FBParams& p, int c, int j0, 
   if (t0 < 0) t0 = 0;
   st.init_uniform(p, j0);
   fwd_stream<J, WP, kPfFwd, VEC, false>(p, st, j0, invz, t0, t_c);
-  if (c > 0) st.save_state(p, p.s_in + (size_t)c * SZ, j0);  // the start the verify checks
+  if (c > 0) st.save_state(p, p.s_in + (size_t)c * SZ, j0);  // the start k_verify checks
   const double lz = fwd_stream<J, WP, kPfFwd, VEC, true>(p, st, j0, invz, t_c, t_e);
   st.save_state(p, p.s_out + (size_t)c * SZ, j0);
   if ((threadIdx.x & 63) == 0) p.chunk_logz[c] = lz;
+}
+
+// the main pass clears the per-call words (the relaxation kernels run after it)
+__device__ __forceinline__ void main_pass_reset(const FBParams& p) {
+  if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) {
+    p.ctl[kCtlRepairs] = 0;
+    p.ctl[kCtlRounds] = 0;
+    p.ctl[kCtlErr] = 0;
+  }
 }
 
 template <int J, int WP>
 __global__ void __launch_bounds__(64) k_forward(FBParams p) {
   const int c = blockIdx.x;
   if (c >= p.M) return;
+  main_pass_reset(p);
   PMG_FB_LANE_SETUP
   (void)lane;
   if constexpr (J % 4 == 0) {
@@ -590,6 +614,20 @@ __device__ __forceinline__ bool relax_barrier(int* ctl, int target) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   return __builtin_amdgcn_readfirstlane(ok) != 0;
+}
+
+// After the rounds: the last wave to leave clears the relaxation words for the next
+// call (every wave has finished polling them before it counts its exit).
+__device__ __forceinline__ void relax_exit(const FBParams& p) {
+  if ((threadIdx.x & 63) == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const int old = __hip_atomic_fetch_add(p.ctl + kCtlExit, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == p.S - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      for (int w = kCtlPending; w <= kCtlExit; ++w)
+        __hip_atomic_store(p.ctl + w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 __device__ __forceinline__ int ctl_load(int* ctl, int w) {
@@ -676,7 +714,7 @@ __device__ __forceinline__ void forward_relax(const FBParams& p, int j0, const f
     const int b = a + p.G < p.M ? a + p.G : p.M;
     Fwd<J, WP> st;
     bool changed = false;
-    // round 0: every boundary the verify flagged (it snapshotted the carry into s_in),
+    // round 0: every boundary the verification flagged (it stored the carry into s_in),
     // in order; a pass that settles before the segment end resumes at the next flag
     int c0 = find_flag<1>(p.flags, a > 1 ? a : 1, b);
     while (c0 >= 0) {
@@ -703,6 +741,7 @@ __device__ __forceinline__ void forward_relax(const FBParams& p, int j0, const f
         }
       }
     }
+    relax_exit(p);
   }
   if (lane == 0 && nrep) atomicAdd(p.ctl + kCtlRepairs, nrep);
   if (s == 0) {  // after the last barrier's acquire (or with no repair at all)
@@ -959,7 +998,7 @@ __device__ __forceinline__ void backward_chunk(const FBParams& p, int c, int j0,
     int64_t t_w = t_e + p.B;  // beta guess (ones) at t_w, exact when t_w is the last bin
     if (t_w > p.T - 1) t_w = p.T - 1;
     bwd_stream_warm<J, WP, kPfBwdWarm, VEC>(p, st, j0, invz, t_w, t_e + 1);
-    st.save_state(p, p.b_in + (size_t)c * SZ, j0);  // beta_{t_e}: the start the verify checks
+    st.save_state(p, p.b_in + (size_t)c * SZ, j0);  // beta_{t_e}: the start k_verify checks
     bwd_plain(p, st, j0, invz, t_e, vp0, vp1);       // -> beta_{t_e-1}
     has_prev = true;
   }
@@ -982,6 +1021,7 @@ template <int J, int WP>
 __global__ void __launch_bounds__(64) k_backward(FBParams p) {
   const int c = blockIdx.x;
   if (c >= p.M) return;
+  main_pass_reset(p);
   PMG_FB_LANE_SETUP
   (void)lane;
   PMG_BWD_DISPATCH(0)
@@ -992,6 +1032,7 @@ template <int J, int WP>
 __global__ void __launch_bounds__(64) k_backward_full(FBParams p) {
   const int c = blockIdx.x;
   if (c >= p.M) return;
+  main_pass_reset(p);
   PMG_FB_LANE_SETUP
   (void)lane;
   PMG_BWD_DISPATCH(1)
@@ -1060,13 +1101,14 @@ __device__ __forceinline__ void backward_relax(const FBParams& p, int j0, const 
       if (s + 1 < p.S && p.seg_chg[(k & 1) * p.S + s + 1]) {
         const float* X = p.seg_end + ((size_t)(k & 1) * p.S + s + 1) * SZ;
         const float* w = p.w_first + (size_t)b * SZ;
-        const float d = hilbert_dist(p.b_in + (size_t)(b - 1) * SZ, X, (int)SZ, w, p.Lpad, p.Lpad);
+        const float d = hilbert_dist(p.b_in + (size_t)(b - 1) * SZ, X, (int)SZ, w);
         if (!(d <= p.tol)) {
           st.load_state(p, X, j0);
           changed = bwd_segment<J, WP, VEC>(p, st, b - 1, a, j0, invz, nullptr, nrep);
         }
       }
     }
+    relax_exit(p);
   }
   if (lane == 0) {
     if (nrep) atomicAdd(p.ctl + kCtlRepairs, nrep);

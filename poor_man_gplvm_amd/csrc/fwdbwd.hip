@@ -6,8 +6,8 @@
 namespace pmg {
 
 // boundary verification: flags[c] = hilbert(x[c], y[c + off]) > tol; a failing
-// boundary also snapshots y[c + off] into x[c] (the restart state of the relaxation)
-// and counts itself in *pending.
+// boundary also copies y[c + off] into x[c] (the restart state of the relaxation) and
+// counts itself in *pending.
 // Backward (w != nullptr): both betas are weighted by alpha at the boundary time
 // t_e = (c+1) C (w[c+1], the (2, Lpad) w_first slot of chunk c+1), i.e. the POSTERIOR at
 // t_e is compared.  An error of beta_{t_e}(j)
@@ -18,13 +18,14 @@ __global__ void __launch_bounds__(256) k_verify(float* __restrict__ x, const flo
                                                 int first, int last, int off, int SZ, float tol,
                                                 int* __restrict__ flags, const float* __restrict__ w,
                                                 int Lpad, int* __restrict__ pending) {
-  const int wv = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  // wave-uniform (readfirstlane): the state pointers below feed scalar buffer descriptors
+  const int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   const int c = first + wv;
   if (c > last) return;
   const float* yc = y + (size_t)(c + off) * SZ;
   float* xc = x + (size_t)c * SZ;
   const float* wc = w ? w + (size_t)(c + 1) * SZ : nullptr;
-  const float d = hilbert_dist(xc, yc, SZ, wc, Lpad, Lpad);
+  const float d = hilbert_dist(xc, yc, SZ, wc);
   const bool bad = !(d <= tol);
   if ((threadIdx.x & 63) == 0) {
     flags[c] = bad ? 1 : 0;
@@ -50,7 +51,9 @@ struct FBWork {
 // workspace layout (the Python diagnostics mirror it): ctl[64] | jsc[2T] | s_in | s_out |
 // b_in | b_first (M x 2 x Lpad f32 each) | chunk_logz[M] | flags[M] | seg_end | seg_chg |
 // w_first (M x 2 x Lpad).  ctl and jsc sit before anything sized by the chunk, so the
-// forward (chunk C) and the backward (chunk Cb) agree on them.
+// forward (chunk C) and the backward (chunk Cb) agree on them.  The workspace must be
+// zero-filled before its first use: the kernels then keep the control words zero
+// between calls.
 static FBWork carve_fb(void* ws, int64_t T, int Lpad, int C, size_t* total = nullptr) {
   const int64_t M = (T + C - 1) / C;
   Carver c(ws);
@@ -195,7 +198,8 @@ float* pmg_fwdbwd_state(void* workspace, int64_t T, int32_t L, int32_t chunk, in
   return base + (size_t)c * 2 * (64 * J);
 }
 
-// phase: 1 = speculative chunk-parallel pass, 2 = verify / relaxation / logZ, 3 = both
+// phase bits: 1 = chunk-parallel main pass, 2 = boundary verification + relaxation
+// (+ logZ), 4 = forward: alpha's d = 1 rows not written
 static int forward_impl(const float* delta, const float* phi, const double* m, int64_t T,
                         const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                         int32_t warmup, double tol, float* alpha, double* logc, double* logz,
@@ -229,12 +233,10 @@ static int forward_impl(const float* delta, const float* phi, const double* m, i
   const bool have = fb_set(J, WP, &ks);
   PMG_REQUIRE(have && ks.forward && ks.forward_relax, "pmg_forward_filter: no kernel for J=%d WP=%d", J, WP);
   if (phase & 1) {
-    PMG_HIP(hipMemsetAsync(p.ctl, 0, 4 * sizeof(int), st));  // repairs, rounds, timeout
     hipLaunchKernelGGL(ks.forward, dim3(p.M), dim3(64), 0, st, p);
     PMG_LAUNCH_CHECK();
   }
   if (phase & 2) {
-    PMG_HIP(hipMemsetAsync(p.ctl + kCtlPending, 0, kCtlPhase2Words * sizeof(int), st));
     if (p.M > 1) {
       // PMG_DEBUG_NO_REPAIR (diagnostics): verify only, count nothing, repair nothing
       int* pend = getenv("PMG_DEBUG_NO_REPAIR") ? p.ctl + kCtlStride - 1 : p.ctl + kCtlPending;
@@ -299,12 +301,10 @@ static int backward_impl(const float* delta, const float* phi, const float* alph
   fb_kernel_t kb = !have ? nullptr : (rho || gamma || !P) ? ks.backward_full : ks.backward;
   PMG_REQUIRE(kb && ks.backward_relax, "pmg_backward_smoother: no kernel for J=%d WP=%d", J, WP);
   if (phase & 1) {
-    PMG_HIP(hipMemsetAsync(p.ctl, 0, 4 * sizeof(int), st));
     hipLaunchKernelGGL(kb, dim3(p.M), dim3(64), 0, st, p);
     PMG_LAUNCH_CHECK();
   }
   if ((phase & 2) && p.M > 1) {
-    PMG_HIP(hipMemsetAsync(p.ctl + kCtlPending, 0, kCtlPhase2Words * sizeof(int), st));
     int* pend = getenv("PMG_DEBUG_NO_REPAIR") ? p.ctl + kCtlStride - 1 : p.ctl + kCtlPending;
     const int nver = p.M - 1;
     hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4), dim3(256), 0, st, w.b_in, (const float*)w.b_first, 0,

@@ -96,13 +96,15 @@ __global__ void k_fill_u64(unsigned long long* __restrict__ x, size_t n, unsigne
   for (; i < n; i += stride) x[i] = v;
 }
 
-// Launch prologue: sentinel-fill both partial arrays and tabulate the bias corrections
-// of every body from the Adam step count, c_k = 1 / (1 - b^(count0 + k + 1)).  A closed
-// form per body (not a running product) gives the same bits however the loop is split
-// into launches (the speculative batches of the neuron-sharded M-step).
+// Launch prologue: sentinel-fill both partial arrays, zero the outputs the loop fills
+// sparsely (histories, stats, the timeout word: no host memsets), and tabulate the bias
+// corrections of every body from the Adam step count, c_k = 1 / (1 - b^(count0 + k + 1)).
+// A closed form per body (not a running product) gives the same bits however the loop
+// is split into launches (the speculative batches of the neuron-sharded M-step).
 __global__ void k_adam_prologue(unsigned long long* __restrict__ lpart, unsigned long long* __restrict__ gpart,
                                 size_t n, const int64_t* __restrict__ count, double b1, double b2, int maxiter,
-                                double* __restrict__ bias) {
+                                double* __restrict__ bias, double* __restrict__ loss_hist,
+                                double* __restrict__ err_hist, double* __restrict__ stats, int* __restrict__ timeout) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t q = i; q < n; q += stride) {
@@ -113,7 +115,11 @@ __global__ void k_adam_prologue(unsigned long long* __restrict__ lpart, unsigned
   for (size_t k = i; k < (size_t)maxiter; k += stride) {
     bias[k] = 1.0 / (1.0 - pow(b1, c0 + (double)k + 1.0));
     bias[maxiter + k] = 1.0 / (1.0 - pow(b2, c0 + (double)k + 1.0));
+    loss_hist[k] = 0.0;
+    err_hist[k] = 0.0;
   }
+  if (i < 4) stats[i] = 0.0;
+  if (i == 0) timeout[0] = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -711,12 +717,9 @@ int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const floa
   {
     const size_t n = ((size_t)maxiter + kLag + 2) * G;
     hipLaunchKernelGGL(k_adam_prologue, dim3(256), dim3(256), 0, st, w.lpart, w.gpart, n, (const int64_t*)count,
-                       cfg->b1, cfg->b2, maxiter, w.bias);
+                       cfg->b1, cfg->b2, maxiter, w.bias, loss_hist, err_hist, stats, w.timeout);
     PMG_LAUNCH_CHECK();
   }
-  PMG_HIP(hipMemsetAsync(w.timeout, 0, sizeof(int), st));
-  PMG_HIP(hipMemsetAsync(loss_hist, 0, sizeof(double) * (size_t)maxiter, st));
-  PMG_HIP(hipMemsetAsync(err_hist, 0, sizeof(double) * (size_t)maxiter, st));
   AdamParams p;
   memset(&p, 0, sizeof(p));
   p.W = W;
@@ -749,7 +752,6 @@ int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const floa
   p.timeout = w.timeout;
   p.ring = w.ring;
   p.bias = w.bias;
-  PMG_HIP(hipMemsetAsync(stats, 0, 4 * sizeof(double), st));
   static long long* prof_buf = nullptr;   // debug: per-phase stamps (PMG_ADAM_PROF set)
   const bool prof = getenv("PMG_ADAM_PROF") != nullptr;
   if (prof) {

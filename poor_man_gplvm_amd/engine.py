@@ -247,7 +247,8 @@ class DeviceEM:
         self.yw = torch.empty((L, N), dtype=f64, device=dev)
         self.tw = torch.empty(L, dtype=f64, device=dev)
         self.ws_em = torch.empty(int(self.lib.pmg_emission_workspace_size(T, L, N)), dtype=torch.uint8, device=dev)
-        self.ws_fb = torch.empty(int(self.lib.pmg_fwdbwd_workspace_size(T, L, min(self.C, self.Cb))),
+        # zero-filled once (include/pmg.h): the scan kernels keep its control words zero
+        self.ws_fb = torch.zeros(int(self.lib.pmg_fwdbwd_workspace_size(T, L, min(self.C, self.Cb))),
                                  dtype=torch.uint8, device=dev)
         ss_bytes = (self.lib.pmg_suffstats_bf16_workspace_size(T, L, N) if spikes.ybt is not None
                     else self.lib.pmg_suffstats_workspace_size(T, L, spikes.Np))
