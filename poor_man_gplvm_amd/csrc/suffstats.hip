@@ -221,14 +221,17 @@ static int atb_run(const float* A, int64_t lda, int Mdim, const float* B, int64_
 typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
 constexpr int KB3 = 64, ROW3 = KB3 + 8;
 
-__device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32_t& l) {
-  const uint32_t u = __float_as_uint(x);
-  h = u >> 16;
-  const float r1 = x - __uint_as_float(u & 0xFFFF0000u);
-  const uint32_t u1 = __float_as_uint(r1);
-  m = u1 >> 16;
-  const float r2 = r1 - __uint_as_float(u1 & 0xFFFF0000u);
-  l = __float_as_uint(r2) >> 16;
+// Exact 3-way bf16 split of a pair of f32 values, packed two per dword (value a in the
+// low half): hi = the top 16 bits, mid / lo = those of the successive remainders (each
+// remainder is exact in f32).  3 byte-permutes + 8 ALU ops per pair.
+__device__ __forceinline__ void split3_pair(float a, float b, uint32_t& hw, uint32_t& mw, uint32_t& lw) {
+  const uint32_t ua = __float_as_uint(a), ub = __float_as_uint(b);
+  hw = __builtin_amdgcn_perm(ub, ua, 0x07060302u);
+  const float ra = a - __uint_as_float(ua & 0xFFFF0000u), rb = b - __uint_as_float(ub & 0xFFFF0000u);
+  const uint32_t va = __float_as_uint(ra), vb = __float_as_uint(rb);
+  mw = __builtin_amdgcn_perm(vb, va, 0x07060302u);
+  const float sa = ra - __uint_as_float(va & 0xFFFF0000u), sb = rb - __uint_as_float(vb & 0xFFFF0000u);
+  lw = __builtin_amdgcn_perm(__float_as_uint(sb), __float_as_uint(sa), 0x07060302u);
 }
 
 // bijective XCD-grouping of workgroup ids (consecutive logical ids share an XCD)
@@ -237,6 +240,12 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
+// Per K-tile (64 time steps) each wave issues 24 MFMAs (2 output tiles x 3 parts x 4
+// k-steps) on the current LDS buffer and, in their shadow, splits the NEXT tile's
+// staged P values (16 per thread) into the other buffer: the split arithmetic (VALU)
+// and the MFMAs overlap inside each wave instead of alternating across a barrier.  P
+// rows are fetched with one buffer descriptor per K-tile whose extent ends at the
+// K-slice end, so rows past it read 0 without per-row clamps or selects.
 __global__ void __launch_bounds__(512) k_ptb3(const float* __restrict__ P, int L,
                                               const uint16_t* __restrict__ Ybt, int64_t Tp, int Np,
                                               int64_t K, int64_t KT, int nMT, int nNT, int nKS,
@@ -258,51 +267,49 @@ __global__ void __launch_bounds__(512) k_ptb3(const float* __restrict__ P, int L
 
   // staging: A column m_l = tid & 127, time rows 16*tg .. 16*tg+15 of the K-tile (tg
   // wave-uniform); B row n_l = tid >> 2, time quarter hq = tid & 3 (16 bf16 = 2 x 16 B).
-  // Branch-free: clamped addresses, rows past the K-slice end selected to zero; rows
-  // m >= L / n >= N only feed output rows/columns the reduction drops.
+  // Rows m >= L / n >= N only feed output rows/columns the reduction drops.
   const int m_l = tid & 127, tg = tid >> 7;
   const int n_l = tid >> 2, hq = tid & 3;
   const int mg = mt * TM + m_l;
   const int ng = nt * TN + n_l;
   const int mgc = mg < L ? mg : L - 1;
+  const uint32_t voffA = (uint32_t)(16 * tg * L + mgc) * 4u;
+  const uint32_t rowB = (uint32_t)L * 4u;
   const uint16_t* yrow = Ybt + (size_t)(ng < Np ? ng : Np - 1) * Tp + 16 * hq;
   float ra[16];
   uint4 rb0, rb1;
-  // row pointers are wave-uniform (tg is): scalar address arithmetic
-#define PMG_SS_LOAD(t0_)                                                          \
-  {                                                                               \
-    const int64_t tl0 = __builtin_amdgcn_readfirstlane((int)((t0_) + 16 * tg - kb)) + kb; \
-    _Pragma("unroll") for (int i = 0; i < 16; ++i) {                              \
-      const int64_t t = tl0 + i;                                                  \
-      const float* prow = P + (t < K ? t : K - 1) * (int64_t)L;                   \
-      const float v = prow[mgc];                                                  \
-      ra[i] = t < ke ? v : 0.f;                                                   \
-    }                                                                             \
-    const int64_t tb = (t0_) < Tp - KB3 ? (t0_) : Tp - KB3;                       \
-    rb0 = *reinterpret_cast<const uint4*>(yrow + tb);                             \
-    rb1 = *reinterpret_cast<const uint4*>(yrow + tb + 8);                         \
+#define PMG_SS_LOAD(t0_)                                                                     \
+  {                                                                                          \
+    const int64_t t0l = (t0_);                                                               \
+    const int64_t nrow = ke - t0l < 0 ? 0 : (ke - t0l > KB3 ? KB3 : ke - t0l);               \
+    const int64_t tbase = t0l < K ? t0l : 0;                                                 \
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(                     \
+        const_cast<float*>(P + tbase * (int64_t)L), (short)0, (int)(nrow * L * 4), 0x00020000); \
+    _Pragma("unroll") for (int i = 0; i < 16; ++i)                                           \
+      ra[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voffA, i * rowB, 0));  \
+    const int64_t tb = t0l < Tp - KB3 ? t0l : Tp - KB3;                                      \
+    rb0 = *reinterpret_cast<const uint4*>(yrow + tb);                                        \
+    rb1 = *reinterpret_cast<const uint4*>(yrow + tb + 8);                                    \
   }
   double tsum = 0.0;                 // t_w partial of column mg (f64)
-#define PMG_SS_STORE(buf)                                                         \
-  {                                                                               \
-    _Pragma("unroll") for (int i = 0; i < 16; ++i) tsum += (double)ra[i];        \
-    _Pragma("unroll") for (int q = 0; q < 2; ++q) {                               \
-      uint32_t hw[4], mw[4], lw[4];                                               \
-      _Pragma("unroll") for (int j = 0; j < 4; ++j) {                             \
-        uint32_t h0, m0, l0, h1, m1, l1;                                          \
-        split3(ra[8 * q + 2 * j], h0, m0, l0);                                    \
-        split3(ra[8 * q + 2 * j + 1], h1, m1, l1);                                \
-        hw[j] = h0 | (h1 << 16);                                                  \
-        mw[j] = m0 | (m1 << 16);                                                  \
-        lw[j] = l0 | (l1 << 16);                                                  \
-      }                                                                           \
-      const int c = 16 * tg + 8 * q;                                              \
-      *reinterpret_cast<uint4*>(&sA[buf][0][m_l][c]) = make_uint4(hw[0], hw[1], hw[2], hw[3]); \
-      *reinterpret_cast<uint4*>(&sA[buf][1][m_l][c]) = make_uint4(mw[0], mw[1], mw[2], mw[3]); \
-      *reinterpret_cast<uint4*>(&sA[buf][2][m_l][c]) = make_uint4(lw[0], lw[1], lw[2], lw[3]); \
-    }                                                                             \
-    *reinterpret_cast<uint4*>(&sB[buf][n_l][16 * hq]) = rb0;                      \
-    *reinterpret_cast<uint4*>(&sB[buf][n_l][16 * hq + 8]) = rb1;                  \
+  // split values 8q .. 8q+7 of the staged rows into buffer buf; t_w in f32 per 8, then f64
+#define PMG_SS_SPLIT(buf, q)                                                              \
+  {                                                                                       \
+    uint32_t hw[4], mw[4], lw[4];                                                         \
+    _Pragma("unroll") for (int j = 0; j < 4; ++j)                                         \
+      split3_pair(ra[8 * (q) + 2 * j], ra[8 * (q) + 2 * j + 1], hw[j], mw[j], lw[j]);    \
+    const float s8 = ((ra[8 * (q)] + ra[8 * (q) + 1]) + (ra[8 * (q) + 2] + ra[8 * (q) + 3])) + \
+                     ((ra[8 * (q) + 4] + ra[8 * (q) + 5]) + (ra[8 * (q) + 6] + ra[8 * (q) + 7])); \
+    tsum += (double)s8;                                                                   \
+    const int c = 16 * tg + 8 * (q);                                                      \
+    *reinterpret_cast<uint4*>(&sA[buf][0][m_l][c]) = make_uint4(hw[0], hw[1], hw[2], hw[3]); \
+    *reinterpret_cast<uint4*>(&sA[buf][1][m_l][c]) = make_uint4(mw[0], mw[1], mw[2], mw[3]); \
+    *reinterpret_cast<uint4*>(&sA[buf][2][m_l][c]) = make_uint4(lw[0], lw[1], lw[2], lw[3]); \
+  }
+#define PMG_SS_STORE_B(buf)                                                               \
+  {                                                                                       \
+    *reinterpret_cast<uint4*>(&sB[buf][n_l][16 * hq]) = rb0;                              \
+    *reinterpret_cast<uint4*>(&sB[buf][n_l][16 * hq + 8]) = rb1;                          \
   }
   double acc64[2][16];
 #pragma unroll
@@ -312,41 +319,39 @@ __global__ void __launch_bounds__(512) k_ptb3(const float* __restrict__ P, int L
   v16f c0 = {0}, c1 = {0};
   const int am = wm * 32 + r;
   const int bn0 = wn * 64 + r, bn1 = bn0 + 32;
-// the empty asm pins the staging registers after the MFMAs, so their loads' waits (and
-// the split arithmetic reading them) are not hoisted in front of the MFMA block
-#define PMG_SS_PIN()                                                                       \
-  _Pragma("unroll") for (int i = 0; i < 16; ++i) asm volatile("" : "+v"(ra[i]));         \
-  asm volatile("" : "+v"(rb0.x), "+v"(rb0.y), "+v"(rb0.z), "+v"(rb0.w));                  \
-  asm volatile("" : "+v"(rb1.x), "+v"(rb1.y), "+v"(rb1.z), "+v"(rb1.w));
-#define PMG_SS_MFMA(buf)                                                                   \
-  _Pragma("unroll") for (int kk = 0; kk < KB3; kk += 16) {                                 \
-    const v8bf b0 = *reinterpret_cast<const v8bf*>(&sB[buf][bn0][kk + 8 * h]);            \
-    const v8bf b1 = *reinterpret_cast<const v8bf*>(&sB[buf][bn1][kk + 8 * h]);            \
+#define PMG_SS_MFMA_K(buf, kk)                                                             \
+  {                                                                                       \
+    const v8bf b0 = *reinterpret_cast<const v8bf*>(&sB[buf][bn0][(kk) + 8 * h]);          \
+    const v8bf b1 = *reinterpret_cast<const v8bf*>(&sB[buf][bn1][(kk) + 8 * h]);          \
     _Pragma("unroll") for (int sp = 0; sp < 3; ++sp) {                                    \
-      const v8bf a = *reinterpret_cast<const v8bf*>(&sA[buf][sp][am][kk + 8 * h]);        \
+      const v8bf a = *reinterpret_cast<const v8bf*>(&sA[buf][sp][am][(kk) + 8 * h]);      \
       c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b0, c0, 0, 0, 0);                   \
       c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b1, c1, 0, 0, 0);                   \
     }                                                                                     \
   }
+// one K-tile: MFMAs on buffer cur, the staged next tile split into buffer nxt between
+// them, then the loads of the tile after that (their latency spans a whole K-tile)
+#define PMG_SS_TILE(cur, nxt, tload)                                                      \
+  PMG_SS_MFMA_K(cur, 0)                                                                   \
+  PMG_SS_SPLIT(nxt, 0)                                                                    \
+  PMG_SS_MFMA_K(cur, 16)                                                                  \
+  PMG_SS_MFMA_K(cur, 32)                                                                  \
+  PMG_SS_SPLIT(nxt, 1)                                                                    \
+  PMG_SS_STORE_B(nxt)                                                                     \
+  PMG_SS_MFMA_K(cur, 48)                                                                  \
+  PMG_SS_LOAD(tload)                                                                      \
+  __syncthreads();
 
-  // pipeline: tile k's MFMAs (buffer k&1) overlap the split/store of tile k+1 (other
-  // buffer, last read before the previous barrier) and the loads of tile k+2.
   if (kb < ke) {
     PMG_SS_LOAD(kb)
-    PMG_SS_STORE(0)
+    PMG_SS_SPLIT(0, 0)
+    PMG_SS_SPLIT(0, 1)
+    PMG_SS_STORE_B(0)
     PMG_SS_LOAD(kb + KB3)
     __syncthreads();
     for (int64_t t0 = kb; t0 < ke; t0 += 2 * KB3) {   // 2 tiles = one kFlush segment
-      PMG_SS_STORE(1)
-      PMG_SS_LOAD(t0 + 2 * KB3)
-      PMG_SS_MFMA(0)
-      PMG_SS_PIN()
-      __syncthreads();
-      PMG_SS_STORE(0)
-      PMG_SS_LOAD(t0 + 3 * KB3)
-      PMG_SS_MFMA(1)
-      PMG_SS_PIN()
-      __syncthreads();
+      PMG_SS_TILE(0, 1, t0 + 2 * KB3)
+      PMG_SS_TILE(1, 0, t0 + 3 * KB3)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         acc64[0][i] += (double)c0[i];
@@ -367,9 +372,10 @@ __global__ void __launch_bounds__(512) k_ptb3(const float* __restrict__ P, int L
   }
   if (nt == 0) twpart[((size_t)ks * 4 + tg) * Mp + mg] = tsum;
 #undef PMG_SS_LOAD
-#undef PMG_SS_STORE
-#undef PMG_SS_MFMA
-#undef PMG_SS_PIN
+#undef PMG_SS_SPLIT
+#undef PMG_SS_STORE_B
+#undef PMG_SS_MFMA_K
+#undef PMG_SS_TILE
 }
 
 __global__ void k_tw_reduce(const double* __restrict__ twpart, int nKS, int Mp, int L,
