@@ -174,29 +174,50 @@ __global__ void __launch_bounds__(512, 4) k_emission_i8(
 #undef PMG_EM_LOAD
 #undef PMG_EM_STORE
 
-  // epilogue: int64 recombination, f64 ll, 32-latent block max, coalesced rows
+  // Epilogue: digit recombination in f64 (Horner over the 5 int32 accumulators; exact
+  // while |ll| < 2^21, every partial an integer below 2^53), f64 ll, the 32-latent block
+  // max, coalesced rows.  Straight-line over the 16 outputs of a lane: every global
+  // access goes through a buffer descriptor bounded by the workgroup's last valid row, and
+  // lanes that must not write (latents past L; all but lane 0 of a block for rblk) aim
+  // past the bound, so the 16 DPP reductions interleave freely (no per-row branches).
   const int nblk = Lp >> 5;
   const int blk = (l0 >> 5) + wl;
   if (blk >= nblk) return;
   const int l = l0 + wl * 32 + r;
   const bool lvalid = l < L;
   const bool lmask = lvalid && ma_latent && ma_latent[l] == 0;
-  const double lsum = lamsum[l];           // l < Lp here
+  const bool over = !lvalid || lmask;                   // ll replaced by a constant
+  const double ov = lvalid ? -1e20 : -INFINITY;
+  const double lsum = lamsum[l];                        // l < Lp here
+  const int64_t nrow64 = T - t0 < ET ? T - t0 : ET;     // >= 1
+  const int nrow = (int)nrow64;
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(delta + t0 * (int64_t)L, (short)0,
+                                                                       nrow * L * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(rblk + t0 * (int64_t)nblk, (short)0,
+                                                                       nrow * nblk * 8, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(gconst + t0), (short)0,
+                                                                       nrow * 8, 0x00020000);
+  const uint32_t kNoWrite = 0x80000000u;                // past any bound above
+  const int trow0 = wt * 32 + 4 * h;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    const int64_t t = t0 + wt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-    long long q = (long long)acc[0][i];
+    const int tr = trow0 + (i & 3) + 8 * (i >> 2);      // row within the workgroup tile
+    double q = (double)acc[kDig - 1][i];
 #pragma unroll
-    for (int d = 1; d < kDig; ++d) q += (long long)acc[d][i] << (8 * d);
-    const double gc = gconst[t < T ? t : T - 1];
-    double v = (double)q * kQInv - lsum - gc;
-    v = lmask ? -1e20 : v;
-    v = lvalid ? v : -INFINITY;
+    for (int d = kDig - 2; d >= 0; --d) q = fma(q, 256.0, (double)acc[d][i]);
+    const uint32_t g0 = __builtin_amdgcn_raw_buffer_load_b32(rg, tr * 8, 0, 0);
+    const uint32_t g1 = __builtin_amdgcn_raw_buffer_load_b32(rg, tr * 8 + 4, 0, 0);
+    const double gc = __hiloint2double((int)g1, (int)g0);
+    double v = q * kQInv - lsum - gc;
+    v = over ? ov : v;
     const double mx = (double)half_max32((float)v);
-    if (t < T) {
-      if (r == 0) rblk[t * nblk + blk] = mx;
-      if (lvalid) delta[t * (int64_t)L + l] = (float)(v - mx);
-    }
+    const float dv = (float)(v - mx);
+    const uint32_t od = lvalid ? (uint32_t)(tr * L + l - l0 + l0) * 4u : kNoWrite;
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dv), rd, od, 0, 0);
+    const uint32_t orb = r == 0 ? (uint32_t)(tr * nblk + blk) * 8u : kNoWrite;
+    const unsigned long long mu = (unsigned long long)__double_as_longlong(mx);
+    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)mu, rr, orb, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(mu >> 32), rr, orb + 4, 0, 0);
   }
 }
 
