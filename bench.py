@@ -345,9 +345,14 @@ def main():
     ap.add_argument("--halo", type=int, default=512, help="time-shard halo (steps)")
     ap.add_argument("--replicated-adam", action="store_true",
                     help="time shards: run the whole Adam loop on every rank instead of one neuron block each")
+    ap.add_argument("--restarts", type=int, default=0,
+                    help="R > 1: R restarts per GPU as one batched fit (engine.RestartBatchEM; SURVEY 8(e), "
+                         "C5 runs 8 per GPU); reports restart-iterations/s beside the one-restart engine")
     args = ap.parse_args()
     if args.shard == "time":
         return bench_timeshard(args)
+    if args.restarts > 1:
+        return bench_restarts(args)
 
     import torch
     import torch.distributed as dist
@@ -475,6 +480,146 @@ def main():
         out["fit_em_api"] = api_fit_wall(y, B, W0, lp0, L)
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(N, T, L, adam_iters)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_restarts(args):
+    """R restarts of one recording per GPU (model_selection_helper.py:53-59; C5 = 64
+    restarts over 8 GPUs = 8 per GPU): one step = one EM iteration of all R restarts as
+    ONE batched fit (stacked-latent emission and suff-stats GEMMs, one scan launch per
+    pass, R Adam loops).  value = R x steps / time (restart-iterations/s, summed over
+    ranks).  The same R restarts run one after another on the single-restart engine
+    are timed beside it (sequential_restart_iters_per_s)."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from poor_man_gplvm_amd.engine import SpikeData, DeviceEM, RestartBatchEM, AdamConfig, ScanConfig, KernelTimer
+    from poor_man_gplvm_amd.gp_kernel import banded_transition
+    cfg = args.config if args.config != "c3" else "c5"
+    N, T, L = CONFIGS[cfg]
+    R = args.restarts
+    y, B, W0, _ = synth(N, T, L, rank=rank)
+    lps = []
+    for r in range(R):                      # restart r of rank k: posterior-init seed 3 + k R + r
+        uu = np.random.default_rng(3 + rank * R + r).random((T, L)) * 0.1
+        lps.append(np.log(uu / uu.sum(1, keepdims=True)).astype(np.float32))
+    lps = np.stack(lps)
+    dev = torch.device("cuda", local)
+    adam = AdamConfig(lr=0.01, maxiter=1000, tol=1e-6, prior_std=1.0)
+    tr = banded_transition(L, 1.0, 0.01, 0.01)
+    sp = SpikeData(y)
+    n_all = args.warmup + args.steps
+    eng = RestartBatchEM(sp, L, B, R, scan=ScanConfig(chunk=args.chunk or None, warmup=args.warm_steps))
+    eng.set_transition(tr)
+    NB = B.shape[1]
+    W = torch.empty((R, NB, N), dtype=torch.float64, device=dev)
+    mu, nu = torch.zeros_like(W), torch.zeros_like(W)
+    cnt = torch.zeros(R, dtype=torch.int64, device=dev)
+    stats = torch.zeros((n_all, R, 4), dtype=torch.float64, device=dev)
+    lh = torch.zeros((n_all, R, adam.maxiter), dtype=torch.float64, device=dev)
+    eh = torch.zeros_like(lh)
+    logz = torch.zeros((n_all, R), dtype=torch.float64, device=dev)
+
+    def fresh():
+        eng.set_log_posterior(lps)
+        W.copy_(torch.as_tensor(np.broadcast_to(W0.astype(np.float64), (R, NB, N)).copy(), device=dev))
+        mu.zero_(); nu.zero_(); cnt.zero_()
+
+    def it(i):
+        eng.m_step(W, mu, nu, cnt, adam, stats[i], lh[i], eh[i])
+        eng.compute_tuning(W)
+        eng.e_step(1.0, logz[i])
+
+    def run(fresh_fn, step_fn):
+        fresh_fn(); step_fn(0); torch.cuda.synchronize()     # code-object pre-warm
+        fresh_fn()
+        for i in range(args.warmup):
+            step_fn(i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for i in range(args.warmup, n_all):
+            step_fn(i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            te = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(te, op=dist.ReduceOp.MAX)
+            el = float(te.item())
+        return el
+    timer = KernelTimer()
+    elapsed = run(fresh, lambda i: it(i))
+    eng.timer = timer
+    fresh()
+    for i in range(min(3, n_all)):
+        it(i)
+    eng.timer = None
+    summ = timer.summary()
+    s = stats.cpu().numpy()
+    adam_iters = float(np.mean(s[args.warmup:, :, 0])) if args.steps else 0.0
+    lz = logz.cpu().numpy()
+    del eng
+    # the same restarts on the one-restart engine, one after another
+    one = DeviceEM(sp, L, basis=B, scan=ScanConfig(warmup=args.warm_steps))
+    one.set_transition(tr)
+    W1 = torch.empty((NB, N), dtype=torch.float64, device=dev)
+    mu1, nu1 = torch.zeros_like(W1), torch.zeros_like(W1)
+    cnt1 = torch.zeros(1, dtype=torch.int64, device=dev)
+    st1 = torch.zeros((n_all, 4), dtype=torch.float64, device=dev)
+    lh1 = torch.zeros((n_all, adam.maxiter), dtype=torch.float64, device=dev)
+    eh1 = torch.zeros_like(lh1)
+    lz1 = torch.zeros(n_all, dtype=torch.float64, device=dev)
+    seq = 0.0
+    n_seq = min(R, 2)                      # time 2 restarts, scale to R
+    for r in range(n_seq):
+        def fresh1(r=r):
+            one.set_log_posterior(lps[r])
+            W1.copy_(torch.as_tensor(W0.astype(np.float64), device=dev))
+            mu1.zero_(); nu1.zero_(); cnt1.zero_()
+
+        def it1(i):
+            one.m_step(W1, mu1, nu1, cnt1, adam, st1[i], lh1[i], eh1[i])
+            one.compute_tuning(W1)
+            one.e_step(1.0, lz1[i:i + 1])
+        seq += run(fresh1, it1)
+    seq_rate = world * n_seq * args.steps / seq
+    value = world * R * args.steps / elapsed
+    out = {
+        "metric": f"restart EM iters/sec at {cfg.upper()} (N={N}, T={T}, L={L}), {R} restarts per GPU",
+        "value": value,
+        "unit": "restart EM iters/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 state / int8-exact emission / f64 stats",
+        "data": "synthetic (spikes sampled from the model; seeds of BASELINE.md section 2)",
+        "config": {"workload": f"{cfg}: {R} restarts x PoissonGPLVMJump1D.fit_em N={N} T={T} L={L} nb={NB} per "
+                               f"GPU as one batched fit; one step = one EM iteration of every restart",
+                   "n_neuron": N, "n_time": T, "n_latent_bin": L, "restarts_per_gpu": R,
+                   "parallelism": f"restarts {R} x {world} GPUs"},
+        "sequential_restart_iters_per_s": seq_rate,
+        "batched_vs_sequential": value / seq_rate,
+        "kernels_ms": {k: round(v[1], 4) for k, v in summ.items()},
+        "kernel_calls": {k: v[0] for k, v in summ.items()},
+        "adam_iters_mean": adam_iters,
+        "chunk": [int(eng_c) for eng_c in (max(32, -(-R * T // 2048)),)],
+        "log_marginal_last": [float(v) for v in lz[n_all - 1]],
+    }
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -68,6 +68,10 @@ int pmg_spikes_prepare(const float* y, int64_t T, int32_t N, const float* ma_neu
 /* tuning64 (L,N) f64 and tuning32 (L,N) f32 (either may be NULL).       */
 int pmg_tuning_softplus(const float* basis, const double* W, int32_t L, int32_t NB, int32_t N,
                         double* tuning64, float* tuning32, void* stream);
+/* R restarts at once: W (R,NB,N) f64 -> tuning rows r*L + l of the stacked */
+/* (R*L, N) outputs (the latents of the batched emission).       */
+int pmg_tuning_softplus_batched(const float* basis, const double* W, int32_t L, int32_t NB, int32_t N, int32_t R,
+                                double* tuning64, float* tuning32, void* stream);
 
 /* ------------------------------------------------------------------ */
 /* Poisson emission  -- decoder.get_loglikelihood_ma_poisson            */
@@ -101,6 +105,11 @@ int pmg_emission_latent_mask(const float* delta0, const double* rblk0, int64_t T
 /* exp(s*ll[t,l] - s*m[t]) = exp(s*delta[t,l] + phi[t,l/32]).                              */
 int pmg_emission_rowref(const double* rblk, int64_t T, int32_t nblk, double likelihood_scale,
                         float* phi, double* m, void* stream);
+/* Batched restarts (R restarts per GPU): rblk holds R restarts'  */
+/* stacked latents, nblk = R * nblk_r; m (T, R) and phi (T, nblk) are taken  */
+/* per restart (each restart's row reference is its own block maximum).      */
+int pmg_emission_rowref_batched(const double* rblk, int64_t T, int32_t nblk, int32_t R, double likelihood_scale,
+                                float* phi, double* m, void* stream);
 /* ll (T,L) f32 = delta + rblk  (the log_likelihood_all output, decoder.py:307). */
 int pmg_loglik_materialize(const float* delta, const double* rblk, int64_t T, int32_t L,
                            float* ll, void* stream);
@@ -234,6 +243,28 @@ size_t pmg_fwdbwd_repair_counter_offset(int64_t T, int32_t L, int32_t chunk);
 #define PMG_STATE_BWD_FIRST 3
 int32_t pmg_fwdbwd_lpad(int32_t L);
 float* pmg_fwdbwd_state(void* workspace, int64_t T, int32_t L, int32_t chunk, int32_t which, int64_t c);
+
+/* Batched restarts (R independent fits of one recording on one GPU,          */
+/* model_selection_helper.py:53-59; SURVEY 8(e): 8 restarts per GPU at C5).    */
+/* The R restarts' latents are stacked side by side: delta (T, R*L),          */
+/* phi (T, R*nblk_r), m (T, R) (pmg_emission_poisson over the (R*L, N) tuning, */
+/* then pmg_emission_rowref_batched), P (T, R*L) (so pmg_suffstats_bf16 over   */
+/* R*L latents gives every restart's y_w / t_w in one GEMM).  Each restart has */
+/* its own sequence outputs alpha (R,T,2,L), logc (R,T), logz (R) and its own  */
+/* workspace slab (workspace_bytes / R, 256-byte aligned; size it with         */
+/* pmg_fwdbwd_batched_workspace_size at the smaller of the two chunks, zero-   */
+/* filled once).  One launch per pass covers every restart (blockIdx.y); the   */
+/* phases are those of the _phase calls; the backward writes P and, if         */
+/* non-NULL, gamma (R,T,2,L).  Requires L % 32 == 0.                           */
+size_t pmg_fwdbwd_batched_workspace_size(int64_t T, int32_t L, int32_t chunk, int32_t R);
+int pmg_forward_filter_batched(const float* delta, const float* phi, const double* m, int64_t T, int32_t R,
+                               const pmg_transition* tr, double likelihood_scale, int32_t chunk,
+                               int32_t warmup, double tol, float* alpha, double* logc, double* logz,
+                               void* workspace, size_t workspace_bytes, void* stream, int32_t phase);
+int pmg_backward_smoother_batched(const float* delta, const float* phi, const float* alpha, int64_t T, int32_t R,
+                                  const pmg_transition* tr, double likelihood_scale, int32_t chunk,
+                                  int32_t warmup, double tol, float* P, float* gamma, void* workspace,
+                                  size_t workspace_bytes, void* stream, int32_t phase);
 
 /* ------------------------------------------------------------------ */
 /* Dense log-domain scans: any continuous kernel (custom_transition_kernel,  */

@@ -43,6 +43,8 @@ EXPORTED_SYMBOLS = (
     "pmg_emission_poisson_dt", "pmg_naive_bayes_normalize",
     "pmg_tuning_linear", "pmg_emission_gaussian", "pmg_gaussian_mstep_workspace_size", "pmg_gaussian_mstep",
     "pmg_dense_workspace_size", "pmg_dense_forward", "pmg_dense_backward", "pmg_joint_log_accumulate",
+    "pmg_tuning_softplus_batched", "pmg_emission_rowref_batched", "pmg_fwdbwd_batched_workspace_size",
+    "pmg_forward_filter_batched", "pmg_backward_smoother_batched",
 )
 
 
@@ -132,6 +134,13 @@ _SIGS = {
                             _P, _P, _P, _P, _P, _P, _SZ, _P], _I32),
     "pmg_joint_log_accumulate": ([_P, _P, _I64, _I32, _P, _P], _I32),
     "pmg_joint_accumulate": ([_P, _P, _I64, _I32, _P, _P, _SZ, _P], _I32),
+    "pmg_tuning_softplus_batched": ([_P, _P, _I32, _I32, _I32, _I32, _P, _P, _P], _I32),
+    "pmg_emission_rowref_batched": ([_P, _I64, _I32, _I32, _D, _P, _P, _P], _I32),
+    "pmg_fwdbwd_batched_workspace_size": ([_I64, _I32, _I32, _I32], _SZ),
+    "pmg_forward_filter_batched": ([_P, _P, _P, _I64, _I32, ctypes.POINTER(Transition), _D, _I32, _I32, _D,
+                                    _P, _P, _P, _P, _SZ, _P, _I32], _I32),
+    "pmg_backward_smoother_batched": ([_P, _P, _P, _I64, _I32, ctypes.POINTER(Transition), _D, _I32, _I32, _D,
+                                       _P, _P, _P, _SZ, _P, _I32], _I32),
 }
 
 _lib = None

@@ -24,7 +24,7 @@ import numpy as np
 import torch
 
 from . import _native as nat
-from .engine import AdamConfig, DeviceEM, ScanConfig, SpikeData, default_device, log_of
+from .engine import AdamConfig, DeviceEM, RestartBatchEM, ScanConfig, SpikeData, default_device, log_of
 from .gp_kernel import (DenseTransition, banded_transition, create_transition_prob_1d, dense_transition,
                         generate_basis, make_transition, transition_from_log_kernels)
 
@@ -600,6 +600,22 @@ def compute_transition_posterior_prob(log_accumulated_joint_total):
     return {k: r[k].astype(np.float32) for k in sorted(r)}
 
 
+def _m_step_res(s, lhn, ehn, n_iter):
+    """m_step_res_l of the fit_em dict (core.py:655-658, histories trimmed to n_iter as
+    core.py:819-826) from the device's per-iteration (n_iter, final_loss, final_error)
+    stats and the padded loss / error histories."""
+    out = {'params': [], 'opt_state': [], 'n_iter': [], 'final_loss': [], 'final_error': [],
+           'loss_history': [], 'error_history': []}
+    for i in range(n_iter):
+        n = int(s[i, 0])
+        out['n_iter'].append(n)
+        out['final_loss'].append(float(s[i, 1]))
+        out['final_error'].append(float(s[i, 2]))
+        out['loss_history'].append(lhn[i, :n].copy())
+        out['error_history'].append(ehn[i, :n].copy())
+    return out
+
+
 def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=None, ma_latent=None,
            likelihood_scale=1.0, save_every=None, adam: AdamConfig | None = None,
            scan: ScanConfig | None = None, opt_state=None, timing=None, noise_std=None):
@@ -663,19 +679,9 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
         if timing is not None:
             torch.cuda.synchronize()
             timing.append(time.perf_counter() - t0)
-    s = _np(stats)
-    lhn, ehn = _np(lh), _np(eh)
     lz = _np(logz)
     saved['log_marginal_saved'] = [float(lz[i]) for i in saved_idx]
-    m_step_res_l = {'params': [], 'opt_state': [], 'n_iter': [], 'final_loss': [], 'final_error': [],
-                    'loss_history': [], 'error_history': []}
-    for i in range(n_iter):
-        n = int(s[i, 0])
-        m_step_res_l['n_iter'].append(n)
-        m_step_res_l['final_loss'].append(float(s[i, 1]))
-        m_step_res_l['final_error'].append(float(s[i, 2]))
-        m_step_res_l['loss_history'].append(lhn[i, :n].copy())
-        m_step_res_l['error_history'].append(ehn[i, :n].copy())
+    m_step_res_l = _m_step_res(_np(stats), _np(lh), _np(eh), n_iter)
     posterior = _np(gamma)
     res = {'log_posterior_all_saved': saved['log_posterior_all_saved'],
            'log_posterior_init': log_posterior_init,
@@ -698,6 +704,177 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
     info = {'opt_state': {'mu': _np(mu), 'nu': _np(nu), 'count': int(_np(cnt)[0])},
             'params64': _np(W), 'repairs': eng.repairs(), 'chunk': eng.C}
     return res, info
+
+
+def run_em_restarts(y, params, basis, log_posterior_inits, n_iter, transition, ma_neuron=None, ma_latent=None,
+                    likelihood_scale=1.0, save_every=None, adam: AdamConfig | None = None,
+                    scan: ScanConfig | None = None, timing=None):
+    """R restarts of the Poisson EM loop (core.py:650-676) batched on one GPU
+    (engine.RestartBatchEM); returns [(fit_em dict, info)] per restart, each the same as
+    run_em would return for that restart alone.  params: (NB, N) shared initial W or
+    (R, NB, N); log_posterior_inits: (R, T, L).  The restart loop this replaces is
+    model_selection_helper.py:53-59 (one fit_em per key)."""
+    adam = adam or AdamConfig()
+    y = np.asarray(y)
+    lpi = np.asarray(log_posterior_inits, np.float32)
+    R, T, L = lpi.shape
+    B = np.asarray(basis, np.float32)
+    if B.shape[0] != L or y.shape[0] != T:
+        raise ValueError("log_posterior_inits must be (R, n_time, n_latent_bin)")
+    if save_every is None:
+        save_every = n_iter
+    ma = None if ma_neuron is None else np.asarray(ma_neuron, np.float32)
+    sp = SpikeData(y, ma)
+    eng = RestartBatchEM(sp, L, B, R, scan=scan)
+    eng.set_transition(transition)
+    eng.set_ma_latent(ma_latent)
+    mlat = None if ma_latent is None else np.asarray(ma_latent).astype(bool)
+    eng.set_log_posterior(lpi)
+    dev = eng.dev
+    W0 = np.asarray(params, np.float64)
+    W = torch.as_tensor(np.ascontiguousarray(np.broadcast_to(W0, (R,) + W0.shape[-2:])), device=dev).contiguous()
+    mu = torch.zeros_like(W)
+    nu = torch.zeros_like(W)
+    cnt = torch.zeros(R, dtype=torch.int64, device=dev)
+    mi = max(int(adam.maxiter), 1)
+    stats = torch.zeros((n_iter, R, 4), dtype=torch.float64, device=dev)
+    lh = torch.zeros((n_iter, R, mi), dtype=torch.float64, device=dev)
+    eh = torch.zeros((n_iter, R, mi), dtype=torch.float64, device=dev)
+    logz = torch.zeros((max(n_iter, 1), R), dtype=torch.float64, device=dev)
+    gamma = torch.empty((R, T, 2, L), dtype=torch.float32, device=dev)
+    saved = [{'log_posterior_all_saved': [], 'params_saved': [], 'tuning_saved': [], 'iter_saved': []}
+             for _ in range(R)]
+    saved_idx = []
+
+    def log_post(r):
+        return _masked_log(_np(log_of(gamma[r])), mlat)
+    import time
+    for i in range(n_iter):
+        t0 = time.perf_counter() if timing is not None else 0.0
+        eng.m_step(W, mu, nu, cnt, adam, stats[i], lh[i], eh[i])
+        eng.compute_tuning(W)
+        want_gamma = (i == n_iter - 1) or (i % save_every == 0)
+        eng.e_step(likelihood_scale, logz[i], gamma=gamma if want_gamma else None)
+        if i % save_every == 0:
+            for r in range(R):
+                saved[r]['log_posterior_all_saved'].append(log_post(r))
+                saved[r]['params_saved'].append(_np(W[r]).astype(np.float32))
+                saved[r]['tuning_saved'].append(_np(eng.tuning32[r * L:(r + 1) * L]))
+                saved[r]['iter_saved'].append(i)
+            saved_idx.append(i)
+        if timing is not None:
+            torch.cuda.synchronize()
+            timing.append(time.perf_counter() - t0)
+    lz = _np(logz)
+    st, lhn, ehn = _np(stats), _np(lh), _np(eh)
+    repairs = eng.repairs()
+    out = []
+    for r in range(R):
+        posterior = _np(gamma[r])
+        res = {'log_posterior_all_saved': saved[r]['log_posterior_all_saved'],
+               'log_posterior_init': lpi[r],
+               'params_saved': saved[r]['params_saved'],
+               'tuning_saved': saved[r]['tuning_saved'],
+               'iter_saved': saved[r]['iter_saved'],
+               'params': _np(W[r]).astype(np.float32),
+               'tuning': _np(eng.tuning32[r * L:(r + 1) * L]),
+               'log_posterior_final': log_post(r),
+               'log_marginal': float(lz[n_iter - 1, r]) if n_iter else float('nan'),
+               'log_marginal_l': [float(v) for v in lz[:n_iter, r]],
+               'log_marginal_saved': [float(lz[i, r]) for i in saved_idx],
+               'posterior': posterior,
+               'posterior_latent_marg': posterior.sum(axis=1),
+               'posterior_dynamics_marg': posterior.sum(axis=2),
+               'm_step_res_l': _m_step_res(st[:, r], lhn[:, r], ehn[:, r], n_iter)}
+        info = {'opt_state': {'mu': _np(mu[r]), 'nu': _np(nu[r]), 'count': int(_np(cnt)[r])},
+                'params64': _np(W[r]), 'repairs': repairs[r], 'chunk': eng.C, 'batched_restarts': R}
+        out.append((res, info))
+    return out
+
+
+def fit_em_restarts(models, y, keys, hyperparam={}, n_iter=20, ma_neuron=None, ma_latent=None,
+                    likelihood_scale=1., save_every=None, m_step_step_size=0.01, m_step_maxiter=1000,
+                    m_step_tol=1e-6, posterior_init_kwargs={'random_scale': 0.1}, **kwargs):
+    """models[r].fit_em(y, hyperparam, key=keys[r], ...) for every r, run as ONE batched
+    fit on the GPU (run_em_restarts) when the models allow it: the same exact class
+    PoissonGPLVMJump1D, identical configuration and initial params, a banded transition
+    and n_latent_bin % 32 == 0.  Otherwise the fits run one after another.  Each model
+    ends in the state its own fit_em would leave (params, tuning, kernels, basis)."""
+    models = list(models)
+    keys = list(keys)
+    if len(models) != len(keys):
+        raise ValueError("one key per model")
+    fit_kw = dict(n_iter=n_iter, ma_neuron=ma_neuron, ma_latent=ma_latent, likelihood_scale=likelihood_scale,
+                  save_every=save_every, m_step_step_size=m_step_step_size, m_step_maxiter=m_step_maxiter,
+                  m_step_tol=m_step_tol, posterior_init_kwargs=posterior_init_kwargs, **kwargs)
+    if len(models) < 2 or not _restarts_batchable(models, hyperparam):
+        return [m.fit_em(y, hyperparam=hyperparam, key=k, **fit_kw) for m, k in zip(models, keys)]
+    m0 = models[0]
+    y_in = y
+    y = np.asarray(y.d if _is_tsd(y) else y)
+    T = y.shape[0]
+    hp = dict(hyperparam)
+    prior_std = hp.get('param_prior_std', m0.param_prior_std)
+    mv = hp.get('movement_variance', m0.movement_variance)
+    pmj = hp.get('p_move_to_jump', m0.p_move_to_jump)
+    pjm = hp.get('p_jump_to_move', m0.p_jump_to_move)
+    ls = hp.get('tuning_lengthscale', m0.tuning_lengthscale)
+    tuning_basis = (generate_basis(ls, m0.n_latent_bin, m0.explained_variance_threshold_basis, include_bias=True)
+                    if 'tuning_lengthscale' in hyperparam else m0.tuning_basis)
+    if ma_neuron is None:
+        ma_neuron = m0.ma_neuron_default
+    if ma_latent is None:
+        ma_latent = m0.ma_latent_default
+    lp_given = kwargs.get('log_posterior_init')
+    if lp_given is not None:   # fit_em(log_posterior_init=...) starts every restart there
+        lpi = np.stack([np.asarray(lp_given, np.float32)] * len(models))
+    else:
+        lpi = np.stack([m.init_latent_posterior(T, k, **posterior_init_kwargs)[0] for m, k in zip(models, keys)])
+    outs = run_em_restarts(y, m0.params, tuning_basis, lpi, n_iter=n_iter,
+                           transition=m0._transition(mv, pmj, pjm), ma_neuron=ma_neuron, ma_latent=ma_latent,
+                           likelihood_scale=likelihood_scale, save_every=save_every,
+                           adam=AdamConfig(lr=m_step_step_size, maxiter=m_step_maxiter, tol=m_step_tol,
+                                           prior_std=prior_std), scan=m0.scan_config)
+    _, lk, _, la = create_transition_prob_1d(m0.n_latent_bin, mv, pmj, pjm, m0.custom_transition_kernel)
+    results = []
+    for m, (res, info) in zip(models, outs):
+        m.tuning_lengthscale, m.movement_variance, m.p_move_to_jump, m.p_jump_to_move = ls, mv, pmj, pjm
+        m._m_step_step_size, m._m_step_maxiter, m._m_step_tol = m_step_step_size, m_step_maxiter, m_step_tol
+        m.params = res['params']
+        m.tuning = res['tuning']
+        m.fit_info = info
+        m.log_marginal_final = res['log_marginal']
+        m.log_latent_transition_kernel_l = lk
+        m.log_dynamics_transition_kernel = la
+        m.tuning_basis = tuning_basis
+        if _is_tsd(y_in):
+            res['posterior_latent_marg'] = nap.TsdFrame(d=res['posterior_latent_marg'], t=y_in.t)
+            res['posterior_dynamics_marg'] = nap.TsdFrame(d=res['posterior_dynamics_marg'], t=y_in.t)
+        results.append(res)
+    return results
+
+
+def _restarts_batchable(models, hyperparam):
+    """run_em_restarts holds these fits: exact PoissonGPLVMJump1D models with identical
+    configuration and initial params, a banded transition and n_latent_bin % 32 == 0."""
+    m0 = models[0]
+    if any(type(m) is not PoissonGPLVMJump1D for m in models):
+        return False
+    if m0.n_latent_bin % 32 or m0.custom_transition_kernel is not None:
+        return False
+    keys = ('n_neuron', 'n_latent_bin', 'tuning_lengthscale', 'param_prior_std', 'movement_variance',
+            'p_move_to_jump', 'p_jump_to_move', 'smoothness_penalty')
+    for m in models[1:]:
+        if any(np.any(np.asarray(getattr(m, k, None)) != np.asarray(getattr(m0, k, None))) for k in keys):
+            return False
+        if not np.array_equal(np.asarray(m.params), np.asarray(m0.params)):
+            return False
+        if not np.array_equal(np.asarray(m.tuning_basis), np.asarray(m0.tuning_basis)):
+            return False
+    mv = hyperparam.get('movement_variance', m0.movement_variance)
+    pmj = hyperparam.get('p_move_to_jump', m0.p_move_to_jump)
+    pjm = hyperparam.get('p_jump_to_move', m0.p_jump_to_move)
+    return not isinstance(m0._transition(mv, pmj, pjm), DenseTransition)
 
 
 class GaussianGPLVMJump1D(PoissonGPLVMJump1D):

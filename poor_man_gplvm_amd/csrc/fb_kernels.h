@@ -35,6 +35,8 @@
 #pragma once
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "pmg_common.h"
 
 // Contract a*b+c only inside one expression (the explicit fmaf calls).  Chunk
@@ -118,7 +120,39 @@ struct FBParams {
   int* seg_chg;    // [2][S]
   int G, S;
   int Lpad;  // 64*J
+  // row strides: delta and P (floats; L, or R L when R restarts' latents are stacked
+  // side by side), phi (nblk or R nblk), m (1 or R)
+  int ldd, ldphi, ldm;
+  // batched restarts (blockIdx.y = restart r): per-restart offsets of the stacked inputs
+  // (delta / P: r L floats, phi: r nblk, m: r), of the sequence outputs (alpha / gamma:
+  // r T 2L, logc: r T, logz: r) and of the restart's own workspace slab (r ws_stride bytes)
+  int64_t ws_stride;
 };
+
+// this restart's view of the parameters (identity for blockIdx.y = 0)
+__device__ __forceinline__ FBParams batch_view(const FBParams& p0) {
+  FBParams p = p0;
+  const int r = blockIdx.y;
+  if (r == 0) return p;
+  const int64_t seq = (int64_t)r * p.T;
+  p.delta += (int64_t)r * p.L;
+  if (p.P) p.P += (int64_t)r * p.L;
+  p.phi += (int64_t)r * p.nblk;
+  p.m += r;
+  if (p.alpha) p.alpha += seq * 2 * p.L;
+  if (p.alpha_in) p.alpha_in += seq * 2 * p.L;
+  if (p.gamma) p.gamma += seq * 2 * p.L;
+  if (p.logc) p.logc += seq;
+  if (p.logz) p.logz += r;
+  const int64_t o = (int64_t)r * p.ws_stride;
+  auto mv = [o](auto*& q) {
+    typedef std::remove_reference_t<decltype(q)> ptr_t;
+    if (q) q = reinterpret_cast<ptr_t>(reinterpret_cast<uintptr_t>(q) + (uintptr_t)o);
+  };
+  mv(p.jsc); mv(p.chunk_logz); mv(p.s_in); mv(p.s_out); mv(p.w_first); mv(p.b_in); mv(p.b_first);
+  mv(p.flags); mv(p.ctl); mv(p.seg_end); mv(p.seg_chg);
+  return p;
+}
 
 // ---------------------------------------------------------------------------
 // per-lane helpers (lane owns latents j0 .. j0+J-1, j0 = lane*J)
@@ -146,9 +180,9 @@ struct EmRaw {
 
 template <int J>
 __device__ __forceinline__ void em_load(const FBParams& p, int64_t t, int j0, EmRaw<J>& r) {
-  load_row<J>(p.delta + t * p.L, p.L, j0, r.d);
+  load_row<J>(p.delta + t * p.ldd, p.L, j0, r.d);
   const int b = j0 >> 5;
-  r.ph = (b < p.nblk) ? p.phi[t * p.nblk + b] : 0.f;
+  r.ph = (b < p.nblk) ? p.phi[t * p.ldphi + b] : 0.f;
 }
 
 template <int J>
@@ -486,8 +520,8 @@ __device__ __forceinline__ void bstore_f64_lane0(double* base, int64_t t, double
 
 template <int J, bool VEC>
 __device__ __forceinline__ void bem_load(const FBParams& p, int64_t t, int j0, EmRaw<J>& r) {
-  bload_row<J, VEC>(p.delta + t * p.L, p.L, j0, r.d);
-  const __amdgpu_buffer_rsrc_t rs = rsrc_of(p.phi + t * p.nblk, (uint32_t)p.nblk * 4u);
+  bload_row<J, VEC>(p.delta + t * p.ldd, p.L, j0, r.d);
+  const __amdgpu_buffer_rsrc_t rs = rsrc_of(p.phi + t * p.ldphi, (uint32_t)p.nblk * 4u);
   r.ph = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (j0 >> 5) * 4, 0, 0));
 }
 
@@ -504,7 +538,7 @@ __device__ __forceinline__ double fwd_stream(const FBParams& p, Fwd<J, WP>& st, 
   for (int q = 0; q < PF; ++q) {
     const int64_t tl = t_a + q < last ? t_a + q : last;
     bem_load<J, VEC>(p, tl, j0, ring[q]);
-    if constexpr (OUT) mr[q] = p.m[tl];
+    if constexpr (OUT) mr[q] = p.m[tl * p.ldm];
   }
   auto body = [&](int q, int64_t t, bool refill) {
     float e[J];
@@ -514,7 +548,7 @@ __device__ __forceinline__ double fwd_stream(const FBParams& p, Fwd<J, WP>& st, 
     if (refill) {
       const int64_t tl = t + PF < last ? t + PF : last;
       bem_load<J, VEC>(p, tl, j0, ring[q]);
-      if constexpr (OUT) mr[q] = p.m[tl];
+      if constexpr (OUT) mr[q] = p.m[tl * p.ldm];
     }
     const float S = st.step(p, j0, invz, e);
     if constexpr (OUT) {
@@ -571,7 +605,8 @@ __device__ __forceinline__ void main_pass_reset(const FBParams& p) {
 }
 
 template <int J, int WP>
-__global__ void __launch_bounds__(64) k_forward(FBParams p) {
+__global__ void __launch_bounds__(64) k_forward(FBParams p_arg) {
+  const FBParams p = batch_view(p_arg);
   const int c = blockIdx.x;
   if (c >= p.M) return;
   main_pass_reset(p);
@@ -708,10 +743,10 @@ __device__ __forceinline__ void forward_relax(const FBParams& p, int j0, const f
   const size_t SZ = (size_t)2 * p.Lpad;
   const int s = blockIdx.x;
   const int lane = threadIdx.x & 63;
+  const int a = s * p.G;
+  const int b = a + p.G < p.M ? a + p.G : p.M;
   int nrep = 0, rounds = 0;
   if (ctl_load(p.ctl, kCtlPending) > 0) {
-    const int a = s * p.G;
-    const int b = a + p.G < p.M ? a + p.G : p.M;
     Fwd<J, WP> st;
     bool changed = false;
     // round 0: every boundary the verification flagged (it stored the carry into s_in),
@@ -754,7 +789,8 @@ __device__ __forceinline__ void forward_relax(const FBParams& p, int j0, const f
 }
 
 template <int J, int WP>
-__global__ void __launch_bounds__(64) k_forward_relax(FBParams p) {
+__global__ void __launch_bounds__(64) k_forward_relax(FBParams p_arg) {
+  const FBParams p = batch_view(p_arg);
   PMG_FB_LANE_SETUP
   (void)lane;
   if constexpr (J % 4 == 0) {
@@ -949,9 +985,9 @@ __device__ __forceinline__ void bwd_stream_out(const FBParams& p, Bwd<J, WP>& st
       pp[j] = a0[j] + a1[j];
     }
     if constexpr (MODE == 0) {
-      bstore_row<J, VEC>(p.P + t * L, p.L, j0, pp);
+      bstore_row<J, VEC>(p.P + t * p.ldd, p.L, j0, pp);
     } else {
-      if (p.P) bstore_row<J, VEC>(p.P + t * L, p.L, j0, pp);
+      if (p.P) bstore_row<J, VEC>(p.P + t * p.ldd, p.L, j0, pp);
       if (p.gamma) {
         bstore_row<J, VEC>(p.gamma + t * 2 * L, p.L, j0, a0);
         bstore_row<J, VEC>(p.gamma + t * 2 * L + L, p.L, j0, a1);
@@ -1018,7 +1054,8 @@ __device__ __forceinline__ void backward_chunk(const FBParams& p, int c, int j0,
 
 // speculative pass, EM outputs (P only)
 template <int J, int WP>
-__global__ void __launch_bounds__(64) k_backward(FBParams p) {
+__global__ void __launch_bounds__(64) k_backward(FBParams p_arg) {
+  const FBParams p = batch_view(p_arg);
   const int c = blockIdx.x;
   if (c >= p.M) return;
   main_pass_reset(p);
@@ -1029,7 +1066,8 @@ __global__ void __launch_bounds__(64) k_backward(FBParams p) {
 
 // speculative pass, decode outputs (P / gamma / rho as given)
 template <int J, int WP>
-__global__ void __launch_bounds__(64) k_backward_full(FBParams p) {
+__global__ void __launch_bounds__(64) k_backward_full(FBParams p_arg) {
+  const FBParams p = batch_view(p_arg);
   const int c = blockIdx.x;
   if (c >= p.M) return;
   main_pass_reset(p);
@@ -1075,11 +1113,11 @@ __device__ __forceinline__ void backward_relax(const FBParams& p, int j0, const 
   const size_t SZ = (size_t)2 * p.Lpad;
   const int s = blockIdx.x;
   const int lane = threadIdx.x & 63;
+  const int a = s * p.G;
+  const int b = a + p.G < p.M ? a + p.G : p.M;
+  const int top = b < p.M - 1 ? b : p.M - 1;  // boundaries c <= M-2 have a successor
   int nrep = 0, rounds = 0;
   if (ctl_load(p.ctl, kCtlPending) > 0) {
-    const int a = s * p.G;
-    const int b = a + p.G < p.M ? a + p.G : p.M;
-    const int top = b < p.M - 1 ? b : p.M - 1;  // boundaries c <= M-2 have a successor
     Bwd<J, WP> st;
     bool changed = false;
     // round 0: every flagged boundary, top down (see forward_relax)
@@ -1117,7 +1155,8 @@ __device__ __forceinline__ void backward_relax(const FBParams& p, int j0, const 
 }
 
 template <int J, int WP>
-__global__ void __launch_bounds__(64) k_backward_relax(FBParams p) {
+__global__ void __launch_bounds__(64) k_backward_relax(FBParams p_arg) {
+  const FBParams p = batch_view(p_arg);
   PMG_FB_LANE_SETUP
   (void)lane;
   if constexpr (J % 4 == 0) {

@@ -14,10 +14,20 @@ namespace pmg {
 // reaches gamma_t(i), t < t_e, only through the joint P(x_t = i, x_{t_e} = j) <=
 // gamma_{t_e}(j), so components with negligible posterior cannot move any output
 // above ~1e-18 probability, while they are exactly the ones the chain forgets slowly.
+// Batched restarts: blockIdx.y = restart, whose operands (all in its workspace slab) sit
+// ws_stride bytes further per restart.
 __global__ void __launch_bounds__(256) k_verify(float* __restrict__ x, const float* __restrict__ y,
                                                 int first, int last, int off, int SZ, float tol,
                                                 int* __restrict__ flags, const float* __restrict__ w,
-                                                int Lpad, int* __restrict__ pending) {
+                                                int Lpad, int* __restrict__ pending, int64_t ws_stride) {
+  if (blockIdx.y) {
+    const uintptr_t o = (uintptr_t)blockIdx.y * (uintptr_t)ws_stride;
+    x = reinterpret_cast<float*>(reinterpret_cast<uintptr_t>(x) + o);
+    y = reinterpret_cast<const float*>(reinterpret_cast<uintptr_t>(y) + o);
+    flags = reinterpret_cast<int*>(reinterpret_cast<uintptr_t>(flags) + o);
+    if (w) w = reinterpret_cast<const float*>(reinterpret_cast<uintptr_t>(w) + o);
+    pending = reinterpret_cast<int*>(reinterpret_cast<uintptr_t>(pending) + o);
+  }
   // wave-uniform (readfirstlane): the state pointers below feed scalar buffer descriptors
   const int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   const int c = first + wv;
@@ -96,6 +106,10 @@ static void relax_shape(FBParams& p) {
   p.S = (p.M + p.G - 1) / p.G;
 }
 
+// PMG_DEBUG_NO_REPAIR (diagnostics): k_verify flags the boundaries into a dummy
+// pending word, so the relaxation kernel repairs nothing (it only sums logZ).
+static bool debug_no_repair() { return getenv("PMG_DEBUG_NO_REPAIR") != nullptr; }
+
 static int pick_J(int L) {
   if (L <= 64) return 1;
   if (L <= 128) return 2;
@@ -153,7 +167,34 @@ static int fill_params(FBParams& p, const pmg_transition* tr, int64_t T, int C, 
   p.M = (int)((T + C - 1) / C);
   p.tol = (float)tol;
   p.Lpad = 64 * J;
+  p.ldd = p.L;
+  p.ldphi = p.nblk;
+  p.ldm = 1;
+  p.ws_stride = 0;
   for (int k = 0; k <= kMaxBand; ++k) p.g[k] = (k <= tr->band) ? tr->g[k] : 0.f;
+  return PMG_OK;
+}
+
+// R > 1: R restarts' latents stacked side by side in delta / phi / m (and P), each
+// restart its own alpha / logc sequence and its own workspace slab of
+// (workspace_bytes / R) rounded down to 256 bytes; blockIdx.y selects the restart.
+// The relaxation runs <= #CUs / R segments per restart, so all R S waves stay resident.
+static int batch_params(FBParams& p, int R, int64_t T, int chunk, size_t workspace_bytes, size_t* slab) {
+  PMG_REQUIRE(R >= 1 && R <= 65535, "pmg scans: R=%d restarts", R);
+  *slab = R == 1 ? workspace_bytes : (workspace_bytes / (size_t)R) & ~(size_t)255;
+  PMG_REQUIRE(*slab >= pmg_fwdbwd_workspace_size(T, p.L, chunk), "pmg scans: workspace too small (%zu per restart)",
+              *slab);
+  if (R == 1) return PMG_OK;
+  PMG_REQUIRE(p.L % 32 == 0, "pmg scans: batched restarts need L %% 32 == 0 (L=%d)", p.L);
+  p.ldd = R * p.L;
+  p.ldphi = R * p.nblk;
+  p.ldm = R;
+  p.ws_stride = (int64_t)*slab;
+  int S = device_cus() / R;
+  if (S < 1) S = 1;
+  if (S > p.S) S = p.S;
+  p.G = (p.M + S - 1) / S;
+  p.S = (p.M + p.G - 1) / p.G;
   return PMG_OK;
 }
 
@@ -203,7 +244,7 @@ float* pmg_fwdbwd_state(void* workspace, int64_t T, int32_t L, int32_t chunk, in
 static int forward_impl(const float* delta, const float* phi, const double* m, int64_t T,
                         const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                         int32_t warmup, double tol, float* alpha, double* logc, double* logz,
-                        void* workspace, size_t workspace_bytes, void* stream, int phase) {
+                        void* workspace, size_t workspace_bytes, void* stream, int phase, int R = 1) {
   FBParams p;
   int rc = fill_params(p, tr, T, chunk, warmup, likelihood_scale, tol);
   if (rc) return rc;
@@ -228,24 +269,27 @@ static int forward_impl(const float* delta, const float* phi, const double* m, i
   p.seg_end = w.seg_end;
   p.seg_chg = w.seg_chg;
   relax_shape(p);
+  size_t slab = 0;
+  rc = batch_params(p, R, T, chunk, workspace_bytes, &slab);
+  if (rc) return rc;
   const int J = p.Lpad / 64, WP = pick_WP(tr->band);
   FBKernelSet ks;
   const bool have = fb_set(J, WP, &ks);
   PMG_REQUIRE(have && ks.forward && ks.forward_relax, "pmg_forward_filter: no kernel for J=%d WP=%d", J, WP);
   if (phase & 1) {
-    hipLaunchKernelGGL(ks.forward, dim3(p.M), dim3(64), 0, st, p);
+    hipLaunchKernelGGL(ks.forward, dim3(p.M, R), dim3(64), 0, st, p);
     PMG_LAUNCH_CHECK();
   }
   if (phase & 2) {
     if (p.M > 1) {
-      // PMG_DEBUG_NO_REPAIR (diagnostics): verify only, count nothing, repair nothing
-      int* pend = getenv("PMG_DEBUG_NO_REPAIR") ? p.ctl + kCtlStride - 1 : p.ctl + kCtlPending;
+      int* pend = debug_no_repair() ? p.ctl + kCtlStride - 1 : p.ctl + kCtlPending;
       const int nver = p.M - 1;
-      hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4), dim3(256), 0, st, w.s_in, (const float*)w.s_out, 1,
-                         p.M - 1, -1, 2 * p.Lpad, p.tol, w.flags, (const float*)nullptr, p.Lpad, pend);
+      hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4, R), dim3(256), 0, st, w.s_in, (const float*)w.s_out, 1,
+                         p.M - 1, -1, 2 * p.Lpad, p.tol, w.flags, (const float*)nullptr, p.Lpad, pend,
+                         p.ws_stride);
       PMG_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(ks.forward_relax, dim3(p.S), dim3(64), 0, st, p);  // also sums logZ
+    hipLaunchKernelGGL(ks.forward_relax, dim3(p.S, R), dim3(64), 0, st, p);  // also sums logZ
     PMG_LAUNCH_CHECK();
   }
   return PMG_OK;
@@ -271,13 +315,14 @@ int pmg_forward_filter_phase(const float* delta, const float* phi, const double*
 static int backward_impl(const float* delta, const float* phi, const float* alpha, int64_t T,
                          const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                          int32_t warmup, double tol, float* P, float* gamma, float* rho,
-                         void* workspace, size_t workspace_bytes, void* stream, int phase) {
+                         void* workspace, size_t workspace_bytes, void* stream, int phase, int R = 1) {
   FBParams p;
   int rc = fill_params(p, tr, T, chunk, warmup, likelihood_scale, tol);
   if (rc) return rc;
   PMG_REQUIRE(delta && phi && alpha && workspace, "pmg_backward_smoother: null");
   PMG_REQUIRE(workspace_bytes >= pmg_fwdbwd_workspace_size(T, tr->L, chunk),
               "pmg_backward_smoother: workspace too small");
+  PMG_REQUIRE(R == 1 || (P && !rho), "pmg_backward_smoother: batched restarts write P (and gamma), not rho");
   hipStream_t st = as_stream(stream);
   FBWork w = carve_fb(workspace, T, p.Lpad, chunk);
   p.delta = delta;
@@ -295,22 +340,25 @@ static int backward_impl(const float* delta, const float* phi, const float* alph
   p.seg_end = w.seg_end;
   p.seg_chg = w.seg_chg;
   relax_shape(p);
+  size_t slab = 0;
+  rc = batch_params(p, R, T, chunk, workspace_bytes, &slab);
+  if (rc) return rc;
   const int J = p.Lpad / 64, WP = pick_WP(tr->band);
   FBKernelSet ks;
   const bool have = fb_set(J, WP, &ks);
   fb_kernel_t kb = !have ? nullptr : (rho || gamma || !P) ? ks.backward_full : ks.backward;
   PMG_REQUIRE(kb && ks.backward_relax, "pmg_backward_smoother: no kernel for J=%d WP=%d", J, WP);
   if (phase & 1) {
-    hipLaunchKernelGGL(kb, dim3(p.M), dim3(64), 0, st, p);
+    hipLaunchKernelGGL(kb, dim3(p.M, R), dim3(64), 0, st, p);
     PMG_LAUNCH_CHECK();
   }
   if ((phase & 2) && p.M > 1) {
-    int* pend = getenv("PMG_DEBUG_NO_REPAIR") ? p.ctl + kCtlStride - 1 : p.ctl + kCtlPending;
+    int* pend = debug_no_repair() ? p.ctl + kCtlStride - 1 : p.ctl + kCtlPending;
     const int nver = p.M - 1;
-    hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4), dim3(256), 0, st, w.b_in, (const float*)w.b_first, 0,
-                       p.M - 2, 1, 2 * p.Lpad, p.tol, w.flags, (const float*)w.w_first, p.Lpad, pend);
+    hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4, R), dim3(256), 0, st, w.b_in, (const float*)w.b_first, 0,
+                       p.M - 2, 1, 2 * p.Lpad, p.tol, w.flags, (const float*)w.w_first, p.Lpad, pend, p.ws_stride);
     PMG_LAUNCH_CHECK();
-    hipLaunchKernelGGL(ks.backward_relax, dim3(p.S), dim3(64), 0, st, p);
+    hipLaunchKernelGGL(ks.backward_relax, dim3(p.S, R), dim3(64), 0, st, p);
     PMG_LAUNCH_CHECK();
   }
   return PMG_OK;
@@ -331,6 +379,30 @@ int pmg_backward_smoother_phase(const float* delta, const float* phi, const floa
   PMG_REQUIRE(phase >= 1 && phase <= 3, "pmg_backward_smoother_phase: phase %d", phase);
   return backward_impl(delta, phi, alpha, T, tr, likelihood_scale, chunk, warmup, tol, P, gamma, rho,
                        workspace, workspace_bytes, stream, phase);
+}
+
+size_t pmg_fwdbwd_batched_workspace_size(int64_t T, int32_t L, int32_t chunk, int32_t R) {
+  const size_t one = pmg_fwdbwd_workspace_size(T, L, chunk);
+  if (one == 0 || R < 1) return 0;
+  return R == 1 ? one : (size_t)R * ((one + 255) & ~(size_t)255);
+}
+
+int pmg_forward_filter_batched(const float* delta, const float* phi, const double* m, int64_t T, int32_t R,
+                               const pmg_transition* tr, double likelihood_scale, int32_t chunk,
+                               int32_t warmup, double tol, float* alpha, double* logc, double* logz,
+                               void* workspace, size_t workspace_bytes, void* stream, int32_t phase) {
+  PMG_REQUIRE((phase & 3) != 0 && (phase & ~7) == 0, "pmg_forward_filter_batched: phase %d", phase);
+  return forward_impl(delta, phi, m, T, tr, likelihood_scale, chunk, warmup, tol, alpha, logc, logz,
+                      workspace, workspace_bytes, stream, phase, R);
+}
+
+int pmg_backward_smoother_batched(const float* delta, const float* phi, const float* alpha, int64_t T, int32_t R,
+                                  const pmg_transition* tr, double likelihood_scale, int32_t chunk,
+                                  int32_t warmup, double tol, float* P, float* gamma, void* workspace,
+                                  size_t workspace_bytes, void* stream, int32_t phase) {
+  PMG_REQUIRE(phase >= 1 && phase <= 3, "pmg_backward_smoother_batched: phase %d", phase);
+  return backward_impl(delta, phi, alpha, T, tr, likelihood_scale, chunk, warmup, tol, P, gamma, nullptr,
+                       workspace, workspace_bytes, stream, phase, R);
 }
 
 }  // extern "C"

@@ -64,27 +64,38 @@ __global__ void __launch_bounds__(256) k_spikes_prepare(
 __global__ void k_tuning_softplus(const float* __restrict__ basis, const double* __restrict__ W,
                                   int L, int NB, int N, double* __restrict__ t64,
                                   float* __restrict__ t32) {
+  // blockIdx.z = restart r of a batched fit: W (R, NB, N) -> rows r L + l of the stacked
+  // (R L, N) tuning
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   const int l = blockIdx.y;
   if (n >= N) return;
+  const int64_t r = blockIdx.z;
+  W += r * NB * (int64_t)N;
+  const int64_t row = r * L + l;
   const float* br = basis + (int64_t)l * NB;
   double acc = 0.0;
   for (int k = 0; k < NB; ++k) acc = fma((double)br[k], W[(int64_t)k * N + n], acc);
   double f = softplus_d(acc);
-  if (t64) t64[(int64_t)l * N + n] = f;
-  if (t32) t32[(int64_t)l * N + n] = (float)f;
+  if (t64) t64[row * N + n] = f;
+  if (t32) t32[row * N + n] = (float)f;
 }
 
-__global__ void k_rowref(const double* __restrict__ rblk, int64_t T, int nblk, double s,
+// one thread per (t, group): R groups of nb = nblk / R blocks each (batched restarts'
+// stacked latents; R = 1: the whole row), m (T, R), phi (T, nblk)
+__global__ void k_rowref(const double* __restrict__ rblk, int64_t T, int nblk, int R, double s,
                          float* __restrict__ phi, double* __restrict__ m) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= T) return;
-  const double* r = rblk + t * nblk;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= T * R) return;
+  const int nb = nblk / R;
+  const int64_t t = i / R;
+  const int g = (int)(i - t * R);
+  const double* r = rblk + t * nblk + (int64_t)g * nb;
   double mx = -INFINITY;
-  for (int b = 0; b < nblk; ++b) mx = fmax(mx, r[b]);
+  for (int b = 0; b < nb; ++b) mx = fmax(mx, r[b]);
   if (mx == -INFINITY) mx = 0.0;  // cannot happen for L >= 1 (masked latents are -1e20)
-  m[t] = mx;
-  for (int b = 0; b < nblk; ++b) phi[t * nblk + b] = (float)(s * (r[b] - mx));
+  m[i] = mx;
+  float* ph = phi + t * nblk + (int64_t)g * nb;
+  for (int b = 0; b < nb; ++b) ph[b] = (float)(s * (r[b] - mx));
 }
 
 __global__ void k_loglik(const float* __restrict__ delta, const double* __restrict__ rblk,
@@ -153,8 +164,13 @@ int pmg_spikes_prepare(const float* y, int64_t T, int32_t N, const float* ma_neu
 
 int pmg_tuning_softplus(const float* basis, const double* W, int32_t L, int32_t NB, int32_t N,
                         double* tuning64, float* tuning32, void* stream) {
-  PMG_REQUIRE(L > 0 && NB > 0 && N > 0 && basis && W, "pmg_tuning_softplus: bad args");
-  dim3 grid((N + 127) / 128, L);
+  return pmg_tuning_softplus_batched(basis, W, L, NB, N, 1, tuning64, tuning32, stream);
+}
+
+int pmg_tuning_softplus_batched(const float* basis, const double* W, int32_t L, int32_t NB, int32_t N, int32_t R,
+                                double* tuning64, float* tuning32, void* stream) {
+  PMG_REQUIRE(L > 0 && NB > 0 && N > 0 && R > 0 && R <= 65535 && basis && W, "pmg_tuning_softplus: bad args");
+  dim3 grid((N + 127) / 128, L, R);
   hipLaunchKernelGGL(k_tuning_softplus, grid, dim3(128), 0, as_stream(stream), basis, W, L, NB,
                      N, tuning64, tuning32);
   PMG_LAUNCH_CHECK();
@@ -165,7 +181,17 @@ int pmg_emission_rowref(const double* rblk, int64_t T, int32_t nblk, double like
                         float* phi, double* m, void* stream) {
   PMG_REQUIRE(T > 0 && nblk > 0 && rblk && phi && m, "pmg_emission_rowref: bad args");
   hipLaunchKernelGGL(k_rowref, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
-                     as_stream(stream), rblk, T, nblk, likelihood_scale, phi, m);
+                     as_stream(stream), rblk, T, nblk, 1, likelihood_scale, phi, m);
+  PMG_LAUNCH_CHECK();
+  return PMG_OK;
+}
+
+int pmg_emission_rowref_batched(const double* rblk, int64_t T, int32_t nblk, int32_t R, double likelihood_scale,
+                                float* phi, double* m, void* stream) {
+  PMG_REQUIRE(T > 0 && nblk > 0 && R > 0 && nblk % R == 0 && rblk && phi && m,
+              "pmg_emission_rowref_batched: bad args (nblk=%d, R=%d)", nblk, R);
+  hipLaunchKernelGGL(k_rowref, dim3((unsigned)((T * R + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), rblk, T, nblk, R, likelihood_scale, phi, m);
   PMG_LAUNCH_CHECK();
   return PMG_OK;
 }

@@ -623,3 +623,201 @@ def log_of(x: torch.Tensor) -> torch.Tensor:
     out = torch.empty_like(x)
     nat.check(nat.load().pmg_log(nat.ptr(x), x.numel(), nat.ptr(out), nat.stream_handle()), "pmg_log")
     return out
+
+
+class RestartBatchEM:
+    """R independent EM restarts of one recording on one GPU (model_selection_helper.py:53-59:
+    the restarts differ only in their posterior init; SURVEY 8(e): 8 restarts per GPU at C5).
+
+    The restarts' latents are stacked side by side, so the dense stages run once for all
+    of them:
+      * tuning: pmg_tuning_softplus_batched, W (R, NB, N) -> the (R L, N) tuning;
+      * emission: ONE int8-MFMA contraction of y (T, N) against R L latents -> delta
+        (T, R L), then pmg_emission_rowref_batched (each restart its own row reference);
+      * scans: pmg_forward_filter_batched / pmg_backward_smoother_batched, one launch per
+        pass with blockIdx.y = restart (each restart its own alpha (T, 2, L), logc, logZ
+        and workspace slab), writing P (T, R L);
+      * sufficient statistics: ONE bf16-MFMA GEMM over the R L latents -> y_w (R L, N),
+        t_w (R L), whose row blocks are the restarts' statistics;
+      * Adam: the persistent loop once per restart on its (L, N) slab (each restart keeps
+        its own stop rule, as R separate fits would).
+    Chunks are sized so the R restarts together run ~2048 chains (R x longer chunks than
+    one restart alone: the warm-up is amortised over R x more output steps).
+    Banded transitions only; L % 32 == 0; Poisson observation model."""
+
+    def __init__(self, spikes: SpikeData, L: int, basis, R: int, scan: ScanConfig | None = None):
+        self.lib = nat.load()
+        self.sp = spikes
+        self.dev = spikes.device
+        self.R = int(R)
+        self.T, self.N, self.L = spikes.T, spikes.N, int(L)
+        if self.R < 1:
+            raise ValueError("R >= 1 restarts")
+        if self.L % 32:
+            raise nat.NativeError(f"batched restarts need n_latent_bin % 32 == 0 (got {self.L})")
+        self.scan = scan or ScanConfig()
+        T, L, N, R, dev = self.T, self.L, self.N, self.R, self.dev
+        RT = R * T
+        self.C = self.scan.chunk if self.scan.chunk else max(32, int(math.ceil(RT / 2048)))
+        self.Cb = self.scan.chunk_bwd or (self.scan.chunk if self.scan.chunk else 2 * self.C)
+        b = np.ascontiguousarray(basis, dtype=np.float32)
+        if b.shape[0] != L:
+            raise ValueError("basis must have n_latent_bin rows")
+        self.NB = int(b.shape[1])
+        self.basis = torch.as_tensor(b, device=dev)
+        LA = R * L
+        self.nblk = L // 32
+        f32, f64 = torch.float32, torch.float64
+        self.delta = torch.empty((T, LA), dtype=f32, device=dev)
+        self.rblk = torch.empty((T, R * self.nblk), dtype=f64, device=dev)
+        self.phi = torch.empty((T, R * self.nblk), dtype=f32, device=dev)
+        self.mref = torch.empty((T, R), dtype=f64, device=dev)
+        self.alpha = torch.empty((R, T, 2, L), dtype=f32, device=dev)
+        self.logc = torch.empty((R, T), dtype=f64, device=dev)
+        self.P = torch.empty((T, LA), dtype=f32, device=dev)
+        self.tuning64 = torch.empty((LA, N), dtype=f64, device=dev)
+        self.tuning32 = torch.empty((LA, N), dtype=f32, device=dev)
+        self.yw = torch.empty((LA, N), dtype=f64, device=dev)
+        self.tw = torch.empty(LA, dtype=f64, device=dev)
+        self.ws_em = torch.empty(int(self.lib.pmg_emission_workspace_size(T, LA, N)), dtype=torch.uint8, device=dev)
+        fb = int(self.lib.pmg_fwdbwd_batched_workspace_size(T, L, min(self.C, self.Cb), R))
+        if fb == 0:
+            raise nat.NativeError(f"n_latent_bin={L} unsupported by the scan kernels (max 1024)")
+        self.ws_fb = torch.zeros(fb, dtype=torch.uint8, device=dev)    # zero-filled once (include/pmg.h)
+        self.slab = (fb // R) & ~255 if R > 1 else fb
+        ss_bytes = (self.lib.pmg_suffstats_bf16_workspace_size(T, LA, N) if spikes.ybt is not None
+                    else self.lib.pmg_suffstats_workspace_size(T, LA, spikes.Np))
+        self.ws_ss = torch.empty(int(ss_bytes), dtype=torch.uint8, device=dev)
+        self.ws_ad = None
+        self.warm = [int(self.scan.warmup), int(self.scan.warmup)]
+        self.timer = None
+        self._tr_c = None
+        self.ma_latent = None
+
+    _t = DeviceEM._t
+
+    def set_transition(self, tr):
+        if isinstance(tr, DenseTransition):
+            raise NotImplementedError("batched restarts run the banded scans only")
+        DeviceEM.set_transition(self, tr)
+
+    def set_ma_latent(self, ma_latent):
+        if ma_latent is None:
+            self.ma_latent = None
+            return
+        m = np.asarray(ma_latent)
+        if m.shape != (self.L,):
+            raise ValueError(f"ma_latent must have shape ({self.L},)")
+        self.ma_latent = None if np.all(m != 0) else torch.as_tensor(
+            np.tile((m != 0).astype(np.uint8), self.R), device=self.dev)
+
+    def set_log_posterior(self, log_posts):
+        """P[:, r L:(r+1) L] = exp(log_posts[r]) for the first M-step; log_posts (R, T, L)."""
+        lp = torch.as_tensor(np.ascontiguousarray(log_posts, dtype=np.float32), device=self.dev)
+        if tuple(lp.shape) != (self.R, self.T, self.L):
+            raise ValueError(f"log_posteriors must be {(self.R, self.T, self.L)}")
+        stacked = lp.permute(1, 0, 2).contiguous()       # (T, R, L) = the stacked layout
+        nat.check(self.lib.pmg_exp(nat.ptr(stacked), stacked.numel(), nat.ptr(self.P), nat.stream_handle()),
+                  "pmg_exp")
+
+    # ------------------------------------------------------------------ M-step
+    def m_step(self, W, mu, nu, count, cfg: AdamConfig, stats_out, lh_out, eh_out):
+        """W, mu, nu (R, NB, N) f64, count (R,) int64; stats_out (R, 4), lh/eh (R, maxiter)."""
+        sh = nat.stream_handle()
+        T, LA, N = self.T, self.R * self.L, self.N
+        with self._t('suffstats'):
+            if self.sp.ybt is not None:
+                nat.check(self.lib.pmg_suffstats_bf16(nat.ptr(self.P), nat.ptr(self.sp.ybt), T, self.sp.Tp, LA, N,
+                                                      self.sp.Np, nat.ptr(self.yw), nat.ptr(self.tw),
+                                                      nat.ptr(self.ws_ss), self.ws_ss.numel(), sh),
+                          "pmg_suffstats_bf16")
+            else:
+                nat.check(self.lib.pmg_suffstats(nat.ptr(self.P), nat.ptr(self.sp.yext), T, LA, N, self.sp.Np,
+                                                 nat.ptr(self.yw), nat.ptr(self.tw), nat.ptr(self.ws_ss),
+                                                 self.ws_ss.numel(), sh), "pmg_suffstats")
+        L, NB = self.L, self.NB
+        tiled = (L > DeviceEM.PERSISTENT_MAX_L or NB > DeviceEM.PERSISTENT_MAX_NB
+                 or not self.lib.pmg_mstep_adam_supported(L, NB, N))
+        need = int(self.lib.pmg_mstep_tiled_workspace_size(L, NB, N) if tiled
+                   else self.lib.pmg_mstep_workspace_size(N, int(cfg.maxiter)))
+        if self.ws_ad is None or self.ws_ad.numel() < need:
+            self.ws_ad = torch.empty(need, dtype=torch.uint8, device=self.dev)
+        c = cfg.to_c()
+        fn = self.lib.pmg_mstep_adam_tiled if tiled else self.lib.pmg_mstep_adam
+        with self._t('mstep_adam'):
+            for r in range(self.R):
+                nat.check(fn(nat.ptr(W[r]), nat.ptr(mu[r]), nat.ptr(nu[r]), nat.ptr(count[r:r + 1]),
+                             nat.ptr(self.basis), nat.ptr(self.yw[r * L:(r + 1) * L]),
+                             nat.ptr(self.tw[r * L:(r + 1) * L]), L, NB, N, ctypes.byref(c),
+                             nat.ptr(stats_out[r]), nat.ptr(lh_out[r]), nat.ptr(eh_out[r]),
+                             nat.ptr(self.ws_ad), self.ws_ad.numel(), sh),
+                          "pmg_mstep_adam_tiled" if tiled else "pmg_mstep_adam")
+
+    def compute_tuning(self, W):
+        with self._t('tuning_softplus'):
+            nat.check(self.lib.pmg_tuning_softplus_batched(nat.ptr(self.basis), nat.ptr(W), self.L, self.NB, self.N,
+                                                           self.R, nat.ptr(self.tuning64), nat.ptr(self.tuning32),
+                                                           nat.stream_handle()), "pmg_tuning_softplus_batched")
+
+    # ------------------------------------------------------------------ E-step
+    def emission(self, likelihood_scale=1.0):
+        sp, sh = self.sp, nat.stream_handle()
+        T, LA, N = self.T, self.R * self.L, self.N
+        with self._t('emission'):
+            if sp.int_path:
+                ma1 = sp.ma if (sp.ma is not None and not sp.ma_2d) else None
+                nat.check(self.lib.pmg_emission_poisson(nat.ptr(sp.yq), nat.ptr(sp.gconst), nat.ptr(self.tuning64),
+                                                        nat.ptr(ma1), nat.ptr(self.ma_latent), 1.0, T, LA, N, sp.Kp,
+                                                        nat.ptr(self.delta), nat.ptr(self.rblk), nat.ptr(self.ws_em),
+                                                        self.ws_em.numel(), sh), "pmg_emission_poisson")
+            else:
+                nat.check(self.lib.pmg_emission_poisson_f64(nat.ptr(sp.y), nat.ptr(sp.gconst), nat.ptr(self.tuning64),
+                                                            nat.ptr(sp.ma), int(sp.ma_2d), nat.ptr(self.ma_latent),
+                                                            1.0, T, LA, N, nat.ptr(self.delta), nat.ptr(self.rblk),
+                                                            nat.ptr(self.ws_em), self.ws_em.numel(), sh),
+                          "pmg_emission_poisson_f64")
+        with self._t('emission_rowref'):
+            nat.check(self.lib.pmg_emission_rowref_batched(nat.ptr(self.rblk), T, self.R * self.nblk, self.R,
+                                                           float(likelihood_scale), nat.ptr(self.phi),
+                                                           nat.ptr(self.mref), sh), "pmg_emission_rowref_batched")
+
+    def forward(self, likelihood_scale, logz_out, keep_alpha=True):
+        """logz_out: (R,) f64 device tensor."""
+        bits = 0 if keep_alpha else nat.PHASE_NO_JUMP_ROWS
+        args = (nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.mref), self.T, self.R,
+                ctypes.byref(self._tr_c), float(likelihood_scale), self.C, int(self.warm[0]), float(self.scan.tol),
+                nat.ptr(self.alpha), nat.ptr(self.logc), nat.ptr(logz_out), nat.ptr(self.ws_fb),
+                self.ws_fb.numel(), nat.stream_handle())
+        with self._t('forward_filter'):
+            nat.check(self.lib.pmg_forward_filter_batched(*args, 1 | bits), "pmg_forward_filter_batched")
+        with self._t('forward_repair'):
+            nat.check(self.lib.pmg_forward_filter_batched(*args, 2 | bits), "pmg_forward_filter_batched")
+
+    def backward(self, likelihood_scale, gamma=None):
+        """gamma: optional (R, T, 2, L) f32 posterior output."""
+        args = (nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.alpha), self.T, self.R,
+                ctypes.byref(self._tr_c), float(likelihood_scale), self.Cb, int(self.warm[1]), float(self.scan.tol),
+                nat.ptr(self.P), nat.ptr(gamma), nat.ptr(self.ws_fb), self.ws_fb.numel(), nat.stream_handle())
+        with self._t('backward_smoother'):
+            nat.check(self.lib.pmg_backward_smoother_batched(*args, 1), "pmg_backward_smoother_batched")
+        with self._t('backward_repair'):
+            nat.check(self.lib.pmg_backward_smoother_batched(*args, 2), "pmg_backward_smoother_batched")
+
+    def e_step(self, likelihood_scale, logz_out, gamma=None):
+        self.emission(likelihood_scale)
+        self.forward(likelihood_scale, logz_out, keep_alpha=gamma is not None)
+        self.backward(likelihood_scale, gamma)
+
+    def ctl_words(self, r):
+        """Restart r's scan control words (device view)."""
+        return self.ws_fb[r * self.slab:r * self.slab + 4 * nat.CTL_WORDS].view(torch.int32)
+
+    def repairs(self):
+        """[(forward, backward) chunks recomputed] per restart (device read: syncs)."""
+        out = []
+        for r in range(self.R):
+            w = self.ctl_words(r).cpu().numpy()
+            if w[nat.CTL_FWD + nat.CTL_ERR] or w[nat.CTL_BWD + nat.CTL_ERR]:
+                raise nat.NativeError(f"scan relaxation (restart {r}): grid barrier timed out (results invalid)")
+            out.append((int(w[nat.CTL_FWD + nat.CTL_REPAIRS]), int(w[nat.CTL_BWD + nat.CTL_REPAIRS])))
+        return out

@@ -20,7 +20,7 @@ import itertools
 
 import numpy as np
 
-from .core import GaussianGPLVM1D, GaussianGPLVMJump1D, PoissonGPLVM1D, PoissonGPLVMJump1D
+from .core import GaussianGPLVM1D, GaussianGPLVMJump1D, PoissonGPLVM1D, PoissonGPLVMJump1D, fit_em_restarts
 
 model_class_dict = {'poisson': PoissonGPLVMJump1D, 'gaussian': GaussianGPLVMJump1D,
                     'poisson_latentonly': PoissonGPLVM1D, 'gaussian_latentonly': GaussianGPLVM1D}
@@ -66,13 +66,22 @@ def fit_model_one_config(config, y_train, key=0, fit_kwargs=default_fit_kwargs, 
     dist = _dist()
     rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)
     mine = []
-    for k_idx in range(rank, len(key_l), world):
-        model_fit = model_class(n_neuron=np.asarray(y_train).shape[1], **config)
-        if fit_fn is None:
-            em_res = model_fit.fit_em(y_train, hyperparam={}, key=key_l[k_idx], **fit_kwargs)
-        else:
-            em_res = fit_fn(model_fit, y_train, key_l[k_idx], fit_kwargs)
-        mine.append((k_idx, model_fit, em_res))
+    idx = list(range(rank, len(key_l), world))
+    if fit_fn is None and len(idx) > 1:
+        # this rank's restarts as ONE batched fit (core.fit_em_restarts: stacked-latent
+        # emission / suff-stats GEMMs, one scan launch per pass for all of them; it runs
+        # them one by one where the model cannot be batched)
+        models = [model_class(n_neuron=np.asarray(y_train).shape[1], **config) for _ in idx]
+        ems = fit_em_restarts(models, y_train, [key_l[k] for k in idx], hyperparam={}, **fit_kwargs)
+        mine = list(zip(idx, models, ems))
+    else:
+        for k_idx in idx:
+            model_fit = model_class(n_neuron=np.asarray(y_train).shape[1], **config)
+            if fit_fn is None:
+                em_res = model_fit.fit_em(y_train, hyperparam={}, key=key_l[k_idx], **fit_kwargs)
+            else:
+                em_res = fit_fn(model_fit, y_train, key_l[k_idx], fit_kwargs)
+            mine.append((k_idx, model_fit, em_res))
     if dist and world > 1:
         gathered = [None] * world
         dist.all_gather_object(gathered, mine)

@@ -11,9 +11,11 @@ C2 (N=128, T=1e4, L=256): the f64 oracle needs ~1 min per E-step at this size, s
   tuning rel 1e-5; identical Adam iteration count.
 C4 (N=1024, L=1024; a T=1e5 slice of the T=1e6 job): 8 time shards (virtual, one GPU)
   vs the unsharded engine, one EM iteration (bars of test_gpu_timeshard._vs_single).
-C5 (8 restarts, N=256, T=5e4, L=256 through model_selection_helper.fit_model_one_config):
-  properties of every restart (finite, normalised, restarts differ, re-running a key
-  reproduces it bit for bit) and one restart against the f64 oracle at T=1500.
+C5 (8 restarts, N=256, T=5e4, L=256 through model_selection_helper.fit_model_one_config,
+  which batches a rank's restarts in one fit, core.fit_em_restarts): properties of every
+  restart (finite, normalised, restarts differ, re-running the keys reproduces them bit
+  for bit, one restart alone on the same chunk grid gives the same fit) and one restart
+  against the f64 oracle at T=1500.
 """
 import os
 
@@ -109,10 +111,26 @@ def test_c5_restarts():
         np.testing.assert_allclose(np.asarray(e['posterior'], np.float64).sum(axis=(1, 2)), 1.0, rtol=1e-5)
         assert np.all(np.isfinite(e['tuning'])) and np.all(np.asarray(e['tuning']) > 0)
     assert all(np.abs(tun[i] - tun[0]).max() > 0 for i in range(1, R))      # different posterior inits
+    # the 8 restarts ran as one batched fit (core.fit_em_restarts)
+    assert all(m.fit_info.get('batched_restarts') == R for m in models)
     keys = MS.split_keys(0, R)
-    again, ems2 = MS.fit_model_one_config(cfg, d['y'], key=[keys[3]], fit_kwargs=kw)
-    np.testing.assert_array_equal(ems2[0]['tuning'], ems[3]['tuning'])
-    np.testing.assert_array_equal(ems2[0]['posterior_latent_marg'], ems[3]['posterior_latent_marg'])
+    _, ems_again = MS.fit_model_one_config(cfg, d['y'], key=keys, fit_kwargs=kw)   # deterministic
+    for a, b in zip(ems, ems_again):
+        np.testing.assert_array_equal(a['tuning'], b['tuning'])
+        np.testing.assert_array_equal(a['posterior_latent_marg'], b['posterior_latent_marg'])
+    # restart 3 alone (one fit_em, same chunk grid as the batch): the same fit up to the
+    # relaxation's segment grid (CUs / 8 segments per restart in the batch, CUs alone),
+    # which moves repaired boundaries within the scan tolerance; after the second
+    # M-step that reaches the posterior through its tuning sensitivity,
+    # hence the multi-iteration EM bar of test_fit_em_fixed_iterations_golden
+    import poor_man_gplvm_amd as P
+    C = models[0].fit_info['chunk']
+    cfg1 = dict(cfg, scan_config=P.ScanConfig(chunk=C, chunk_bwd=2 * C))
+    _, ems2 = MS.fit_model_one_config(cfg1, d['y'], key=[keys[3]], fit_kwargs=kw)
+    assert ems2[0]['m_step_res_l']['n_iter'] == ems[3]['m_step_res_l']['n_iter']
+    np.testing.assert_allclose(ems2[0]['tuning'], ems[3]['tuning'], rtol=1e-5)
+    assert np.abs(ems2[0]['posterior_latent_marg'] - ems[3]['posterior_latent_marg']).max() <= 1e-5
+    argmax_match(ems2[0]['posterior_latent_marg'], ems[3]['posterior_latent_marg'])
 
 
 def test_c5_restart_vs_oracle():

@@ -110,3 +110,16 @@ def test_model_class_dict_matches_reference_names():
     import poor_man_gplvm_amd as P
     assert MS.model_class_dict['gaussian_latentonly'] is P.GaussianGPLVM1D
     assert issubclass(P.GaussianGPLVM1D, P.PoissonGPLVM1D)      # latent-only engine
+
+
+def test_restarts_batchable_rules():
+    """core._restarts_batchable: which model lists fit_em_restarts runs as one batch."""
+    import poor_man_gplvm_amd as P
+    from poor_man_gplvm_amd.core import _restarts_batchable
+    mk = lambda cls=P.PoissonGPLVMJump1D, **kw: cls(12, **dict(dict(n_latent_bin=64, tuning_lengthscale=10.), **kw))
+    assert _restarts_batchable([mk(), mk(), mk()], {})
+    assert not _restarts_batchable([mk(n_latent_bin=100), mk(n_latent_bin=100)], {})      # L % 32
+    assert not _restarts_batchable([mk(), mk(movement_variance=2.0)], {})                  # configs differ
+    assert not _restarts_batchable([mk(), mk(rng_init_int=5)], {})                         # initial W differs
+    assert not _restarts_batchable([mk(P.GaussianGPLVMJump1D), mk(P.GaussianGPLVMJump1D)], {})
+    assert not _restarts_batchable([mk(), mk()], {'movement_variance': 9.0})               # dense transition
