@@ -356,6 +356,18 @@ int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const floa
                    const double* yw, const double* tw, int32_t L, int32_t NB, int32_t N,
                    const pmg_adam_cfg* cfg, double* stats, double* loss_hist, double* err_hist,
                    void* workspace, size_t workspace_bytes, void* stream);
+/* R restarts' M-steps (batched restarts): W, mu, nu (R,NB,N),  */
+/* count (R), yw (R*L, N) and tw (R*L) (the stacked suff-stats), stats (R,4), */
+/* loss_hist / err_hist (R, max(maxiter,1)).  Each restart runs its own loop */
+/* and stop rule (bit-identical to R pmg_mstep_adam calls); several restarts */
+/* share one persistent launch (blockIdx.y) with up to 4 neurons per        */
+/* workgroup, so R loops cost ~R * N / (4 * #CUs) launches instead of R.     */
+size_t pmg_mstep_batched_workspace_size(int32_t L, int32_t NB, int32_t N, int32_t R, int32_t maxiter);
+int pmg_mstep_adam_batched_supported(int32_t L, int32_t NB, int32_t N, int32_t R);
+int pmg_mstep_adam_batched(double* W, double* mu, double* nu, int64_t* count, const float* basis,
+                           const double* yw, const double* tw, int32_t L, int32_t NB, int32_t N, int32_t R,
+                           const pmg_adam_cfg* cfg, double* stats, double* loss_hist, double* err_hist,
+                           void* workspace, size_t workspace_bytes, void* stream);
 
 /* Same loop and outputs for shapes the persistent kernel does not hold          */
 /* (L > 512 or NB > 128, e.g. BASELINE C4: L = 1024, NB = 154): per body an f64    */

@@ -45,6 +45,7 @@ EXPORTED_SYMBOLS = (
     "pmg_dense_workspace_size", "pmg_dense_forward", "pmg_dense_backward", "pmg_joint_log_accumulate",
     "pmg_tuning_softplus_batched", "pmg_emission_rowref_batched", "pmg_fwdbwd_batched_workspace_size",
     "pmg_forward_filter_batched", "pmg_backward_smoother_batched",
+    "pmg_mstep_batched_workspace_size", "pmg_mstep_adam_batched_supported", "pmg_mstep_adam_batched",
 )
 
 
@@ -135,6 +136,10 @@ _SIGS = {
     "pmg_joint_log_accumulate": ([_P, _P, _I64, _I32, _P, _P], _I32),
     "pmg_joint_accumulate": ([_P, _P, _I64, _I32, _P, _P, _SZ, _P], _I32),
     "pmg_tuning_softplus_batched": ([_P, _P, _I32, _I32, _I32, _I32, _P, _P, _P], _I32),
+    "pmg_mstep_batched_workspace_size": ([_I32, _I32, _I32, _I32, _I32], _SZ),
+    "pmg_mstep_adam_batched_supported": ([_I32, _I32, _I32, _I32], ctypes.c_int),
+    "pmg_mstep_adam_batched": ([_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, ctypes.POINTER(AdamCfg),
+                                _P, _P, _P, _P, _SZ, _P], _I32),
     "pmg_emission_rowref_batched": ([_P, _I64, _I32, _I32, _D, _P, _P, _P], _I32),
     "pmg_fwdbwd_batched_workspace_size": ([_I64, _I32, _I32, _I32], _SZ),
     "pmg_forward_filter_batched": ([_P, _P, _P, _I64, _I32, ctypes.POINTER(Transition), _D, _I32, _I32, _D,

@@ -56,7 +56,35 @@ struct AdamParams {
   double* ring;               // [G][kRing][3][NBM*4] (W, mu, nu) after each body
   int* timeout;
   long long* prof;            // optional (PMG_ADAM_PROF): s_memtime stamps of WG 0, bodies < 64
+  // batched restarts (blockIdx.y = restart r of this launch): per-restart strides of the
+  // operands (elements) and of the restart's workspace slab (bytes)
+  int64_t rs_W, rs_yw, rs_ws;
+  int rs_tw, rs_hist;
 };
+
+// restart r's view of the parameters (identity for blockIdx.y = 0)
+__device__ __forceinline__ AdamParams adam_view(const AdamParams& p0) {
+  AdamParams p = p0;
+  const int64_t r = blockIdx.y;
+  if (r == 0) return p;
+  p.W += r * p.rs_W;
+  p.mu += r * p.rs_W;
+  p.nu += r * p.rs_W;
+  p.count += r;
+  p.yw += r * p.rs_yw;
+  p.tw += r * p.rs_tw;
+  p.stats += 4 * r;
+  p.loss_hist += r * p.rs_hist;
+  p.err_hist += r * p.rs_hist;
+  const uintptr_t o = (uintptr_t)(r * p.rs_ws);
+  p.bias = reinterpret_cast<const double*>(reinterpret_cast<uintptr_t>(p.bias) + o);
+  p.lpart = reinterpret_cast<unsigned long long*>(reinterpret_cast<uintptr_t>(p.lpart) + o);
+  p.gpart = reinterpret_cast<unsigned long long*>(reinterpret_cast<uintptr_t>(p.gpart) + o);
+  p.ring = reinterpret_cast<double*>(reinterpret_cast<uintptr_t>(p.ring) + o);
+  p.timeout = reinterpret_cast<int*>(reinterpret_cast<uintptr_t>(p.timeout) + o);
+  p.prof = nullptr;
+  return p;
+}
 
 #define PMG_ADAM_STAMP(k, i)                                                   \
   if (p.prof && g == 0 && tid == 0 && (k) < 64) p.prof[(k) * 8 + (i)] = __builtin_amdgcn_s_memtime();
@@ -101,10 +129,18 @@ __global__ void k_fill_u64(unsigned long long* __restrict__ x, size_t n, unsigne
 // corrections of every body from the Adam step count, c_k = 1 / (1 - b^(count0 + k + 1)).
 // A closed form per body (not a running product) gives the same bits however the loop
 // is split into launches (the speculative batches of the neuron-sharded M-step).
-__global__ void k_adam_prologue(unsigned long long* __restrict__ lpart, unsigned long long* __restrict__ gpart,
-                                size_t n, const int64_t* __restrict__ count, double b1, double b2, int maxiter,
-                                double* __restrict__ bias, double* __restrict__ loss_hist,
-                                double* __restrict__ err_hist, double* __restrict__ stats, int* __restrict__ timeout) {
+__global__ void k_adam_prologue(AdamParams p_arg, size_t n) {
+  const AdamParams p = adam_view(p_arg);
+  unsigned long long* __restrict__ lpart = p.lpart;
+  unsigned long long* __restrict__ gpart = p.gpart;
+  const int64_t* __restrict__ count = p.count;
+  const double b1 = p.b1, b2 = p.b2;
+  const int maxiter = p.maxiter > 1 ? p.maxiter : 1;
+  double* __restrict__ bias = const_cast<double*>(p.bias);
+  double* __restrict__ loss_hist = p.loss_hist;
+  double* __restrict__ err_hist = p.err_hist;
+  double* __restrict__ stats = p.stats;
+  int* __restrict__ timeout = p.timeout;
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t q = i; q < n; q += stride) {
@@ -230,7 +266,8 @@ __device__ __forceinline__ int scatter_slot(int lane) {
 }
 
 template <int A, int BC, int SP>
-__global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
+__global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
+  const AdamParams p = adam_view(p_arg);
   constexpr int BCP = (BC + 3) & ~3;                                   // padded q-block (b128 reads)
   constexpr int QS = 16 * BCP;                                         // padded columns per neuron
   __shared__ __attribute__((aligned(16))) double sW[kSMax * QS];       // W_k (f64), [s][qb][BCP]
@@ -577,7 +614,8 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p) {
 // Histories (fit_tuning_helper.py:147-149, :175-176) from the published partials, summed
 // in the decision's order: loss_hist[0] = loss of body 0, loss_hist[j+1] = loss of body j
 // (j + 1 < n_iter); the same for the gradient norm; final_error = norm of the last body.
-__global__ void __launch_bounds__(64) k_adam_hist(AdamParams p) {
+__global__ void __launch_bounds__(64) k_adam_hist(AdamParams p_arg) {
+  const AdamParams p = adam_view(p_arg);
   const int lane = threadIdx.x;
   const int n_iter = (int)p.stats[0];
   if (n_iter <= 0) return;
@@ -671,6 +709,29 @@ static void adam_geometry(int N, int L, int NB, int& S, int& G, int& ng, int& LG
   LG = (L + ng - 1) / ng;
 }
 
+// R restarts: Rg of them per launch, each on G workgroups of S neurons, with Rg G <= #CUs
+// (one 512-thread workgroup per CU: every workgroup of a launch is resident).  S grows
+// (up to kSMax, while the kernel still fits) so that more restarts share a launch.
+static void adam_batch_geometry(int N, int L, int NB, int R, int& S, int& G, int& ng, int& LG, int& Rg) {
+  adam_geometry(N, L, NB, S, G, ng, LG);
+  const int cus = num_cus();
+  if (R > 1) {
+    int want = (int)(((int64_t)R * N + cus - 1) / cus);
+    if (want == 3) want = 4;
+    for (int s = want < kSMax ? want : kSMax; s > S; s = (s == 4 ? 2 : s - 1)) {
+      AdamKernel k = pick_adam(NB, L, s);
+      if (NB * s <= kThreads && k.fn != nullptr && k.lds <= 160 * 1024) {
+        S = s;
+        G = (N + S - 1) / S;
+        break;
+      }
+    }
+  }
+  Rg = cus / G;
+  if (Rg < 1) Rg = 1;
+  if (Rg > R) Rg = R;
+}
+
 }  // namespace pmg
 
 using namespace pmg;
@@ -692,34 +753,28 @@ int pmg_mstep_adam_supported(int32_t L, int32_t NB, int32_t N) {
   return (kern.fn != nullptr && kern.lds <= 160 * 1024) ? 1 : 0;
 }
 
-int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const float* basis,
-                   const double* yw, const double* tw, int32_t L, int32_t NB, int32_t N,
-                   const pmg_adam_cfg* cfg, double* stats, double* loss_hist, double* err_hist,
-                   void* workspace, size_t workspace_bytes, void* stream) {
-  PMG_REQUIRE(cfg && W && mu && nu && count && basis && yw && tw && stats && loss_hist && err_hist &&
-                  workspace,
+// R restarts (R = 1: the plain call): restarts r0 .. r0+Rg-1 of each launch are its
+// blockIdx.y; every restart has its own workspace slab of `slab` bytes.
+static int adam_run(double* W, double* mu, double* nu, int64_t* count, const float* basis, const double* yw,
+                    const double* tw, int L, int NB, int N, int R, const pmg_adam_cfg* cfg, double* stats,
+                    double* loss_hist, double* err_hist, void* workspace, size_t workspace_bytes, hipStream_t st) {
+  PMG_REQUIRE(cfg && W && mu && nu && count && basis && yw && tw && stats && loss_hist && err_hist && workspace,
               "pmg_mstep_adam: null argument");
   PMG_REQUIRE(L > 0 && L <= kThreads, "pmg_mstep_adam: L=%d must be in [1, %d]", L, kThreads);
-  PMG_REQUIRE(NB > 0 && N > 0, "pmg_mstep_adam: bad shape");
-  int S, G, ng, LG;
-  adam_geometry(N, L, NB, S, G, ng, LG);
+  PMG_REQUIRE(NB > 0 && N > 0 && R >= 1 && R <= 65535, "pmg_mstep_adam: bad shape");
+  int S, G, ng, LG, Rg;
+  adam_batch_geometry(N, L, NB, R, S, G, ng, LG, Rg);
   PMG_REQUIRE(S <= kSMax, "pmg_mstep_adam: N=%d needs %d neurons per workgroup (> %d)", N, S, kSMax);
   PMG_REQUIRE(NB * S <= kThreads, "pmg_mstep_adam: NB*S=%d > %d", NB * S, kThreads);
   AdamKernel kern = pick_adam(NB, L, S);
   PMG_REQUIRE(kern.fn != nullptr && kern.lds <= 160 * 1024,
               "pmg_mstep_adam: NB=%d unsupported (basis must fit registers + 160 KiB LDS)", NB);
   const int maxiter = cfg->maxiter > 1 ? cfg->maxiter : 1;
-  PMG_REQUIRE(workspace_bytes >= adam_ws(G, maxiter, nullptr, nullptr),
+  const size_t slab = (adam_ws(G, maxiter, nullptr, nullptr) + 255) & ~(size_t)255;
+  PMG_REQUIRE(workspace_bytes >= (R == 1 ? adam_ws(G, maxiter, nullptr, nullptr) : (size_t)R * slab),
               "pmg_mstep_adam: workspace too small");
-  hipStream_t st = as_stream(stream);
   AdamWork w;
   adam_ws(G, maxiter, &w, workspace);
-  {
-    const size_t n = ((size_t)maxiter + kLag + 2) * G;
-    hipLaunchKernelGGL(k_adam_prologue, dim3(256), dim3(256), 0, st, w.lpart, w.gpart, n, (const int64_t*)count,
-                       cfg->b1, cfg->b2, maxiter, w.bias, loss_hist, err_hist, stats, w.timeout);
-    PMG_LAUNCH_CHECK();
-  }
   AdamParams p;
   memset(&p, 0, sizeof(p));
   p.W = W;
@@ -752,6 +807,11 @@ int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const floa
   p.timeout = w.timeout;
   p.ring = w.ring;
   p.bias = w.bias;
+  p.rs_W = (int64_t)NB * N;
+  p.rs_yw = (int64_t)L * N;
+  p.rs_tw = L;
+  p.rs_hist = maxiter;
+  p.rs_ws = (int64_t)slab;
   static long long* prof_buf = nullptr;   // debug: per-phase stamps (PMG_ADAM_PROF set)
   const bool prof = getenv("PMG_ADAM_PROF") != nullptr;
   if (prof) {
@@ -761,31 +821,87 @@ int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const floa
   } else {
     p.prof = nullptr;
   }
-  hipLaunchKernelGGL(kern.fn, dim3(G), dim3(kThreads), kern.lds, st, p);
-  PMG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_adam_hist, dim3(64), dim3(64), 0, st, p);
-  PMG_LAUNCH_CHECK();
+  const size_t n = ((size_t)maxiter + kLag + 2) * G;
+  for (int r0 = 0; r0 < R; r0 += Rg) {
+    const int rg = R - r0 < Rg ? R - r0 : Rg;
+    AdamParams q = p;   // restart r0's pointers
+    q.W += r0 * p.rs_W;
+    q.mu += r0 * p.rs_W;
+    q.nu += r0 * p.rs_W;
+    q.count += r0;
+    q.yw += r0 * p.rs_yw;
+    q.tw += (int64_t)r0 * p.rs_tw;
+    q.stats += 4 * (int64_t)r0;
+    q.loss_hist += (int64_t)r0 * p.rs_hist;
+    q.err_hist += (int64_t)r0 * p.rs_hist;
+    const size_t o = (size_t)r0 * slab;
+    q.bias = reinterpret_cast<const double*>(reinterpret_cast<char*>(w.bias) + o);
+    q.lpart = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(w.lpart) + o);
+    q.gpart = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(w.gpart) + o);
+    q.ring = reinterpret_cast<double*>(reinterpret_cast<char*>(w.ring) + o);
+    q.timeout = reinterpret_cast<int*>(reinterpret_cast<char*>(w.timeout) + o);
+    hipLaunchKernelGGL(k_adam_prologue, dim3(256, rg), dim3(256), 0, st, q, n);
+    PMG_LAUNCH_CHECK();
+    // rg x G workgroups, at most one per CU (adam_batch_geometry): all co-resident
+    hipLaunchKernelGGL(kern.fn, dim3(G, rg), dim3(kThreads), kern.lds, st, q);
+    PMG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_adam_hist, dim3(64, rg), dim3(64), 0, st, q);
+    PMG_LAUNCH_CHECK();
+  }
   if (prof) {
     long long h[64 * 8];
     PMG_HIP(hipMemcpyAsync(h, prof_buf, sizeof(h), hipMemcpyDeviceToHost, st));
     PMG_HIP(hipStreamSynchronize(st));
     double acc[6] = {0, 0, 0, 0, 0, 0};
     long long spins = 0;
-    int n = 0;
+    int cnt = 0;
     for (int k = 8; k + 1 < 64; ++k) {   // skip the pipeline fill
       if (h[k * 8 + 4] == 0 || h[(k + 1) * 8] == 0) break;
       for (int i = 0; i < 4; ++i) acc[i] += (double)(h[k * 8 + i + 1] - h[k * 8 + i]);
       acc[4] += (double)(h[(k + 1) * 8] - h[k * 8 + 4]);
       acc[5] += (double)(h[k * 8 + 6] - h[k * 8 + 5]);
       spins += h[k * 8 + 7];
-      ++n;
+      ++cnt;
     }
-    if (n > 0)
+    if (cnt > 0)
       fprintf(stderr, "[pmg adam prof] bodies=%d ticks/body: rows %.0f | bar1 %.0f | update %.0f | "
-              "sums+bar2+publish %.0f | loop %.0f | decision (ctl wave) %.0f, blocking polls %lld\n", n,
-              acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n, spins);
+              "sums+bar2+publish %.0f | loop %.0f | decision (ctl wave) %.0f, blocking polls %lld\n", cnt,
+              acc[0] / cnt, acc[1] / cnt, acc[2] / cnt, acc[3] / cnt, acc[4] / cnt, acc[5] / cnt, spins);
   }
   return PMG_OK;
+}
+
+int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const float* basis,
+                   const double* yw, const double* tw, int32_t L, int32_t NB, int32_t N,
+                   const pmg_adam_cfg* cfg, double* stats, double* loss_hist, double* err_hist,
+                   void* workspace, size_t workspace_bytes, void* stream) {
+  return adam_run(W, mu, nu, count, basis, yw, tw, L, NB, N, 1, cfg, stats, loss_hist, err_hist, workspace,
+                  workspace_bytes, as_stream(stream));
+}
+
+size_t pmg_mstep_batched_workspace_size(int32_t L, int32_t NB, int32_t N, int32_t R, int32_t maxiter) {
+  if (L <= 0 || NB <= 0 || N <= 0 || R < 1) return 0;
+  int S, G, ng, LG, Rg;
+  adam_batch_geometry(N, L, NB, R, S, G, ng, LG, Rg);
+  const size_t one = adam_ws(G, maxiter > 1 ? maxiter : 1, nullptr, nullptr);
+  return R == 1 ? one : (size_t)R * ((one + 255) & ~(size_t)255);
+}
+
+int pmg_mstep_adam_batched_supported(int32_t L, int32_t NB, int32_t N, int32_t R) {
+  if (L <= 0 || L > kThreads || NB <= 0 || N <= 0 || R < 1) return 0;
+  int S, G, ng, LG, Rg;
+  adam_batch_geometry(N, L, NB, R, S, G, ng, LG, Rg);
+  if (S > kSMax || NB * S > kThreads) return 0;
+  AdamKernel kern = pick_adam(NB, L, S);
+  return (kern.fn != nullptr && kern.lds <= 160 * 1024) ? 1 : 0;
+}
+
+int pmg_mstep_adam_batched(double* W, double* mu, double* nu, int64_t* count, const float* basis,
+                           const double* yw, const double* tw, int32_t L, int32_t NB, int32_t N, int32_t R,
+                           const pmg_adam_cfg* cfg, double* stats, double* loss_hist, double* err_hist,
+                           void* workspace, size_t workspace_bytes, void* stream) {
+  return adam_run(W, mu, nu, count, basis, yw, tw, L, NB, N, R, cfg, stats, loss_hist, err_hist, workspace,
+                  workspace_bytes, as_stream(stream));
 }
 
 }  // extern "C"

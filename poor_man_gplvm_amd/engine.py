@@ -639,8 +639,9 @@ class RestartBatchEM:
         and workspace slab), writing P (T, R L);
       * sufficient statistics: ONE bf16-MFMA GEMM over the R L latents -> y_w (R L, N),
         t_w (R L), whose row blocks are the restarts' statistics;
-      * Adam: the persistent loop once per restart on its (L, N) slab (each restart keeps
-        its own stop rule, as R separate fits would).
+      * Adam: pmg_mstep_adam_batched, several restarts per persistent launch (each its
+        own loop and stop rule, bit-identical to separate fits); the tiled kernels run
+        once per restart where the persistent one cannot hold the shape.
     Chunks are sized so the R restarts together run ~2048 chains (R x longer chunks than
     one restart alone: the warm-up is amortised over R x more output steps).
     Banded transitions only; L % 32 == 0; Poisson observation model."""
@@ -735,14 +736,26 @@ class RestartBatchEM:
                 nat.check(self.lib.pmg_suffstats(nat.ptr(self.P), nat.ptr(self.sp.yext), T, LA, N, self.sp.Np,
                                                  nat.ptr(self.yw), nat.ptr(self.tw), nat.ptr(self.ws_ss),
                                                  self.ws_ss.numel(), sh), "pmg_suffstats")
-        L, NB = self.L, self.NB
-        tiled = (L > DeviceEM.PERSISTENT_MAX_L or NB > DeviceEM.PERSISTENT_MAX_NB
-                 or not self.lib.pmg_mstep_adam_supported(L, NB, N))
-        need = int(self.lib.pmg_mstep_tiled_workspace_size(L, NB, N) if tiled
-                   else self.lib.pmg_mstep_workspace_size(N, int(cfg.maxiter)))
+        L, NB, R = self.L, self.NB, self.R
+        batched = (L <= DeviceEM.PERSISTENT_MAX_L and NB <= DeviceEM.PERSISTENT_MAX_NB
+                   and bool(self.lib.pmg_mstep_adam_batched_supported(L, NB, N, R)))
+        tiled = not batched and (L > DeviceEM.PERSISTENT_MAX_L or NB > DeviceEM.PERSISTENT_MAX_NB
+                                 or not self.lib.pmg_mstep_adam_supported(L, NB, N))
+        if batched:
+            need = int(self.lib.pmg_mstep_batched_workspace_size(L, NB, N, R, int(cfg.maxiter)))
+        else:
+            need = int(self.lib.pmg_mstep_tiled_workspace_size(L, NB, N) if tiled
+                       else self.lib.pmg_mstep_workspace_size(N, int(cfg.maxiter)))
         if self.ws_ad is None or self.ws_ad.numel() < need:
             self.ws_ad = torch.empty(need, dtype=torch.uint8, device=self.dev)
         c = cfg.to_c()
+        if batched:     # several restarts per persistent launch, each its own loop and stop rule
+            with self._t('mstep_adam'):
+                nat.check(self.lib.pmg_mstep_adam_batched(
+                    nat.ptr(W), nat.ptr(mu), nat.ptr(nu), nat.ptr(count), nat.ptr(self.basis), nat.ptr(self.yw),
+                    nat.ptr(self.tw), L, NB, N, R, ctypes.byref(c), nat.ptr(stats_out), nat.ptr(lh_out),
+                    nat.ptr(eh_out), nat.ptr(self.ws_ad), self.ws_ad.numel(), sh), "pmg_mstep_adam_batched")
+            return
         fn = self.lib.pmg_mstep_adam_tiled if tiled else self.lib.pmg_mstep_adam
         with self._t('mstep_adam'):
             for r in range(self.R):

@@ -100,3 +100,61 @@ def test_fit_em_restarts_public_api():
     g = [P.GaussianGPLVMJump1D(N, n_latent_bin=L, tuning_lengthscale=10.) for _ in range(2)]
     out = P.fit_em_restarts(g, d['y'], [1, 2], n_iter=1)
     assert len(out) == 2 and 'batched_restarts' not in g[0].fit_info
+
+
+@pytest.mark.parametrize("L,NB_ls,N,R,maxiter,tol", [(256, 10., 256, 8, 1000, 1e-6), (64, 10., 40, 5, 300, 1e-6),
+                                                     (128, 5., 300, 3, 50, 0.0)])
+def test_batched_adam_bit_identical(L, NB_ls, N, R, maxiter, tol):
+    """pmg_mstep_adam_batched (several restarts per persistent launch, up to 4 neurons per
+    workgroup) == R pmg_mstep_adam calls: W / mu / nu and the step counts bit for bit (the
+    per-element arithmetic does not depend on the neuron partition), iteration counts
+    identical, loss histories to the last bits of their summation order."""
+    import ctypes
+    from poor_man_gplvm_amd import _native as nat
+    from poor_man_gplvm_amd.engine import AdamConfig
+    lib = nat.load()
+    dev = torch.device('cuda', 0)
+    B = O.generate_basis(NB_ls, L).astype(np.float32)
+    NB = B.shape[1]
+    rng = np.random.default_rng(4)
+    W0 = torch.tensor(rng.normal(size=(R, NB, N)), dtype=torch.float64, device=dev)
+    P = rng.random((R, 2000, L))
+    P /= P.sum(-1, keepdims=True)
+    y = rng.poisson(2.0, size=(2000, N)).astype(np.float64)
+    yw = torch.tensor(np.concatenate([p.T @ y for p in P]), dtype=torch.float64, device=dev)     # (R L, N)
+    tw = torch.tensor(np.concatenate([p.sum(0) for p in P]), dtype=torch.float64, device=dev)
+    Bt = torch.tensor(B, device=dev)
+    cfg = AdamConfig(maxiter=maxiter, tol=tol).to_c()
+    mi = max(maxiter, 1)
+
+    def run(batched):
+        W, mu, nu = W0.clone(), torch.zeros_like(W0), torch.zeros_like(W0)
+        cnt = torch.zeros(R, dtype=torch.int64, device=dev)
+        st = torch.zeros((R, 4), dtype=torch.float64, device=dev)
+        lh = torch.zeros((R, mi), dtype=torch.float64, device=dev)
+        eh = torch.zeros_like(lh)
+        for _ in range(2):    # two M-steps: the Adam state carries over
+            if batched:
+                assert lib.pmg_mstep_adam_batched_supported(L, NB, N, R)
+                ws = torch.empty(int(lib.pmg_mstep_batched_workspace_size(L, NB, N, R, maxiter)), dtype=torch.uint8,
+                                 device=dev)
+                nat.check(lib.pmg_mstep_adam_batched(nat.ptr(W), nat.ptr(mu), nat.ptr(nu), nat.ptr(cnt), nat.ptr(Bt),
+                                                     nat.ptr(yw), nat.ptr(tw), L, NB, N, R, ctypes.byref(cfg),
+                                                     nat.ptr(st), nat.ptr(lh), nat.ptr(eh), nat.ptr(ws), ws.numel(),
+                                                     nat.stream_handle()), "batched")
+            else:
+                ws = torch.empty(int(lib.pmg_mstep_workspace_size(N, maxiter)), dtype=torch.uint8, device=dev)
+                for r in range(R):
+                    nat.check(lib.pmg_mstep_adam(nat.ptr(W[r]), nat.ptr(mu[r]), nat.ptr(nu[r]), nat.ptr(cnt[r:r + 1]),
+                                                 nat.ptr(Bt), nat.ptr(yw[r * L:(r + 1) * L]),
+                                                 nat.ptr(tw[r * L:(r + 1) * L]), L, NB, N, ctypes.byref(cfg),
+                                                 nat.ptr(st[r]), nat.ptr(lh[r]), nat.ptr(eh[r]), nat.ptr(ws),
+                                                 ws.numel(), nat.stream_handle()), "single")
+        torch.cuda.synchronize()
+        return [t.cpu().numpy() for t in (W, mu, nu, cnt, st, lh)]
+    a, b = run(True), run(False)
+    for x, z in zip(a[:4], b[:4]):
+        np.testing.assert_array_equal(x, z)
+    np.testing.assert_array_equal(a[4][:, 0], b[4][:, 0])          # n_iter per restart
+    np.testing.assert_allclose(a[5], b[5], rtol=1e-12)             # loss histories
+    assert len(set(a[4][:, 0].tolist())) >= 1 and np.all(a[4][:, 0] >= 1)
