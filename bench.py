@@ -538,12 +538,14 @@ def bench_restarts(args):
         eng.compute_tuning(W)
         eng.e_step(1.0, logz[i])
 
-    def run(fresh_fn, step_fn):
+    def run(fresh_fn, step_fn, timed_engine=None, timer=None):
         fresh_fn(); step_fn(0); torch.cuda.synchronize()     # code-object pre-warm
         fresh_fn()
         for i in range(args.warmup):
             step_fn(i)
         torch.cuda.synchronize()
+        if timed_engine is not None:
+            timed_engine.timer = timer
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
@@ -553,18 +555,15 @@ def bench_restarts(args):
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
+        if timed_engine is not None:
+            timed_engine.timer = None
         if world > 1:
             te = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(te, op=dist.ReduceOp.MAX)
             el = float(te.item())
         return el
     timer = KernelTimer()
-    elapsed = run(fresh, lambda i: it(i))
-    eng.timer = timer
-    fresh()
-    for i in range(min(3, n_all)):
-        it(i)
-    eng.timer = None
+    elapsed = run(fresh, lambda i: it(i), eng, timer)      # per-kernel HIP events over the timed window
     summ = timer.summary()
     s = stats.cpu().numpy()
     adam_iters = float(np.mean(s[args.warmup:, :, 0])) if args.steps else 0.0
@@ -617,7 +616,7 @@ def bench_restarts(args):
         "kernels_ms": {k: round(v[1], 4) for k, v in summ.items()},
         "kernel_calls": {k: v[0] for k, v in summ.items()},
         "adam_iters_mean": adam_iters,
-        "chunk": [int(eng_c) for eng_c in (max(32, -(-R * T // 2048)),)],
+        "chunk": max(32, -(-R * T // 2048)),
         "log_marginal_last": [float(v) for v in lz[n_all - 1]],
     }
     if rank == 0:
