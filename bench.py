@@ -335,6 +335,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-api-fit", action="store_true", help="skip the public-API fit_em(n_iter=20) timing")
     ap.add_argument("--chunk", type=int, default=0)
+    ap.add_argument("--chunk-bwd", type=int, default=0, help="backward chunk (0: ScanConfig default, 2x forward)")
     ap.add_argument("--warm-steps", type=int, default=48)
     ap.add_argument("--warm-fb", type=str, default="", help="fixed forward,backward warm-up (no adaptation)")
     ap.add_argument("--verbose", action="store_true")
@@ -369,7 +370,7 @@ def main():
     N, T, L = CONFIGS[args.config]
     y, B, W0, lp0 = synth(N, T, L, rank=rank)
     dev = torch.device("cuda", local)
-    scan = ScanConfig(chunk=args.chunk or None, warmup=args.warm_steps)
+    scan = ScanConfig(chunk=args.chunk or None, warmup=args.warm_steps, chunk_bwd=args.chunk_bwd or None)
     sp = SpikeData(y)
     eng = DeviceEM(sp, L, basis=B, scan=scan)
     eng.set_transition(banded_transition(L, 1.0, 0.01, 0.01))

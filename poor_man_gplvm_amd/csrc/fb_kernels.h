@@ -228,12 +228,48 @@ __device__ __forceinline__ void band_conv(const FBParams& p, const float in[J], 
       if (k * J + i - (J - 1) <= WP) win[C + k * J + i] = wave_shl1(win[C + (k - 1) * J + i]);
       else win[C + k * J + i] = 0.f;
     }
+  if constexpr ((J & 1) == 0) {
+    // output pairs (j, j+1) on packed math (v_pk_fma_f32 / v_pk_add_f32): per lane the
+    // same IEEE operations as the scalar form below, so identical bits.  For even taps
+    // k both window pairs are register-aligned (one packed add); for odd k the two
+    // sums are formed by scalar adds straight into an aligned pair.
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 acc[J / 2];
 #pragma unroll
-  for (int j = 0; j < J; ++j) {
-    float acc = p.g[0] * win[C + j];
+    for (int jp = 0; jp < J / 2; ++jp) {
+      const f2 c = {win[C + 2 * jp], win[C + 2 * jp + 1]};
+      acc[jp] = (f2){p.g[0], p.g[0]} * c;
+    }
 #pragma unroll
-    for (int k = 1; k <= WP; ++k) acc = fmaf(p.g[k], win[C + j - k] + win[C + j + k], acc);
-    out[j] = acc;
+    for (int k = 1; k <= WP; ++k) {
+      const f2 gk = {p.g[k], p.g[k]};
+#pragma unroll
+      for (int jp = 0; jp < J / 2; ++jp) {
+        const int a = C + 2 * jp - k, b = C + 2 * jp + k;
+        f2 sm;
+        if ((k & 1) == 0) {
+          const f2 l = {win[a], win[a + 1]}, r = {win[b], win[b + 1]};
+          sm = l + r;
+        } else {
+          sm.x = win[a] + win[b];
+          sm.y = win[a + 1] + win[b + 1];
+        }
+        acc[jp] = __builtin_elementwise_fma(gk, sm, acc[jp]);
+      }
+    }
+#pragma unroll
+    for (int jp = 0; jp < J / 2; ++jp) {
+      out[2 * jp] = acc[jp].x;
+      out[2 * jp + 1] = acc[jp].y;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      float acc = p.g[0] * win[C + j];
+#pragma unroll
+      for (int k = 1; k <= WP; ++k) acc = fmaf(p.g[k], win[C + j - k] + win[C + j + k], acc);
+      out[j] = acc;
+    }
   }
 }
 
