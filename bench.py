@@ -264,8 +264,24 @@ def bench_timeshard(args):
         eng.e_step(1.0, logz[i:i + 1])
         rounds.append(tuple(eng.carry_rounds))
 
+    warm_s, it0 = [], None
     for i in range(args.warmup):
+        t0 = time.perf_counter()
+        if i == 0:
+            t_first = KernelTimer()
+            eng.set_timer(t_first)
         em_iter(i)
+        torch.cuda.synchronize()
+        warm_s.append(time.perf_counter() - t0)
+        if i == 0:
+            eng.set_timer(None)
+            s0 = t_first.summary()
+            it0 = {"wall_s": round(warm_s[0], 4),
+                   "scans_ms": round(sum(s0[k][1] * s0[k][0] for k in ("forward_filter", "forward_repair",
+                                                                        "backward_smoother", "backward_repair")
+                                         if k in s0), 2),
+                   "kernels_ms_total": {k: round(v[1] * v[0], 3) for k, v in s0.items()},
+                   "repairs": [list(s.repairs()) for s in eng.shards]}
     torch.cuda.synchronize()
     timer = KernelTimer()
     eng.set_timer(timer)
@@ -292,7 +308,8 @@ def bench_timeshard(args):
     roof_dom = fwdbwd_roofline(summ, T_ext, L, pmc)
     t_fb = summ["forward_filter"][1] + summ["backward_smoother"][1]
     out = {
-        "metric": "EM iters/sec at N=512, T=1e5, B=512; fwd-bwd achieved HBM GB/s",
+        "metric": (f"EM iters/sec at {args.config.upper()} (N={N}, T={T}, L={L}), one recording time-sharded"
+                   if args.config != "c3" else "EM iters/sec at N=512, T=1e5, B=512; fwd-bwd achieved HBM GB/s"),
         "value": args.steps / elapsed,
         "unit": "EM iters/s",
         "n_gpus": world,
@@ -318,6 +335,8 @@ def bench_timeshard(args):
         "chunk": lays[0].chunk,
         "carry_rounds_timed": rounds[args.warmup:],
         "repairs_last": [list(s.repairs()) for s in eng.shards],
+        "first_iteration": it0,
+        "warmup_iteration_s": [round(v, 4) for v in warm_s],
         "synth_s": round(t_syn, 1),
     }
     if rank == 0:
