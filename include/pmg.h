@@ -211,6 +211,13 @@ int pmg_backward_smoother(const float* delta, const float* phi, const float* alp
 /* d = 1 rows unwritten (their values are jump_t * e_t / S_t; the backward */
 /* rebuilds them), for callers that read only P / logZ (an EM iteration). */
 #define PMG_PHASE_NO_JUMP_ROWS 4
+/* Either direction: OR PMG_PHASE_ADAPTIVE_WARMUP into the phase-1 and the  */
+/* phase-2 call of each E-step to let the device pick the warm-up: when    */
+/* more than 1/8 of a pass's chunk boundaries failed verification (a slowly */
+/* mixing chain), the next main pass of that direction on this workspace   */
+/* warms up 256 steps instead of `warmup` (decided by the relaxation kernel, */
+/* no host sync).  Phase-2 calls without it leave the decision unchanged.   */
+#define PMG_PHASE_ADAPTIVE_WARMUP 8
 int pmg_forward_filter_phase(const float* delta, const float* phi, const double* m, int64_t T,
                              const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                              int32_t warmup, double tol, float* alpha, double* logc, double* logz,

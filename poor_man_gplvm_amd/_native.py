@@ -25,6 +25,8 @@ CTL_WORDS, CTL_FWD, CTL_BWD = 32, 0, 16
 CTL_REPAIRS, CTL_ROUNDS, CTL_ERR = 0, 1, 2
 # pmg_forward_filter_phase flag: alpha's d = 1 rows are not written (PMG_PHASE_NO_JUMP_ROWS)
 PHASE_NO_JUMP_ROWS = 4
+# both phase calls of an E-step: the device lengthens the next warm-up after a cascade (PMG_PHASE_ADAPTIVE_WARMUP)
+PHASE_ADAPTIVE_WARMUP = 8
 ABI_VERSION = 1
 
 # every symbol the header declares (checked by tests/test_capi_symbols.py)

@@ -62,6 +62,7 @@ template <int J> constexpr int pf_relax_bwd() { return J >= 16 ? 2 : (J >= 8 ? 4
 // Control words at the start of the scan workspace (int32), one block per direction
 // (forward at word 0, backward at word kCtlStride):
 //   +0 chunks recomputed, +1 relaxation rounds, +2 timeout flag   (zeroed by the main pass)
+//   +3 warm-up of the next main pass (adaptive scans; written by the relaxation kernel)
 //   +4 boundaries flagged by k_verify, +5 barrier arrivals,
 //   +6..+8 segment-end changes of rounds k % 3, +9 relaxation exits
 // Words 4..9 are zero between calls: the workspace starts zero-filled and the last
@@ -70,6 +71,7 @@ enum {
   kCtlRepairs = 0,
   kCtlRounds = 1,
   kCtlErr = 2,
+  kCtlWarm = 3,
   kCtlPending = 4,
   kCtlArrive = 5,
   kCtlChanged = 6,
@@ -78,6 +80,14 @@ enum {
 };
 constexpr uint64_t kSpinTicks = 200000000ull;          // 2 s of the 100 MHz real-time clock
 constexpr int kRelaxMaxSeg = 512;                      // segment-state slots in the workspace
+// Adaptive warm-up (FBParams::adapt): when more than 1/kCascadeFrac of a pass's
+// boundaries failed (a slowly mixing chain: the nearly flat tuning of the first EM
+// iterations), the next main pass of that direction warms up kLongWarm steps instead
+// of B, which leaves mostly noise-level boundary failures (~1 chunk of repair each)
+// instead of a relaxation cascade over whole segments.  Decided on the device, so
+// no host sync and identical decisions however far the host runs ahead.
+constexpr int kLongWarm = 256;
+constexpr int kCascadeFrac = 8;
 
 struct FBParams {
   const float* delta;
@@ -120,6 +130,8 @@ struct FBParams {
   int* seg_chg;    // [2][S]
   int G, S;
   int Lpad;  // 64*J
+  // adaptive warm-up (kCtlWarm): main pass uses max(B, ctl[kCtlWarm]); relaxation writes it
+  int adapt;
   // row strides: delta and P (floats; L, or R L when R restarts' latents are stacked
   // side by side), phi (nblk or R nblk), m (1 or R)
   int ldd, ldphi, ldm;
@@ -152,6 +164,19 @@ __device__ __forceinline__ FBParams batch_view(const FBParams& p0) {
   mv(p.jsc); mv(p.chunk_logz); mv(p.s_in); mv(p.s_out); mv(p.w_first); mv(p.b_in); mv(p.b_first);
   mv(p.flags); mv(p.ctl); mv(p.seg_end); mv(p.seg_chg);
   return p;
+}
+
+// this main pass's warm-up: B, or the longer one the last relaxation of this direction
+// asked for (adaptive scans)
+__device__ __forceinline__ int64_t main_warmup(const FBParams& p) {
+  if (!p.adapt) return p.B;
+  const int w = __builtin_amdgcn_readfirstlane(p.ctl[kCtlWarm]);
+  return w > p.B ? w : p.B;
+}
+
+// the relaxation's warm-up decision for the next main pass (s == 0, lane 0)
+__device__ __forceinline__ void relax_warm_decision(const FBParams& p, int pending) {
+  if (p.adapt) p.ctl[kCtlWarm] = (pending * kCascadeFrac > p.M) ? kLongWarm : 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -621,7 +646,7 @@ __device__ __forceinline__ void forward_chunk(const FBParams& p, int c, int j0, 
   const int64_t t_c = (int64_t)c * p.C;
   const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
   Fwd<J, WP> st;
-  int64_t t0 = (c == 0) ? 0 : t_c - p.B;
+  int64_t t0 = (c == 0) ? 0 : t_c - main_warmup(p);
   if (t0 < 0) t0 = 0;
   st.init_uniform(p, j0);
   fwd_stream<J, WP, kPfFwd, VEC, false>(p, st, j0, invz, t0, t_c);
@@ -782,7 +807,8 @@ __device__ __forceinline__ void forward_relax(const FBParams& p, int j0, const f
   const int a = s * p.G;
   const int b = a + p.G < p.M ? a + p.G : p.M;
   int nrep = 0, rounds = 0;
-  if (ctl_load(p.ctl, kCtlPending) > 0) {
+  const int pending = ctl_load(p.ctl, kCtlPending);
+  if (pending > 0) {
     Fwd<J, WP> st;
     bool changed = false;
     // round 0: every boundary the verification flagged (it stored the carry into s_in),
@@ -820,6 +846,7 @@ __device__ __forceinline__ void forward_relax(const FBParams& p, int j0, const f
     if (lane == 0) {
       p.logz[0] = lz;
       p.ctl[kCtlRounds] = rounds;
+      relax_warm_decision(p, pending);
     }
   }
 }
@@ -1067,7 +1094,7 @@ __device__ __forceinline__ void backward_chunk(const FBParams& p, int c, int j0,
   bool has_prev = false;
   st.init_ones(p, j0);
   if (c < p.M - 1) {
-    int64_t t_w = t_e + p.B;  // beta guess (ones) at t_w, exact when t_w is the last bin
+    int64_t t_w = t_e + main_warmup(p);  // beta guess (ones) at t_w, exact when t_w is the last bin
     if (t_w > p.T - 1) t_w = p.T - 1;
     bwd_stream_warm<J, WP, kPfBwdWarm, VEC>(p, st, j0, invz, t_w, t_e + 1);
     st.save_state(p, p.b_in + (size_t)c * SZ, j0);  // beta_{t_e}: the start k_verify checks
@@ -1153,7 +1180,8 @@ __device__ __forceinline__ void backward_relax(const FBParams& p, int j0, const 
   const int b = a + p.G < p.M ? a + p.G : p.M;
   const int top = b < p.M - 1 ? b : p.M - 1;  // boundaries c <= M-2 have a successor
   int nrep = 0, rounds = 0;
-  if (ctl_load(p.ctl, kCtlPending) > 0) {
+  const int pending = ctl_load(p.ctl, kCtlPending);
+  if (pending > 0) {
     Bwd<J, WP> st;
     bool changed = false;
     // round 0: every flagged boundary, top down (see forward_relax)
@@ -1186,7 +1214,10 @@ __device__ __forceinline__ void backward_relax(const FBParams& p, int j0, const 
   }
   if (lane == 0) {
     if (nrep) atomicAdd(p.ctl + kCtlRepairs, nrep);
-    if (s == 0) p.ctl[kCtlRounds] = rounds;
+    if (s == 0) {
+      p.ctl[kCtlRounds] = rounds;
+      relax_warm_decision(p, pending);
+    }
   }
 }
 

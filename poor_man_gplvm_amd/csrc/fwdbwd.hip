@@ -171,6 +171,7 @@ static int fill_params(FBParams& p, const pmg_transition* tr, int64_t T, int C, 
   p.ldphi = p.nblk;
   p.ldm = 1;
   p.ws_stride = 0;
+  p.adapt = 0;
   for (int k = 0; k <= kMaxBand; ++k) p.g[k] = (k <= tr->band) ? tr->g[k] : 0.f;
   return PMG_OK;
 }
@@ -262,6 +263,7 @@ static int forward_impl(const float* delta, const float* phi, const double* m, i
   p.chunk_logz = w.chunk_logz;
   p.jsc = w.jsc;
   p.a1_bytes = (phase & 4) ? 0u : (uint32_t)p.L * 4u;
+  p.adapt = (phase & PMG_PHASE_ADAPTIVE_WARMUP) ? 1 : 0;
   p.s_in = w.s_in;
   p.s_out = w.s_out;
   p.flags = w.flags;
@@ -307,7 +309,8 @@ int pmg_forward_filter_phase(const float* delta, const float* phi, const double*
                              const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                              int32_t warmup, double tol, float* alpha, double* logc, double* logz,
                              void* workspace, size_t workspace_bytes, void* stream, int32_t phase) {
-  PMG_REQUIRE((phase & 3) != 0 && (phase & ~7) == 0, "pmg_forward_filter_phase: phase %d", phase);
+  PMG_REQUIRE((phase & 3) != 0 && (phase & ~(7 | PMG_PHASE_ADAPTIVE_WARMUP)) == 0, "pmg_forward_filter_phase: phase %d",
+              phase);
   return forward_impl(delta, phi, m, T, tr, likelihood_scale, chunk, warmup, tol, alpha, logc, logz,
                       workspace, workspace_bytes, stream, phase);
 }
@@ -333,6 +336,7 @@ static int backward_impl(const float* delta, const float* phi, const float* alph
   p.P = P;
   p.gamma = gamma;
   p.rho = rho;
+  p.adapt = (phase & PMG_PHASE_ADAPTIVE_WARMUP) ? 1 : 0;
   p.b_in = w.b_in;
   p.b_first = w.b_first;
   p.flags = w.flags;
@@ -376,7 +380,8 @@ int pmg_backward_smoother_phase(const float* delta, const float* phi, const floa
                                 const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                                 int32_t warmup, double tol, float* P, float* gamma, float* rho,
                                 void* workspace, size_t workspace_bytes, void* stream, int32_t phase) {
-  PMG_REQUIRE(phase >= 1 && phase <= 3, "pmg_backward_smoother_phase: phase %d", phase);
+  PMG_REQUIRE((phase & 3) != 0 && (phase & ~(3 | PMG_PHASE_ADAPTIVE_WARMUP)) == 0,
+              "pmg_backward_smoother_phase: phase %d", phase);
   return backward_impl(delta, phi, alpha, T, tr, likelihood_scale, chunk, warmup, tol, P, gamma, rho,
                        workspace, workspace_bytes, stream, phase);
 }
@@ -391,7 +396,8 @@ int pmg_forward_filter_batched(const float* delta, const float* phi, const doubl
                                const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                                int32_t warmup, double tol, float* alpha, double* logc, double* logz,
                                void* workspace, size_t workspace_bytes, void* stream, int32_t phase) {
-  PMG_REQUIRE((phase & 3) != 0 && (phase & ~7) == 0, "pmg_forward_filter_batched: phase %d", phase);
+  PMG_REQUIRE((phase & 3) != 0 && (phase & ~(7 | PMG_PHASE_ADAPTIVE_WARMUP)) == 0,
+              "pmg_forward_filter_batched: phase %d", phase);
   return forward_impl(delta, phi, m, T, tr, likelihood_scale, chunk, warmup, tol, alpha, logc, logz,
                       workspace, workspace_bytes, stream, phase, R);
 }
@@ -400,7 +406,8 @@ int pmg_backward_smoother_batched(const float* delta, const float* phi, const fl
                                   const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                                   int32_t warmup, double tol, float* P, float* gamma, void* workspace,
                                   size_t workspace_bytes, void* stream, int32_t phase) {
-  PMG_REQUIRE(phase >= 1 && phase <= 3, "pmg_backward_smoother_batched: phase %d", phase);
+  PMG_REQUIRE((phase & 3) != 0 && (phase & ~(3 | PMG_PHASE_ADAPTIVE_WARMUP)) == 0,
+              "pmg_backward_smoother_batched: phase %d", phase);
   return backward_impl(delta, phi, alpha, T, tr, likelihood_scale, chunk, warmup, tol, P, gamma, nullptr,
                        workspace, workspace_bytes, stream, phase, R);
 }

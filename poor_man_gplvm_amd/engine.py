@@ -67,6 +67,9 @@ class ScanConfig:
     max_warmup: int = 1024
     min_warmup: int = 16
     chunk_bwd: int | None = None  # backward chunk (None: = chunk if set, else 2x the default)
+    device_adaptive: bool = True  # PMG_PHASE_ADAPTIVE_WARMUP: after a pass where > 1/8 of the chunk
+                                  # boundaries failed (the first EM iterations), the next main pass
+                                  # of that direction warms up 256 steps (device-side decision)
 
     def chunk_for(self, T):
         if self.chunk:
@@ -545,10 +548,11 @@ class DeviceEM:
                 nat.ptr(self.logc), nat.ptr(logz_out), nat.ptr(self.ws_fb), self.ws_fb.numel(),
                 nat.stream_handle())
         self.alpha_bits = 0 if keep_alpha else nat.PHASE_NO_JUMP_ROWS
+        ad = nat.PHASE_ADAPTIVE_WARMUP if sc.device_adaptive else 0
         with self._t('forward_filter'):          # main chunk-parallel pass (k_forward)
-            nat.check(self.lib.pmg_forward_filter_phase(*args, 1 | self.alpha_bits), "pmg_forward_filter")
+            nat.check(self.lib.pmg_forward_filter_phase(*args, 1 | ad | self.alpha_bits), "pmg_forward_filter")
         with self._t('forward_repair'):          # verify / relaxation / logZ
-            nat.check(self.lib.pmg_forward_filter_phase(*args, 2 | self.alpha_bits), "pmg_forward_filter")
+            nat.check(self.lib.pmg_forward_filter_phase(*args, 2 | ad | self.alpha_bits), "pmg_forward_filter")
 
     def backward(self, likelihood_scale, P=True, gamma=None, rho=None, log_gamma=None):
         """rho: the joint partner; with the dense scans it is written as log(rho)
@@ -568,10 +572,11 @@ class DeviceEM:
                 float(likelihood_scale), self.Cb, int(self.warm[1]), float(sc.tol),
                 nat.ptr(self.P) if P else None, nat.ptr(gamma), nat.ptr(rho), nat.ptr(self.ws_fb),
                 self.ws_fb.numel(), nat.stream_handle())
+        ad = nat.PHASE_ADAPTIVE_WARMUP if sc.device_adaptive else 0
         with self._t('backward_smoother'):       # main chunk-parallel pass (k_backward)
-            nat.check(self.lib.pmg_backward_smoother_phase(*args, 1), "pmg_backward_smoother")
+            nat.check(self.lib.pmg_backward_smoother_phase(*args, 1 | ad), "pmg_backward_smoother")
         with self._t('backward_repair'):         # verify / relaxation
-            nat.check(self.lib.pmg_backward_smoother_phase(*args, 2), "pmg_backward_smoother")
+            nat.check(self.lib.pmg_backward_smoother_phase(*args, 2 | ad), "pmg_backward_smoother")
 
     def e_step(self, likelihood_scale, logz_out, gamma=None, rho=None, log_gamma=None, keep_alpha=None):
         """keep_alpha (default: whenever a posterior output is requested): write alpha in full."""
@@ -796,7 +801,8 @@ class RestartBatchEM:
 
     def forward(self, likelihood_scale, logz_out, keep_alpha=True):
         """logz_out: (R,) f64 device tensor."""
-        bits = 0 if keep_alpha else nat.PHASE_NO_JUMP_ROWS
+        bits = (0 if keep_alpha else nat.PHASE_NO_JUMP_ROWS) | (nat.PHASE_ADAPTIVE_WARMUP if self.scan.device_adaptive
+                                                                  else 0)
         args = (nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.mref), self.T, self.R,
                 ctypes.byref(self._tr_c), float(likelihood_scale), self.C, int(self.warm[0]), float(self.scan.tol),
                 nat.ptr(self.alpha), nat.ptr(self.logc), nat.ptr(logz_out), nat.ptr(self.ws_fb),
@@ -811,10 +817,11 @@ class RestartBatchEM:
         args = (nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.alpha), self.T, self.R,
                 ctypes.byref(self._tr_c), float(likelihood_scale), self.Cb, int(self.warm[1]), float(self.scan.tol),
                 nat.ptr(self.P), nat.ptr(gamma), nat.ptr(self.ws_fb), self.ws_fb.numel(), nat.stream_handle())
+        ad = nat.PHASE_ADAPTIVE_WARMUP if self.scan.device_adaptive else 0
         with self._t('backward_smoother'):
-            nat.check(self.lib.pmg_backward_smoother_batched(*args, 1), "pmg_backward_smoother_batched")
+            nat.check(self.lib.pmg_backward_smoother_batched(*args, 1 | ad), "pmg_backward_smoother_batched")
         with self._t('backward_repair'):
-            nat.check(self.lib.pmg_backward_smoother_batched(*args, 2), "pmg_backward_smoother_batched")
+            nat.check(self.lib.pmg_backward_smoother_batched(*args, 2 | ad), "pmg_backward_smoother_batched")
 
     def e_step(self, likelihood_scale, logz_out, gamma=None):
         self.emission(likelihood_scale)
