@@ -153,7 +153,7 @@ def test_forward_backward_vs_oracle(case):
     if want_joint:
         S = eng.joint(rho).cpu().numpy().reshape(2, L, 2, L).transpose(0, 2, 1, 3)
         J = np.exp(logA)[:, :, None, None] * K[None] * S
-        np.testing.assert_allclose(J, np.exp(lj), rtol=1e-4, atol=1e-5 * max(1.0, np.exp(lj).max()))
+        np.testing.assert_allclose(J, np.exp(lj), rtol=1e-5, atol=1e-5 * max(1.0, np.exp(lj).max()))
 
 
 def test_flat_tuning_cascade():
@@ -414,8 +414,9 @@ def test_decode_latent_golden(name):
     np.testing.assert_allclose(r['log_marginal_final'], float(f['log_marginal_final']), rtol=1e-7)
     np.testing.assert_allclose(r['log_one_step_predictive_marginals_all'], f['log_one_step'], rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(r['log_likelihood_all'], f['log_likelihood_all'], rtol=2e-7, atol=1e-5)
+    # measured (tools/diag_joint_tol.py): <= 7.2e-7 relative on every entry above 1e-7
     for k in ['p_transition_latent', 'p_transition_dynamics', 'p_joint_dynamics', 'p_joint_latent']:
-        np.testing.assert_allclose(r[k], f[k], rtol=1e-4, atol=1e-7)
+        np.testing.assert_allclose(r[k], f[k], rtol=1e-5, atol=1e-12)
 
 
 # ----------------------------------------------------------------------------- naive Bayes
@@ -475,14 +476,20 @@ def test_latent_only_decode_vs_oracle(masked):
     assert abs(res['log_marginal_final'] - lz) <= 1e-7 * abs(lz)
     np.testing.assert_allclose(res['log_one_step_predictive_marginals_all'], cs, rtol=1e-6, atol=1e-5)
     ref = O.compute_transition_posterior_prob_latent(lj)
-    np.testing.assert_allclose(res['p_joint_latent'], ref['p_joint_latent'], rtol=1e-4,
-                               atol=1e-5 * ref['p_joint_latent'].max())
-    # row-conditional transitions: rows the posterior visits (joint row mass > 1e-6);
-    # a nearly unvisited row is a ratio of two tiny f32-rounded sums
+    np.testing.assert_allclose(res['p_joint_latent'], ref['p_joint_latent'], rtol=1e-5, atol=1e-12)
+    # row-conditional transitions, every kept row: 1e-5 on the rows the posterior visits
+    # (joint row mass > 1e-6).  A row it (almost) never visits is a ratio of two sums of
+    # joint entries that are themselves below ~1e-6 of the total, each an f32
+    # log-sum-exp of the dense scan's log states; there the measured error is up to
+    # 5.8e-5 relative (masked case, r02j), so those rows are held to 1e-4.
     keep = np.ones(L, bool) if ml is None else ml.astype(bool)
-    rows = keep & (ref['p_joint_latent'].sum(1) > 1e-6)
-    np.testing.assert_allclose(res['p_transition_latent'][np.ix_(rows, keep)],
-                               ref['p_transition_latent'][np.ix_(rows, keep)], rtol=1e-4, atol=1e-6)
+    vis = keep & (ref['p_joint_latent'].sum(1) > 1e-6)
+    rare = keep & ~vis
+    np.testing.assert_allclose(res['p_transition_latent'][np.ix_(vis, keep)],
+                               ref['p_transition_latent'][np.ix_(vis, keep)], rtol=1e-5, atol=1e-12)
+    np.testing.assert_allclose(res['p_transition_latent'][np.ix_(rare, keep)],
+                               ref['p_transition_latent'][np.ix_(rare, keep)], rtol=1e-4, atol=1e-12)
+    assert all(np.all(np.isfinite(res[k])) for k in res if k.startswith(('p_', 'log_joint', 'log_transition')))
 
 
 def test_latent_only_fit_em_one_iteration_vs_oracle():
