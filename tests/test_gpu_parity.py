@@ -378,7 +378,7 @@ def test_fit_em_fixed_iterations_golden():
 def test_fit_em_stop_rule_golden():
     f, res = _fit_fixture('em_small_stoprule.npz')
     assert res['m_step_res_l']['n_iter'] == list(f['m_n_iter'])
-    np.testing.assert_allclose(res['tuning'], f['tuning'], rtol=1e-4)
+    np.testing.assert_allclose(res['tuning'], f['tuning'], rtol=1e-5)     # measured 2.0e-6 (r02j)
     argmax_match(res['posterior_latent_marg'], f['posterior'].sum(1))
     np.testing.assert_allclose(res['log_marginal_l'], f['log_marginal_l'], rtol=1e-6)
 
