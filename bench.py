@@ -392,6 +392,7 @@ def main():
     scan = ScanConfig(chunk=args.chunk or None, warmup=args.warm_steps, chunk_bwd=args.chunk_bwd or None)
     sp = SpikeData(y)
     eng = DeviceEM(sp, L, basis=B, scan=scan)
+    eng.adaptive = True          # as run_em: adaptive warm-up across the fit's E-steps
     eng.set_transition(banded_transition(L, 1.0, 0.01, 0.01))
     adam = AdamConfig(lr=0.01, maxiter=1000, tol=1e-6, prior_std=1.0)
     W = torch.empty((B.shape[1], N), dtype=torch.float64, device=dev)
@@ -406,6 +407,7 @@ def main():
     def fresh_fit():
         """Reset to the start of a fit: the initial posterior, W init, Adam state 0."""
         eng.set_log_posterior(lp0)
+        eng.reset_adaptive()
         W.copy_(torch.as_tensor(W0.astype(np.float64), device=dev))
         mu.zero_()
         nu.zero_()
@@ -550,6 +552,7 @@ def bench_restarts(args):
 
     def fresh():
         eng.set_log_posterior(lps)
+        eng.reset_adaptive()
         W.copy_(torch.as_tensor(np.broadcast_to(W0.astype(np.float64), (R, NB, N)).copy(), device=dev))
         mu.zero_(); nu.zero_(); cnt.zero_()
 
@@ -591,6 +594,7 @@ def bench_restarts(args):
     del eng
     # the same restarts on the one-restart engine, one after another
     one = DeviceEM(sp, L, basis=B, scan=ScanConfig(warmup=args.warm_steps))
+    one.adaptive = True
     one.set_transition(tr)
     W1 = torch.empty((NB, N), dtype=torch.float64, device=dev)
     mu1, nu1 = torch.zeros_like(W1), torch.zeros_like(W1)
@@ -604,6 +608,7 @@ def bench_restarts(args):
     for r in range(n_seq):
         def fresh1(r=r):
             one.set_log_posterior(lps[r])
+            one.reset_adaptive()
             W1.copy_(torch.as_tensor(W0.astype(np.float64), device=dev))
             mu1.zero_(); nu1.zero_(); cnt1.zero_()
 

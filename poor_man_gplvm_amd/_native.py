@@ -22,7 +22,7 @@ STATE_FWD_IN, STATE_FWD_OUT, STATE_BWD_IN, STATE_BWD_FIRST = 0, 1, 2, 3
 # int32 control words at the start of a pmg_fwdbwd workspace (fb_kernels.h kCtl*):
 # a forward block and a backward block, each {chunks recomputed, relaxation rounds, timeout}
 CTL_WORDS, CTL_FWD, CTL_BWD = 32, 0, 16
-CTL_REPAIRS, CTL_ROUNDS, CTL_ERR = 0, 1, 2
+CTL_REPAIRS, CTL_ROUNDS, CTL_ERR, CTL_WARM = 0, 1, 2, 3
 # pmg_forward_filter_phase flag: alpha's d = 1 rows are not written (PMG_PHASE_NO_JUMP_ROWS)
 PHASE_NO_JUMP_ROWS = 4
 # both phase calls of an E-step: the device lengthens the next warm-up after a cascade (PMG_PHASE_ADAPTIVE_WARMUP)

@@ -633,6 +633,7 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
     ma = None if ma_neuron is None else np.asarray(ma_neuron, np.float32)
     sp = SpikeData(y, ma)
     eng = DeviceEM(sp, L, basis=B, scan=scan)
+    eng.adaptive = True          # adaptive warm-up across this fit's E-steps
     eng.set_transition(transition)
     eng.set_ma_latent(ma_latent)
     if noise_std is not None:

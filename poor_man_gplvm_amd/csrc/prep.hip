@@ -80,22 +80,46 @@ __global__ void k_tuning_softplus(const float* __restrict__ basis, const double*
   if (t32) t32[row * N + n] = (float)f;
 }
 
-// one thread per (t, group): R groups of nb = nblk / R blocks each (batched restarts'
-// stacked latents; R = 1: the whole row), m (T, R), phi (T, nblk)
-__global__ void k_rowref(const double* __restrict__ rblk, int64_t T, int nblk, int R, double s,
-                         float* __restrict__ phi, double* __restrict__ m) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= T * R) return;
+// Row references: per (t, group) the max over the group's nb = nblk / R blocks (R groups
+// = batched restarts' stacked latents; R = 1: the whole row) -> m (T, R), and
+// phi[t, b] = s (rblk[t, b] - m).  A (t, group) row occupies NBP = pow2 >= nb lanes, so a
+// wave handles 64 / NBP rows with coalesced loads / stores and a segmented shuffle max
+// (one thread per row, as before, read 16 strided f64 per thread: ~21 us at C3).
+template <int NBP>
+__global__ void __launch_bounds__(256) k_rowref(const double* __restrict__ rblk, int64_t T, int nblk, int R,
+                                                double s, float* __restrict__ phi, double* __restrict__ m) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * (64 / NBP) + lane / NBP;
+  const int b = lane % NBP;
   const int nb = nblk / R;
-  const int64_t t = i / R;
-  const int g = (int)(i - t * R);
-  const double* r = rblk + t * nblk + (int64_t)g * nb;
-  double mx = -INFINITY;
-  for (int b = 0; b < nb; ++b) mx = fmax(mx, r[b]);
+  const bool live = row < T * R && b < nb;
+  const int64_t t = live ? row / R : 0;
+  const int g = live ? (int)(row - t * R) : 0;
+  const int64_t o = t * nblk + (int64_t)g * nb + b;
+  const double v = live ? rblk[o] : -INFINITY;
+  double mx = v;
+#pragma unroll
+  for (int d = 1; d < NBP; d <<= 1) mx = fmax(mx, __shfl_xor(mx, d, 64));
   if (mx == -INFINITY) mx = 0.0;  // cannot happen for L >= 1 (masked latents are -1e20)
-  m[i] = mx;
-  float* ph = phi + t * nblk + (int64_t)g * nb;
-  for (int b = 0; b < nb; ++b) ph[b] = (float)(s * (r[b] - mx));
+  if (live) {
+    phi[o] = (float)(s * (v - mx));
+    if (b == 0) m[row] = mx;
+  }
+}
+
+static void launch_rowref(const double* rblk, int64_t T, int nblk, int R, double s, float* phi, double* m,
+                          hipStream_t st) {
+  const int nb = nblk / R;
+  const int64_t rows = T * R;
+#define PMG_RR(NBP)                                                                                  \
+  if (nb <= NBP) {                                                                                   \
+    const int64_t waves = (rows + (64 / NBP) - 1) / (64 / NBP);                                      \
+    hipLaunchKernelGGL(k_rowref<NBP>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, rblk, T, nblk, R, s, \
+                       phi, m);                                                                      \
+    return;                                                                                          \
+  }
+  PMG_RR(1) PMG_RR(2) PMG_RR(4) PMG_RR(8) PMG_RR(16) PMG_RR(32) PMG_RR(64)
+#undef PMG_RR
 }
 
 __global__ void k_loglik(const float* __restrict__ delta, const double* __restrict__ rblk,
@@ -180,8 +204,8 @@ int pmg_tuning_softplus_batched(const float* basis, const double* W, int32_t L, 
 int pmg_emission_rowref(const double* rblk, int64_t T, int32_t nblk, double likelihood_scale,
                         float* phi, double* m, void* stream) {
   PMG_REQUIRE(T > 0 && nblk > 0 && rblk && phi && m, "pmg_emission_rowref: bad args");
-  hipLaunchKernelGGL(k_rowref, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
-                     as_stream(stream), rblk, T, nblk, 1, likelihood_scale, phi, m);
+  PMG_REQUIRE(nblk <= 64, "pmg_emission_rowref: nblk=%d > 64", nblk);
+  launch_rowref(rblk, T, nblk, 1, likelihood_scale, phi, m, as_stream(stream));
   PMG_LAUNCH_CHECK();
   return PMG_OK;
 }
@@ -190,8 +214,8 @@ int pmg_emission_rowref_batched(const double* rblk, int64_t T, int32_t nblk, int
                                 float* phi, double* m, void* stream) {
   PMG_REQUIRE(T > 0 && nblk > 0 && R > 0 && nblk % R == 0 && rblk && phi && m,
               "pmg_emission_rowref_batched: bad args (nblk=%d, R=%d)", nblk, R);
-  hipLaunchKernelGGL(k_rowref, dim3((unsigned)((T * R + 255) / 256)), dim3(256), 0,
-                     as_stream(stream), rblk, T, nblk, R, likelihood_scale, phi, m);
+  PMG_REQUIRE(nblk / R <= 64, "pmg_emission_rowref_batched: %d blocks per restart > 64", nblk / R);
+  launch_rowref(rblk, T, nblk, R, likelihood_scale, phi, m, as_stream(stream));
   PMG_LAUNCH_CHECK();
   return PMG_OK;
 }

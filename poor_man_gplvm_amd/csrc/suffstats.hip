@@ -378,13 +378,27 @@ __global__ void __launch_bounds__(512) k_ptb3(const float* __restrict__ P, int L
 #undef PMG_SS_TILE
 }
 
-__global__ void k_tw_reduce(const double* __restrict__ twpart, int nKS, int Mp, int L,
-                            double* __restrict__ tw) {
-  const int m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= L) return;
+// t_w[m] = sum over the 4 nKS partial rows, in one fixed order: block = 64 latents x
+// 16 k-groups (group g sums rows k = g, g + 16, ... in k order, coalesced over m), then
+// the 16 group sums in g order through LDS.  (One thread per latent summing every row
+// put L threads, i.e. 8 waves, on the whole chip: ~16 us at C3.)
+constexpr int kTwM = 64, kTwG = 16;
+__global__ void __launch_bounds__(kTwM * kTwG) k_tw_reduce(const double* __restrict__ twpart, int nKS, int Mp,
+                                                           int L, double* __restrict__ tw) {
+  __shared__ double sp[kTwG][kTwM];
+  const int mi = threadIdx.x % kTwM, g = threadIdx.x / kTwM;
+  const int m = blockIdx.x * kTwM + mi;
   double s = 0.0;
-  for (int k = 0; k < 4 * nKS; ++k) s += twpart[(size_t)k * Mp + m];
-  tw[m] = s;
+  if (m < L)
+    for (int k = g; k < 4 * nKS; k += kTwG) s += twpart[(size_t)k * Mp + m];
+  sp[g][mi] = s;
+  __syncthreads();
+  if (g == 0 && m < L) {
+    double t = 0.0;
+#pragma unroll
+    for (int q = 0; q < kTwG; ++q) t += sp[q][mi];
+    tw[m] = t;
+  }
 }
 
 // yext (T, Np) f32 -> ybt (Np, Tp) bf16 bits (truncation; exact for integers <= 256),
@@ -495,7 +509,7 @@ int pmg_suffstats_bf16(const float* P, const uint16_t* ybt, int64_t T, int64_t T
   hipLaunchKernelGGL(k_atb_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
                      (const double*)part, nKS, Mp, Npd, L, N, N, yw, -1, (double*)nullptr);
   PMG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_tw_reduce, dim3((unsigned)((L + 255) / 256)), dim3(256), 0, st,
+  hipLaunchKernelGGL(k_tw_reduce, dim3((unsigned)((L + kTwM - 1) / kTwM)), dim3(kTwM * kTwG), 0, st,
                      (const double*)twpart, nKS, Mp, L, tw);
   PMG_LAUNCH_CHECK();
   return PMG_OK;

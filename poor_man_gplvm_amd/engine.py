@@ -271,6 +271,9 @@ class DeviceEM:
         self.ws_dense = None
         self.log_alpha = None       # (T, 2, L) log filter state (dense scans)
         self.alpha_bits = 0         # phase bits of the last forward (PHASE_NO_JUMP_ROWS or 0)
+        # device-side adaptive warm-up across the E-steps of ONE fit (run_em sets it; a
+        # decode is a single E-step whose result must not depend on earlier calls)
+        self.adaptive = False
         self.ma_latent = None
         # Gaussian observation model (GaussianGPLVMJump1D): when noise_std is set, the
         # emission, tuning and M-step dispatch to gaussian.hip; the scans are shared.
@@ -525,6 +528,13 @@ class DeviceEM:
         ws = self.ws_dense if self.dense else self.ws_fb
         return ws[:4 * nat.CTL_WORDS].view(torch.int32)
 
+    def reset_adaptive(self):
+        """Start of a fit: forget the adaptive warm-up decisions of earlier E-steps (the
+        kCtlWarm words of both directions)."""
+        w = self.ws_fb[:4 * nat.CTL_WORDS].view(torch.int32)
+        w[nat.CTL_FWD + nat.CTL_WARM] = 0
+        w[nat.CTL_BWD + nat.CTL_WARM] = 0
+
     def _snapshot_repairs(self):
         self._rep_host.copy_(self.ctl_words(), non_blocking=True)
         self._rep_evt = torch.cuda.Event()
@@ -548,7 +558,7 @@ class DeviceEM:
                 nat.ptr(self.logc), nat.ptr(logz_out), nat.ptr(self.ws_fb), self.ws_fb.numel(),
                 nat.stream_handle())
         self.alpha_bits = 0 if keep_alpha else nat.PHASE_NO_JUMP_ROWS
-        ad = nat.PHASE_ADAPTIVE_WARMUP if sc.device_adaptive else 0
+        ad = nat.PHASE_ADAPTIVE_WARMUP if (sc.device_adaptive and self.adaptive) else 0
         with self._t('forward_filter'):          # main chunk-parallel pass (k_forward)
             nat.check(self.lib.pmg_forward_filter_phase(*args, 1 | ad | self.alpha_bits), "pmg_forward_filter")
         with self._t('forward_repair'):          # verify / relaxation / logZ
@@ -572,7 +582,7 @@ class DeviceEM:
                 float(likelihood_scale), self.Cb, int(self.warm[1]), float(sc.tol),
                 nat.ptr(self.P) if P else None, nat.ptr(gamma), nat.ptr(rho), nat.ptr(self.ws_fb),
                 self.ws_fb.numel(), nat.stream_handle())
-        ad = nat.PHASE_ADAPTIVE_WARMUP if sc.device_adaptive else 0
+        ad = nat.PHASE_ADAPTIVE_WARMUP if (sc.device_adaptive and self.adaptive) else 0
         with self._t('backward_smoother'):       # main chunk-parallel pass (k_backward)
             nat.check(self.lib.pmg_backward_smoother_phase(*args, 1 | ad), "pmg_backward_smoother")
         with self._t('backward_repair'):         # verify / relaxation
@@ -802,7 +812,7 @@ class RestartBatchEM:
     def forward(self, likelihood_scale, logz_out, keep_alpha=True):
         """logz_out: (R,) f64 device tensor."""
         bits = (0 if keep_alpha else nat.PHASE_NO_JUMP_ROWS) | (nat.PHASE_ADAPTIVE_WARMUP if self.scan.device_adaptive
-                                                                  else 0)
+                                                                  else 0)   # RestartBatchEM: always one fit
         args = (nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.mref), self.T, self.R,
                 ctypes.byref(self._tr_c), float(likelihood_scale), self.C, int(self.warm[0]), float(self.scan.tol),
                 nat.ptr(self.alpha), nat.ptr(self.logc), nat.ptr(logz_out), nat.ptr(self.ws_fb),
@@ -831,6 +841,13 @@ class RestartBatchEM:
     def ctl_words(self, r):
         """Restart r's scan control words (device view)."""
         return self.ws_fb[r * self.slab:r * self.slab + 4 * nat.CTL_WORDS].view(torch.int32)
+
+    def reset_adaptive(self):
+        """Start of a fit: forget earlier adaptive warm-up decisions (every restart)."""
+        for r in range(self.R):
+            w = self.ctl_words(r)
+            w[nat.CTL_FWD + nat.CTL_WARM] = 0
+            w[nat.CTL_BWD + nat.CTL_WARM] = 0
 
     def repairs(self):
         """[(forward, backward) chunks recomputed] per restart (device read: syncs)."""

@@ -422,6 +422,7 @@ class TimeShardedEM:
                                       "have no carry hand-off yet)")
         self.shards = [ShardEM(lay, y, self.L, B, scan, ma_neuron, device) for lay in self.lays]
         for s in self.shards:
+            s.adaptive = True       # one fit: adaptive warm-up across its E-steps
             s.set_transition(transition)
             s.set_ma_latent(ma_latent)
         self.dev = self.shards[0].dev
