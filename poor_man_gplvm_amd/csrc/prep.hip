@@ -73,8 +73,18 @@ __global__ void k_tuning_softplus(const float* __restrict__ basis, const double*
   W += r * NB * (int64_t)N;
   const int64_t row = r * L + l;
   const float* br = basis + (int64_t)l * NB;
-  double acc = 0.0;
-  for (int k = 0; k < NB; ++k) acc = fma((double)br[k], W[(int64_t)k * N + n], acc);
+  // four interleaved partial sums (the f64 FMA chain, not the loads, bounded the single
+  // accumulator), combined in a fixed order
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  int k = 0;
+  for (; k + 4 <= NB; k += 4) {
+    a0 = fma((double)br[k], W[(int64_t)k * N + n], a0);
+    a1 = fma((double)br[k + 1], W[(int64_t)(k + 1) * N + n], a1);
+    a2 = fma((double)br[k + 2], W[(int64_t)(k + 2) * N + n], a2);
+    a3 = fma((double)br[k + 3], W[(int64_t)(k + 3) * N + n], a3);
+  }
+  for (; k < NB; ++k) a0 = fma((double)br[k], W[(int64_t)k * N + n], a0);
+  const double acc = (a0 + a1) + (a2 + a3);
   double f = softplus_d(acc);
   if (t64) t64[row * N + n] = f;
   if (t32) t32[row * N + n] = (float)f;
