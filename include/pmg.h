@@ -84,7 +84,12 @@ int pmg_tuning_softplus_batched(const float* basis, const double* W, int32_t L, 
 /* Integer path (flags == 0, 1-D or no mask): exact int8 MFMA            */
 /* (v_mfma_i32_32x32x32_i8) on y and log(lam) in 5 balanced base-256     */
 /* digits of a 2^-32 fixed point (5 digits).  Generic path: f64.         */
+/* The workspace must be zero-filled before its first use: it holds a    */
+/* sticky int32 range flag (pmg_emission_range_flag) that the integer    */
+/* path ORs to 1 when some |log lam| >= 60 (outside the digit range);    */
+/* the caller reads and clears it (no per-call memset).                  */
 size_t pmg_emission_workspace_size(int64_t T, int32_t L, int32_t N);
+int32_t* pmg_emission_range_flag(void* workspace, int64_t T, int32_t L, int32_t N);
 int pmg_emission_poisson(const int8_t* yq, const double* gconst, const double* tuning64,
                          const float* ma_neuron_1d, const uint8_t* ma_latent, double dt,
                          int64_t T, int32_t L, int32_t N, int32_t Kp, float* delta,

@@ -48,6 +48,7 @@ EXPORTED_SYMBOLS = (
     "pmg_tuning_softplus_batched", "pmg_emission_rowref_batched", "pmg_fwdbwd_batched_workspace_size",
     "pmg_forward_filter_batched", "pmg_backward_smoother_batched",
     "pmg_mstep_batched_workspace_size", "pmg_mstep_adam_batched_supported", "pmg_mstep_adam_batched",
+    "pmg_emission_range_flag",
 )
 
 
@@ -138,6 +139,7 @@ _SIGS = {
     "pmg_joint_log_accumulate": ([_P, _P, _I64, _I32, _P, _P], _I32),
     "pmg_joint_accumulate": ([_P, _P, _I64, _I32, _P, _P, _SZ, _P], _I32),
     "pmg_tuning_softplus_batched": ([_P, _P, _I32, _I32, _I32, _I32, _P, _P, _P], _I32),
+    "pmg_emission_range_flag": ([_P, _I64, _I32, _I32], _P),
     "pmg_mstep_batched_workspace_size": ([_I32, _I32, _I32, _I32, _I32], _SZ),
     "pmg_mstep_adam_batched_supported": ([_I32, _I32, _I32, _I32], ctypes.c_int),
     "pmg_mstep_adam_batched": ([_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, ctypes.POINTER(AdamCfg),

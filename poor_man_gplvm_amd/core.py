@@ -244,6 +244,8 @@ class PoissonGPLVMJump1D:
         rho = torch.zeros((T, 2, L), dtype=torch.float32, device=dev) if joint else None
         lgam = torch.empty((T, 2, L), dtype=torch.float32, device=dev) if eng.dense else None
         eng.e_step(likelihood_scale, logz, gamma=gamma, rho=rho, log_gamma=lgam)
+        if eng.noise_std is None:
+            eng.emission_status()
         ml = None if ma_latent is None else np.asarray(ma_latent).astype(bool)
         if eng.dense:     # the log-domain scans hold the exact log posteriors
             log_post, log_causal = _np(lgam), _np(eng.log_alpha)
@@ -702,6 +704,8 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
     if noise_std is not None:
         eng.gaussian_status()
         res['m_step_res_l'] = {'params': [], 'opt_state': []}      # core.py:655-658 with m_step core.py:898-904
+    else:
+        eng.emission_status()
     info = {'opt_state': {'mu': _np(mu), 'nu': _np(nu), 'count': int(_np(cnt)[0])},
             'params64': _np(W), 'repairs': eng.repairs(), 'chunk': eng.C}
     return res, info
@@ -769,6 +773,7 @@ def run_em_restarts(y, params, basis, log_posterior_inits, n_iter, transition, m
     lz = _np(logz)
     st, lhn, ehn = _np(stats), _np(lh), _np(eh)
     repairs = eng.repairs()
+    eng.emission_status()
     out = []
     for r in range(R):
         posterior = _np(gamma[r])

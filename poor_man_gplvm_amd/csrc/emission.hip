@@ -346,6 +346,16 @@ size_t pmg_emission_workspace_size(int64_t T, int32_t L, int32_t N) {
   return c.off + 256;
 }
 
+int32_t* pmg_emission_range_flag(void* workspace, int64_t T, int32_t L, int32_t N) {
+  (void)T;
+  if (!workspace || L <= 0 || N <= 0) return nullptr;
+  const int64_t Lp = round_up(L, 32), Kp = round_up(N, 128);
+  Carver c(workspace);
+  c.take<int8_t>(kDig * Lp * Kp);
+  c.take<double>(Lp);
+  return c.take<int>(4);
+}
+
 int pmg_emission_poisson(const int8_t* yq, const double* gconst, const double* tuning64,
                          const float* ma_neuron_1d, const uint8_t* ma_latent, double dt,
                          int64_t T, int32_t L, int32_t N, int32_t Kp, float* delta,
@@ -360,8 +370,7 @@ int pmg_emission_poisson(const int8_t* yq, const double* gconst, const double* t
   Carver c(workspace);
   int8_t* qd = c.take<int8_t>(kDig * (size_t)Lp * Kp);
   double* lamsum = c.take<double>(Lp);
-  int* bad = c.take<int>(4);
-  PMG_HIP(hipMemsetAsync(bad, 0, sizeof(int), st));
+  int* bad = c.take<int>(4);   // sticky range flag (zero-filled workspace; the caller clears it)
   hipLaunchKernelGGL(k_rates_prepare, dim3((Lp + 3) / 4), dim3(256), 0, st, tuning64, L, N,
                      ma_neuron_1d, dt, Lp, Kp, qd, lamsum, bad);
   PMG_LAUNCH_CHECK();

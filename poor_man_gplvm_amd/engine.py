@@ -249,7 +249,9 @@ class DeviceEM:
         self.tuning32 = torch.empty((L, N), dtype=f32, device=dev)
         self.yw = torch.empty((L, N), dtype=f64, device=dev)
         self.tw = torch.empty(L, dtype=f64, device=dev)
-        self.ws_em = torch.empty(int(self.lib.pmg_emission_workspace_size(T, L, N)), dtype=torch.uint8, device=dev)
+        # zero-filled once: it holds the emission's sticky range flag (include/pmg.h)
+        self.ws_em = torch.zeros(int(self.lib.pmg_emission_workspace_size(T, L, N)), dtype=torch.uint8, device=dev)
+        self._em_flag = _flag_view(self.lib, self.ws_em, T, L, N)
         # zero-filled once (include/pmg.h): the scan kernels keep its control words zero
         self.ws_fb = torch.zeros(int(self.lib.pmg_fwdbwd_workspace_size(T, L, min(self.C, self.Cb))),
                                  dtype=torch.uint8, device=dev)
@@ -535,6 +537,11 @@ class DeviceEM:
         w[nat.CTL_FWD + nat.CTL_WARM] = 0
         w[nat.CTL_BWD + nat.CTL_WARM] = 0
 
+    def emission_status(self):
+        """Raise if an integer-path emission since the last check met |log lam| >= 60
+        (outside the exact digit range; device read: syncs), then clear the flag."""
+        _check_emission_flag(self._em_flag)
+
     def _snapshot_repairs(self):
         self._rep_host.copy_(self.ctl_words(), non_blocking=True)
         self._rep_evt = torch.cuda.Event()
@@ -595,7 +602,8 @@ class DeviceEM:
         self.emission(likelihood_scale)
         self.forward(likelihood_scale, logz_out, keep_alpha)
         self.backward(likelihood_scale, True, gamma, rho, log_gamma)
-        self._snapshot_repairs()
+        if self.scan.adaptive:      # host-side adaptation reads the counters without a sync
+            self._snapshot_repairs()
 
     def repairs(self):
         """(forward, backward) chunks recomputed by the last scans' relaxation (device
@@ -631,6 +639,20 @@ class DeviceEM:
                                                 nat.ptr(ws), ws.numel(), nat.stream_handle()),
                   "pmg_joint_accumulate")
         return S
+
+
+def _flag_view(lib, ws, T, L, N):
+    """The emission workspace's int32 range flag as a (1,) device view."""
+    off = int(lib.pmg_emission_range_flag(ctypes.c_void_p(ws.data_ptr()), T, L, N)) - ws.data_ptr()
+    return ws[off:off + 4].view(torch.int32)
+
+
+def _check_emission_flag(flag):
+    bad = int(flag.item()) != 0
+    flag.zero_()
+    if bad:
+        raise nat.NativeError("pmg_emission_poisson: |log(tuning*dt)| >= 60 somewhere -- outside the exact "
+                              "int8-digit range (the emission of that E-step is invalid)")
 
 
 def log_of(x: torch.Tensor) -> torch.Tensor:
@@ -695,7 +717,8 @@ class RestartBatchEM:
         self.tuning32 = torch.empty((LA, N), dtype=f32, device=dev)
         self.yw = torch.empty((LA, N), dtype=f64, device=dev)
         self.tw = torch.empty(LA, dtype=f64, device=dev)
-        self.ws_em = torch.empty(int(self.lib.pmg_emission_workspace_size(T, LA, N)), dtype=torch.uint8, device=dev)
+        self.ws_em = torch.zeros(int(self.lib.pmg_emission_workspace_size(T, LA, N)), dtype=torch.uint8, device=dev)
+        self._em_flag = _flag_view(self.lib, self.ws_em, T, LA, N)
         fb = int(self.lib.pmg_fwdbwd_batched_workspace_size(T, L, min(self.C, self.Cb), R))
         if fb == 0:
             raise nat.NativeError(f"n_latent_bin={L} unsupported by the scan kernels (max 1024)")
@@ -837,6 +860,9 @@ class RestartBatchEM:
         self.emission(likelihood_scale)
         self.forward(likelihood_scale, logz_out, keep_alpha=gamma is not None)
         self.backward(likelihood_scale, gamma)
+
+    def emission_status(self):
+        _check_emission_flag(self._em_flag)
 
     def ctl_words(self, r):
         """Restart r's scan control words (device view)."""
