@@ -523,3 +523,23 @@ def test_latent_only_fit_em_one_iteration_vs_oracle():
     np.testing.assert_allclose(res['log_marginal_l'], [lz], rtol=1e-7)
     assert res['m_step_res_l']['n_iter'] == [mr['n_iter']]
     assert res['posterior'].shape == (T, L) and res['log_posterior_final'].shape == (T, L)
+
+
+def test_emission_range_flag_raises():
+    """|log(tuning dt)| >= 60 is outside the exact int8-digit range: the sticky range flag
+    makes the fit / decode raise instead of returning a silently wrong emission."""
+    from poor_man_gplvm_amd import _native as nat
+    d = make(8, 32, 200)
+    sp, eng = _engine(d, 32)
+    tun = np.array(d['tuning'], copy=True)
+    eng.set_tuning(tun)
+    eng.emission(1.0)
+    eng.emission_status()                       # in range: no error, flag stays clear
+    tun[3, 2] = 1e30
+    eng.set_tuning(tun)
+    eng.emission(1.0)
+    with pytest.raises(nat.NativeError, match="digit range"):
+        eng.emission_status()
+    eng.set_tuning(d['tuning'])
+    eng.emission(1.0)
+    eng.emission_status()                       # cleared by the previous check
