@@ -228,6 +228,7 @@ def bench_timeshard(args):
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist.get_world_size()       # n_gpus = the world RCCL sees
     from poor_man_gplvm_amd.engine import AdamConfig, ScanConfig, KernelTimer
     from poor_man_gplvm_amd.gp_kernel import banded_transition
     from poor_man_gplvm_amd.timeshard import DistComm, LocalComm, TimeShardedEM, shard_layout
@@ -368,7 +369,16 @@ def main():
     ap.add_argument("--restarts", type=int, default=0,
                     help="R > 1: R restarts per GPU as one batched fit (engine.RestartBatchEM; SURVEY 8(e), "
                          "C5 runs 8 per GPU); reports restart-iterations/s beside the one-restart engine")
+    ap.add_argument("--launcher-selftest", action="store_true",
+                    help="CPU-only check of the N-rank launcher: gloo ranks, barrier + max-over-ranks timing of "
+                         "a host loop, one JSON line (no GPU is touched)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # N ranks requested without a launcher: start them as children (this process
+        # never touches the GPU) and exit with their status
+        return launch_ranks(args.gpus)
+    if args.launcher_selftest:
+        return launcher_selftest(args)
     if args.shard == "time":
         return bench_timeshard(args)
     if args.restarts > 1:
@@ -382,6 +392,7 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist.get_world_size()       # n_gpus = the world RCCL sees
 
     from poor_man_gplvm_amd.engine import SpikeData, DeviceEM, AdamConfig, ScanConfig, KernelTimer
     from poor_man_gplvm_amd.gp_kernel import banded_transition
@@ -523,6 +534,7 @@ def bench_restarts(args):
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist.get_world_size()       # n_gpus = the world RCCL sees
     from poor_man_gplvm_amd.engine import SpikeData, DeviceEM, RestartBatchEM, AdamConfig, ScanConfig, KernelTimer
     from poor_man_gplvm_amd.gp_kernel import banded_transition
     cfg = args.config if args.config != "c3" else "c5"
@@ -646,6 +658,65 @@ def bench_restarts(args):
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` outside a launcher: run N ranks (one process per GPU) through
+    torch.distributed.run on this node, rendezvous on 127.0.0.1.  The parent imports
+    nothing GPU-related and only forwards the children's exit status; rank 0 prints the
+    JSON line.  Under torchrun (WORLD_SIZE set) bench.py runs as one rank directly."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={int(n)}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)]
+    cmd += sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    rc = subprocess.run(cmd, env=env).returncode
+    if rc:
+        sys.exit(rc)
+
+
+def world_info():
+    """(world, rank, local_rank) from the torchrun environment (1, 0, 0 without it)."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def launcher_selftest(args):
+    """The launcher's rank protocol on the CPU (gloo): every rank times the same host
+    loop between two barriers, the max over ranks is taken with all_reduce(MAX), rank 0
+    prints one JSON line whose n_gpus is the world size the process group saw."""
+    import torch
+    import torch.distributed as dist
+    world, rank, _ = world_info()
+    if world > 1:
+        dist.init_process_group("gloo")
+        world = dist.get_world_size()
+    x = np.random.default_rng(rank).random((256, 256))
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        x = np.tanh(x @ x.T / 256.0)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    te = torch.tensor([el], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": "launcher selftest (host loop)", "value": world * args.steps / float(te[0]),
+                          "unit": "loops/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ranks_max_s": float(te[0])}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PMG_ABI_VERSION 1
+#define PMG_ABI_VERSION 2
 
 #define PMG_OK 0
 #define PMG_EINVAL (-1)       /* bad shape / argument */
@@ -90,15 +90,18 @@ int pmg_tuning_softplus_batched(const float* basis, const double* W, int32_t L, 
 /* the caller reads and clears it (no per-call memset).                  */
 size_t pmg_emission_workspace_size(int64_t T, int32_t L, int32_t N);
 int32_t* pmg_emission_range_flag(void* workspace, int64_t T, int32_t L, int32_t N);
+/* ll64 (T,L) f64 (may be NULL): the unsplit ll as well, for consumers   */
+/* that need it exact far below the block maximum (the exact decode's    */
+/* dense scans: delta's f32 rounding is 3e-5 absolute at |delta| ~ 500). */
 int pmg_emission_poisson(const int8_t* yq, const double* gconst, const double* tuning64,
                          const float* ma_neuron_1d, const uint8_t* ma_latent, double dt,
                          int64_t T, int32_t L, int32_t N, int32_t Kp, float* delta,
-                         double* rblk, void* workspace, size_t workspace_bytes, void* stream);
+                         double* rblk, double* ll64, void* workspace, size_t workspace_bytes, void* stream);
 /* Generic f64 emission (non-integer y, weighted or 2-D masks). y (T,N) f32. */
 int pmg_emission_poisson_f64(const float* y, const double* gconst, const double* tuning64,
                              const float* ma_neuron, int32_t ma_is_2d, const uint8_t* ma_latent,
                              double dt, int64_t T, int32_t L, int32_t N, float* delta,
-                             double* rblk, void* workspace, size_t workspace_bytes, void* stream);
+                             double* rblk, double* ll64, void* workspace, size_t workspace_bytes, void* stream);
 /* Latent mask on an unmasked emission (any of the emissions above, run with ma_latent =   */
 /* NULL): (delta, rblk) = the (delta0, rblk0) those kernels would produce with ma_latent   */
 /* (ll[:, ma_latent == 0] = -1e20, decoder.py:46; block references over kept bins).  Used  */
@@ -143,7 +146,7 @@ int pmg_tuning_linear(const float* basis, const double* W, int32_t L, int32_t NB
 /* f64 accumulation; output split as pmg_emission_poisson (delta, rblk).           */
 int pmg_emission_gaussian(const float* y, const double* tuning64, const float* ma_neuron, int32_t ma_is_2d,
                           const uint8_t* ma_latent, double noise_std, double dt, int64_t T, int32_t L,
-                          int32_t N, float* delta, double* rblk, void* stream);
+                          int32_t N, float* delta, double* rblk, double* ll64, void* stream);
 /* Per-time-bin dt (decoder.get_loglikelihood_ma_all_changing_dt with the Gaussian
  * observation model, decoder.py:73-85 -> :50-57): mu = tuning * dt_t[t]; dt_t (T) f64. */
 int pmg_emission_gaussian_dt(const float* y, const double* tuning64, const float* ma_neuron, int32_t ma_is_2d,
@@ -185,7 +188,12 @@ typedef struct pmg_transition {
 /*          logz (1) f64 = sum_t logc (decoder.py:169).                  */
 /* The workspace must be ZERO-FILLED before its first use (one hipMemset);   */
 /* the kernels keep its control words and counters zero between calls, so    */
-/* the scans issue no memsets of their own.                                   */
+/* the scans issue no memsets of their own.  One exception is STICKY: the    */
+/* int32 timeout word at pmg_fwdbwd_repair_counter_offset + 4*2 (forward) /  */
+/* + 4*(16+2) (backward) is set when a relaxation's bounded grid barrier     */
+/* gave up (the call's outputs are then invalid) and stays set across later  */
+/* calls (their relaxations fail fast) until the caller reads and clears it. */
+/* PMG_DEBUG_SPIN_TICKS (env) overrides the 2 s spin bound (tests).          */
 size_t pmg_fwdbwd_workspace_size(int64_t T, int32_t L, int32_t chunk);
 int pmg_forward_filter(const float* delta, const float* phi, const double* m, int64_t T,
                        const pmg_transition* tr, double likelihood_scale, int32_t chunk,
@@ -223,6 +231,14 @@ int pmg_backward_smoother(const float* delta, const float* phi, const float* alp
 /* warms up 256 steps instead of `warmup` (decided by the relaxation kernel, */
 /* no host sync).  Phase-2 calls without it leave the decision unchanged.   */
 #define PMG_PHASE_ADAPTIVE_WARMUP 8
+/* Either direction, phase-2 calls: PMG_PHASE_SEGMENTS(S) (1 <= S <= 4095) sets  */
+/* the relaxation's segment count per sequence (default 0: #CUs, or #CUs / R for */
+/* R batched restarts).  The relaxation's repaired states depend on where its    */
+/* segments end (each segment stops recomputing once a state settles within tol) */
+/* so two calls agree bit for bit only on the same segment grid: a single fit    */
+/* run with S = #CUs / R reproduces restart r of an R-restart batch.             */
+#define PMG_PHASE_SEGMENTS(S) ((int32_t)((S) & 0xfff) << 16)
+#define PMG_PHASE_FLAG_BITS (7 | PMG_PHASE_ADAPTIVE_WARMUP | (0xfff << 16))
 int pmg_forward_filter_phase(const float* delta, const float* phi, const double* m, int64_t T,
                              const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                              int32_t warmup, double tol, float* alpha, double* logc, double* logz,
@@ -297,24 +313,29 @@ typedef struct pmg_dense_transition {
   float logA[4];        /* host values logA00 logA01 logA10 logA11 (-inf allowed)    */
 } pmg_dense_transition;
 size_t pmg_dense_workspace_size(int64_t T, int32_t L, int32_t chunk);
-/* outputs: log_alpha (T,2,L) f32 log filter posteriors (required: the backward */
-/* pass reads it); alpha (T,2,L) f32 = exp(log_alpha) (may be NULL); logc, logz */
-/* as pmg_forward_filter.                                                       */
-int pmg_dense_forward(const float* delta, const float* phi, const double* m, int64_t T,
+/* outputs: log_alpha (T,2,L) F64 log filter posteriors (required: the backward */
+/* pass reads it; f64 because entries far below the row maximum, e.g. -1000,    */
+/* would carry 6e-5 absolute rounding in f32 and the joint of rarely visited     */
+/* states is a ratio of such terms); alpha (T,2,L) f32 = exp(log_alpha) (may be */
+/* NULL); logc, logz as pmg_forward_filter.                                     */
+/* ll64 (T,L) f64 or NULL: the emission's unsplit ll (pmg_emission_poisson's ll64)  */
+/* instead of (delta, phi) -- exact far below the block maxima (exact decodes).       */
+int pmg_dense_forward(const float* delta, const float* phi, const double* ll64, const double* m, int64_t T,
                       const pmg_dense_transition* tr, double likelihood_scale, int32_t chunk, int32_t warmup,
-                      double tol, float* alpha, float* log_alpha, double* logc, double* logz, void* workspace,
+                      double tol, float* alpha, double* log_alpha, double* logc, double* logz, void* workspace,
                       size_t workspace_bytes, void* stream);
 /* outputs (each may be NULL): P (T,L), gamma (T,2,L), log_gamma (T,2,L) (exact   */
 /* log posteriors, the reference's log_acausal_posterior_all), rho (T,2,L) as      */
-/* pmg_backward_smoother, log_rho (T,2,L) = log(rho) (no overflow).                */
-int pmg_dense_backward(const float* delta, const float* phi, const float* log_alpha, int64_t T,
+/* pmg_backward_smoother, log_rho (T,2,L) F64 = log(rho) (no overflow).            */
+int pmg_dense_backward(const float* delta, const float* phi, const double* ll64, const double* log_alpha, int64_t T,
                        const pmg_dense_transition* tr, double likelihood_scale, int32_t chunk, int32_t warmup,
-                       double tol, float* P, float* gamma, float* log_gamma, float* rho, float* log_rho,
+                       double tol, float* P, float* gamma, float* log_gamma, float* rho, double* log_rho,
                        void* workspace, size_t workspace_bytes, void* stream);
 /* Pairwise joint in log space (decode, dense scans): logS (2L x 2L) f64 =           */
-/* LSE_{t<T-1} log_alpha_t[x] + log_rho_{t+1}[x'], x = (d,i); the caller forms the   */
-/* log joint logA[d,d'] + logK[d',i,j] + logS (decoder.py:215-221).                  */
-int pmg_joint_log_accumulate(const float* log_alpha, const float* log_rho, int64_t T, int32_t L, double* logS,
+/* LSE_{t<T-1} log_alpha_t[x] + log_rho_{t+1}[x'], x = (d,i) (f64 inputs, f64 online  */
+/* sum); the caller forms the log joint logA[d,d'] + logK[d',i,j] + logS               */
+/* (decoder.py:215-221).  Every entry is finite wherever the reference's is.           */
+int pmg_joint_log_accumulate(const double* log_alpha, const double* log_rho, int64_t T, int32_t L, double* logS,
                              void* stream);
 
 /* ------------------------------------------------------------------ */

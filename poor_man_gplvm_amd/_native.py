@@ -27,7 +27,15 @@ CTL_REPAIRS, CTL_ROUNDS, CTL_ERR, CTL_WARM = 0, 1, 2, 3
 PHASE_NO_JUMP_ROWS = 4
 # both phase calls of an E-step: the device lengthens the next warm-up after a cascade (PMG_PHASE_ADAPTIVE_WARMUP)
 PHASE_ADAPTIVE_WARMUP = 8
-ABI_VERSION = 1
+ABI_VERSION = 2
+
+
+def phase_segments(S: int) -> int:
+    """PMG_PHASE_SEGMENTS(S): the relaxation's segment count per sequence (0 = default)."""
+    S = int(S or 0)
+    if not 0 <= S <= 0xfff:
+        raise ValueError(f"relax_segments must be in [0, 4095], got {S}")
+    return S << 16
 
 # every symbol the header declares (checked by tests/test_capi_symbols.py)
 EXPORTED_SYMBOLS = (
@@ -89,8 +97,8 @@ _SIGS = {
     "pmg_spikes_prepare": ([_P, _I64, _I32, _P, _I32, _P, _I32, _P, _P, _I32, _P, _P], _I32),
     "pmg_tuning_softplus": ([_P, _P, _I32, _I32, _I32, _P, _P, _P], _I32),
     "pmg_emission_workspace_size": ([_I64, _I32, _I32], _SZ),
-    "pmg_emission_poisson": ([_P, _P, _P, _P, _P, _D, _I64, _I32, _I32, _I32, _P, _P, _P, _SZ, _P], _I32),
-    "pmg_emission_poisson_f64": ([_P, _P, _P, _P, _I32, _P, _D, _I64, _I32, _I32, _P, _P, _P, _SZ, _P], _I32),
+    "pmg_emission_poisson": ([_P, _P, _P, _P, _P, _D, _I64, _I32, _I32, _I32, _P, _P, _P, _P, _SZ, _P], _I32),
+    "pmg_emission_poisson_f64": ([_P, _P, _P, _P, _I32, _P, _D, _I64, _I32, _I32, _P, _P, _P, _P, _SZ, _P], _I32),
     "pmg_emission_poisson_dt": ([_P, _P, _P, _P, _I32, _P, _P, _I64, _I32, _I32, _P, _P, _P], _I32),
     "pmg_naive_bayes_normalize": ([_P, _P, _I64, _I32, _P, _P, _P], _I32),
     "pmg_emission_rowref": ([_P, _I64, _I32, _D, _P, _P, _P], _I32),
@@ -125,16 +133,16 @@ _SIGS = {
                               _P, _P, _P, _P, _SZ, _P], _I32),
     "pmg_tuning_linear": ([_P, _P, _I32, _I32, _I32, _P, _P, _P], _I32),
     "pmg_emission_gaussian": ([_P, _P, _P, _I32, _P, ctypes.c_double, ctypes.c_double, _I64, _I32, _I32,
-                               _P, _P, _P], _I32),
+                               _P, _P, _P, _P], _I32),
     "pmg_emission_gaussian_dt": ([_P, _P, _P, _I32, _P, ctypes.c_double, _P, _I64, _I32, _I32, _P, _P, _P], _I32),
     "pmg_gaussian_mstep_workspace_size": ([_I32, _I32], _SZ),
     "pmg_gaussian_mstep": ([_P, _P, _P, _I32, _I32, _I32, ctypes.c_double, ctypes.c_double, _P, _P, _P, _SZ,
                             _P], _I32),
     "pmg_joint_workspace_size": ([_I64, _I32], _SZ),
     "pmg_dense_workspace_size": ([_I64, _I32, _I32], _SZ),
-    "pmg_dense_forward": ([_P, _P, _P, _I64, ctypes.POINTER(DenseTransition), _D, _I32, _I32, _D,
+    "pmg_dense_forward": ([_P, _P, _P, _P, _I64, ctypes.POINTER(DenseTransition), _D, _I32, _I32, _D,
                            _P, _P, _P, _P, _P, _SZ, _P], _I32),
-    "pmg_dense_backward": ([_P, _P, _P, _I64, ctypes.POINTER(DenseTransition), _D, _I32, _I32, _D,
+    "pmg_dense_backward": ([_P, _P, _P, _P, _I64, ctypes.POINTER(DenseTransition), _D, _I32, _I32, _D,
                             _P, _P, _P, _P, _P, _P, _SZ, _P], _I32),
     "pmg_joint_log_accumulate": ([_P, _P, _I64, _I32, _P, _P], _I32),
     "pmg_joint_accumulate": ([_P, _P, _I64, _I32, _P, _P, _SZ, _P], _I32),

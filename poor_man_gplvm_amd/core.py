@@ -191,11 +191,16 @@ class PoissonGPLVMJump1D:
         """Hook: the Gaussian model switches the engine's emission here."""
 
     def _scan_transition(self, mv, pmj, pjm, logK=None, logA=None):
-        """Device transition for a scan: this model's own (hyper-parameters), or, when
-        log kernels are passed (the _decode_latent arguments), the device form of
+        """Device transition for a decode scan: this model's own (hyper-parameters), or,
+        when log kernels are passed (the _decode_latent arguments), the device form of
         exactly those kernels.  Kernels equal to the model's own (1e-6) keep its
-        transition bit for bit."""
+        transition bit for bit.  With scan_config.decode_exact (default) the decode runs
+        the dense log-domain scans with the whole kernel (exact joint rows for every
+        latent, see ScanConfig.decode_exact)."""
         tr = self._transition(mv, pmj, pjm)
+        exact = bool(getattr(self.scan_config, 'decode_exact', False))
+        if exact and not isinstance(tr, DenseTransition):
+            tr = dense_transition(self.n_latent_bin, mv, pmj, pjm, self.custom_transition_kernel)
         if logK is None or logA is None:
             return tr
         lk = np.asarray(logK, np.float64)
@@ -208,7 +213,7 @@ class PoissonGPLVMJump1D:
                         and np.allclose(np.exp(la), np.exp(la_m), rtol=1e-6, atol=1e-12))
             if same:
                 return tr
-        return transition_from_log_kernels(lk, la, force_dense=isinstance(tr, DenseTransition))
+        return transition_from_log_kernels(lk, la, force_dense=exact or isinstance(tr, DenseTransition))
 
     def _run_decode(self, y, tuning, hyperparam, ma_neuron, ma_latent, likelihood_scale, joint=True,
                     logK=None, logA=None):
@@ -241,14 +246,14 @@ class PoissonGPLVMJump1D:
         T, L = eng.T, self.n_latent_bin
         logz = torch.zeros(1, dtype=torch.float64, device=dev)
         gamma = torch.empty((T, 2, L), dtype=torch.float32, device=dev)
-        rho = torch.zeros((T, 2, L), dtype=torch.float32, device=dev) if joint else None
+        rho = (torch.zeros((T, 2, L), dtype=torch.float64 if eng.dense else torch.float32, device=dev)
+               if joint else None)
         lgam = torch.empty((T, 2, L), dtype=torch.float32, device=dev) if eng.dense else None
         eng.e_step(likelihood_scale, logz, gamma=gamma, rho=rho, log_gamma=lgam)
-        if eng.noise_std is None:
-            eng.emission_status()
+        eng.check_status()
         ml = None if ma_latent is None else np.asarray(ma_latent).astype(bool)
         if eng.dense:     # the log-domain scans hold the exact log posteriors
-            log_post, log_causal = _np(lgam), _np(eng.log_alpha)
+            log_post, log_causal = _np(lgam), _np(eng.log_alpha).astype(np.float32)
         else:
             log_post, log_causal = _np(log_of(gamma)), _np(log_of(eng.alpha))
         out = {
@@ -376,6 +381,8 @@ class PoissonGPLVMJump1D:
         lml = torch.empty(T, dtype=torch.float64, device=dev)
         nat.check(lib.pmg_naive_bayes_normalize(nat.ptr(eng.delta), nat.ptr(eng.rblk), T, L, nat.ptr(log_post),
                                                 nat.ptr(lml), sh), "pmg_naive_bayes_normalize")
+        if eng.noise_std is None:
+            eng.emission_status()
         lp = _np(log_post)
         lml_h = _np(lml)
         posterior_latent = np.exp(lp)
@@ -422,6 +429,7 @@ class PoissonGPLVMJump1D:
         eng = DeviceEM(SpikeData(np.asarray(y), ma), self.n_latent_bin, scan=self.scan_config)
         self._observation(eng, hyperparam)
         eng.set_transition(tr)
+        eng.ll64 = None     # the masks edit (delta, rblk) only; logZ needs no far-state ll
         eng.set_tuning(np.asarray(tuning))
         logz = torch.zeros(len(masks), dtype=torch.float64, device=eng.dev)
         eng.set_ma_latent(None)
@@ -430,6 +438,7 @@ class PoissonGPLVMJump1D:
         for r in range(len(masks)):
             eng.emission_from(delta0, rblk0, mu8[r], likelihood_scale)
             eng.forward(likelihood_scale, logz[r:r + 1])
+        eng.check_status()
         return _np(logz).astype(np.float64)
 
     # ------------------------------------------------------------------ EM

@@ -53,26 +53,28 @@ struct DenseParams {
   float tol;
   // forward
   float* alpha;      // (T, 2, L) linear, may be null
-  float* log_alpha;  // (T, 2, L) log
+  double* log_alpha;  // (T, 2, L) log, f64
   double* logc;
   double* chunk_logz;
   double* logz;
-  float* s_in;
-  float* s_out;
+  double* s_in;     // chunk boundary states (f64: far components are compared to ~tol)
+  double* s_out;
   // backward
-  const float* log_alpha_in;
+  const double* log_alpha_in;
   float* P;
   float* gamma;
   float* log_gamma;
   float* rho;
-  float* log_rho;
-  float* b_in;
-  float* b_first;
+  double* log_rho;
+  double* b_in;
+  double* b_first;
   int* flags;
   int* ctl;
-  float* seg_end;
+  double* seg_end;
   int* seg_chg;
   int G, S;
+  uint64_t spin;
+  const double* ll64;  // (T, L) f64 ll (exact decodes) or null: e from (delta, phi)  // grid-barrier spin bound (kDSpinTicks unless a debug override)
 };
 
 // Precision: the O(L^2) inner loop runs in f32 on arguments taken relative to the
@@ -160,7 +162,8 @@ __device__ __forceinline__ float block_min(float v, float* red) { return -block_
 
 template <int JD>
 struct DenseShared {
-  float vec[2][kDNT * JD];   // the broadcast operand of the mat-vec (double-buffered by step)
+  float vec[2][kDNT * JD];   // the broadcast operand of the mat-vec (double-buffered by step),
+  float veclo[2][kDNT * JD]; // as an f32 hi + lo pair of the f64 value
   double redd[8][kDNW];      // f64 reduction scratch, rotated over call sites
   float red[8][2 * kDNW];    // f32 reduction scratch, rotated over call sites
 };
@@ -199,51 +202,75 @@ __device__ double block_lse_d(const double* v, DenseShared<JD>& sh, Slots<JD>& s
 }
 
 // log emission e[t, j] = s*delta[t, j] + phi[t, j/32] = s*(ll[t, j] - m[t])
+// With ll64 (exact decodes): e = s * (ll[t, j] - m[t]) from the unsplit f64 ll (the
+// backward pass drops the per-step constant s*m[t]: its normalisation absorbs it).
 template <int JD>
 __device__ __forceinline__ void emis(const DenseParams& p, int64_t t, double e[JD]) {
 #pragma unroll
   for (int k = 0; k < JD; ++k) {
     const int j = threadIdx.x + kDNT * k;
-    e[k] = j < p.L ? (double)p.s * (double)p.delta[t * p.L + j] + (double)p.phi[t * p.nblk + (j >> 5)]
-                   : -INFINITY;
+    if (p.ll64)
+      e[k] = j < p.L ? p.s_d * (p.ll64[t * p.L + j] - (p.m ? p.m[t] : 0.0)) : -INFINITY;
+    else
+      e[k] = j < p.L ? (double)p.s * (double)p.delta[t * p.L + j] + (double)p.phi[t * p.nblk + (j >> 5)]
+                     : -INFINITY;
   }
 }
 
-// per own output j: LSE_i(vec[i] + K[i, j]) over a column given as f32 hi + lo parts.
-// f32 inner loop with an online max; each term is exp(((Khi - m) + Klo) + vec): for the
-// terms near the max Khi - m is exact (Sterbenz), so a far weight (Khi ~ -2500, ulp 2.4e-4)
-// keeps its f64 value instead of the f32 rounding of Khi + vec.  Value in f64.
-__device__ __forceinline__ double matvec_lse(const float* vec, const float* col, const float* clo, int L) {
+// the mat-vec operand v (f64, <= 0 after the shift) as an f32 hi + lo pair
+__device__ __forceinline__ void put_vec(float* hi, float* lo, int i, double v) {
+  const float h = (float)v;
+  hi[i] = h;
+  lo[i] = (float)(v - (double)h);
+}
+
+// per own output j: LSE_i(vec[i] + K[i, j]), both operands as f32 hi + lo pairs, f32
+// inner loop with an online max.  Each term is exp((s - m) + ((err + vlo) + klo)) with
+// s = vhi + khi rounded, err its exact rounding error (two-sum) and m the running max
+// (an earlier s): for the terms that matter s - m is exact (Sterbenz), so a term whose
+// operands are both far below the peak (vec ~ -1000, K ~ -1000, ulp 6e-5) keeps its
+// f64 value to ~1e-7 -- the joint rows of latents the posterior never visits are ratios
+// of exactly such terms.  Value in f64.
+__device__ __forceinline__ double matvec_lse(const float* vec, const float* veclo, const float* col,
+                                             const float* clo, int L) {
   Lse l;
   int i = 0;
   for (; i + 8 <= L; i += 8) {
-    float kh[8], kl[8], v[8];
+    float kh[8], kl[8], sv[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       kh[q] = col[(size_t)(i + q) * L];
       kl[q] = clo[(size_t)(i + q) * L];
-      v[q] = vec[i + q] + kh[q];
+      sv[q] = vec[i + q] + kh[q];
     }
-    float bm = v[0];
+    float bm = sv[0];
 #pragma unroll
-    for (int q = 1; q < 8; ++q) bm = fmaxf(bm, v[q]);
+    for (int q = 1; q < 8; ++q) bm = fmaxf(bm, sv[q]);
     if (bm > l.m) {
-      l.s *= __expf(l.m - bm);
+      l.s *= exp_lg(l.m - bm);
       l.m = bm;
     }
     float acc = 0.f;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) acc += exp_lg(((kh[q] - l.m) + kl[q]) + vec[i + q]);
+    for (int q = 0; q < 8; ++q) {
+      const float vh = vec[i + q];
+      const float bb = sv[q] - vh;
+      const float err = (vh - (sv[q] - bb)) + (kh[q] - bb);
+      acc += exp_lg((sv[q] - l.m) + ((err + veclo[i + q]) + kl[q]));
+    }
     l.s += acc;
   }
   for (; i < L; ++i) {
     const float kh = col[(size_t)i * L], kl = clo[(size_t)i * L];
-    const float x = vec[i] + kh;
+    const float vh = vec[i];
+    const float x = vh + kh;
     if (x > l.m) {
-      l.s *= __expf(l.m - x);
+      l.s *= exp_lg(l.m - x);
       l.m = x;
     }
-    l.s += exp_lg(((kh - l.m) + kl) + vec[i]);
+    const float bb = x - vh;
+    const float err = (vh - (x - bb)) + (kh - bb);
+    l.s += exp_lg((x - l.m) + ((err + veclo[i]) + kl));
   }
   return l.value();
 }
@@ -278,28 +305,29 @@ struct DFwd {
       x1[k] -= z;
     }
   }
-  __device__ void load(const DenseParams& p, const float* src, DenseShared<JD>& sh) {
+  __device__ void load(const DenseParams& p, const double* src, DenseShared<JD>& sh) {
 #pragma unroll
     for (int k = 0; k < JD; ++k) {
       const int j = threadIdx.x + kDNT * k;
-      x0[k] = j < p.L ? (double)src[j] : -INFINITY;
-      x1[k] = j < p.L ? (double)src[p.Lp + j] : -INFINITY;
+      x0[k] = j < p.L ? src[j] : -INFINITY;
+      x1[k] = j < p.L ? src[p.Lp + j] : -INFINITY;
     }
     normalise(sh);
   }
-  __device__ void save(const DenseParams& p, float* dst) const {
+  __device__ void save(const DenseParams& p, double* dst) const {
 #pragma unroll
     for (int k = 0; k < JD; ++k) {
       const int j = threadIdx.x + kDNT * k;
       if (j < p.L) {
-        dst[j] = (float)x0[k];
-        dst[p.Lp + j] = (float)x1[k];
+        dst[j] = x0[k];
+        dst[p.Lp + j] = x1[k];
       }
     }
   }
   // one step with log emission e; returns the log normaliser c
   __device__ double step(const DenseParams& p, DenseShared<JD>& sh, int buf, const double e[JD]) {
     float* vec = sh.vec[buf];
+    float* veclo = sh.veclo[buf];
     double a0[JD], a1[JD], am = -INFINITY;
 #pragma unroll
     for (int k = 0; k < JD; ++k) {
@@ -309,13 +337,13 @@ struct DFwd {
     }
     const double A = block_max_d(am, sl.d(sh));          // shift of the continuous operand
 #pragma unroll
-    for (int k = 0; k < JD; ++k) vec[threadIdx.x + kDNT * k] = (float)(a0[k] - A);
+    for (int k = 0; k < JD; ++k) put_vec(vec, veclo, threadIdx.x + kDNT * k, a0[k] - A);
     const double jump = block_lse_d<JD, JD>(a1, sh, sl) - (double)p.logL;   // barriers: vec visible
     double x[2 * JD];
 #pragma unroll
     for (int k = 0; k < JD; ++k) {
       const int j = threadIdx.x + kDNT * k;
-      const double pr = j < p.L ? A + matvec_lse(vec, p.K + j, p.Klo + j, p.L) : -INFINITY;
+      const double pr = j < p.L ? A + matvec_lse(vec, veclo, p.K + j, p.Klo + j, p.L) : -INFINITY;
       x[k] = pr + e[k];
       x[JD + k] = jump + e[k];
     }
@@ -333,8 +361,8 @@ struct DFwd {
       const int j = threadIdx.x + kDNT * k;
       if (j < p.L) {
         const size_t o = (size_t)t * 2 * p.L + j;
-        p.log_alpha[o] = (float)x0[k];
-        p.log_alpha[o + p.L] = (float)x1[k];
+        p.log_alpha[o] = x0[k];
+        p.log_alpha[o + p.L] = x1[k];
         if (p.alpha) {
           p.alpha[o] = (float)exp(x0[k]);
           p.alpha[o + p.L] = (float)exp(x1[k]);
@@ -390,51 +418,52 @@ __global__ void __launch_bounds__(kDNT) k_dense_forward(DenseParams p) {
 // components below -1e19 on both sides (masked latents, empty dynamics) are skipped;
 // one side only is a failure.  Down to kDFar below the max (1e-13 relative: below the
 // outputs' 1e-12 atol) the tolerance is tol itself; further down it grows by kDRel per
-// unit of |log value| -- there only a later far move can make a component dominant, and
-// its fp32 rounding grows with it (an f32 log near -2500 has a 2.4e-4 ulp).
+// unit of |log value| (the states are f64 and the mat-vec keeps far terms to ~1e-7
+// absolute, so the slack is only a guard against f64 rounding of huge logs; round 2
+// needed 1e-6 with f32 states, which let far components of a boundary differ by 1e-3).
 // Returns max(|a - b| - kDRel * max(0, max(|a|, |b|) - kDFar)), compared against tol.
 // ---------------------------------------------------------------------------
-constexpr float kDRel = 1e-6f;
-constexpr float kDFar = 30.f;
-constexpr float kDEmpty = -1e19f;
+constexpr double kDRel = 1e-10;
+constexpr double kDFar = 30.0;
+constexpr double kDEmpty = -1e19;
 
-__device__ __forceinline__ float dense_comp(float a, float b) {
+__device__ __forceinline__ double dense_comp(double a, double b) {
   const bool ea = a < kDEmpty, eb = b < kDEmpty;
-  if (ea && eb) return 0.f;
+  if (ea && eb) return 0.0;
   if (ea != eb) return INFINITY;
-  return fabsf(a - b) - kDRel * fmaxf(0.f, fmaxf(fabsf(a), fabsf(b)) - kDFar);
+  return fabs(a - b) - kDRel * fmax(0.0, fmax(fabs(a), fabs(b)) - kDFar);
 }
 
-__device__ float dense_hilbert(const float* x, const float* y, int L, int Lp, const float* w) {
+__device__ float dense_hilbert(const double* x, const double* y, int L, int Lp, const float* w) {
   (void)w;
   const int lane = threadIdx.x & 63;
-  float xm = -INFINITY, ym = -INFINITY;
+  double xm = -INFINITY, ym = -INFINITY;
   for (int i = lane; i < 2 * L; i += 64) {
     const int d = i >= L, j = i - d * L;
-    xm = fmaxf(xm, x[d * Lp + j]);
-    ym = fmaxf(ym, y[d * Lp + j]);
+    xm = fmax(xm, x[d * Lp + j]);
+    ym = fmax(ym, y[d * Lp + j]);
   }
-  xm = wave_max_shfl(xm);
-  ym = wave_max_shfl(ym);
+  xm = wave_max_f64(xm);
+  ym = wave_max_f64(ym);
   if (!(xm > kDEmpty) || !(ym > kDEmpty)) return INFINITY;
-  float dev = 0.f;
+  double dev = 0.0;
   for (int i = lane; i < 2 * L; i += 64) {
     const int d = i >= L, j = i - d * L;
-    dev = fmaxf(dev, dense_comp(x[d * Lp + j] - xm, y[d * Lp + j] - ym));
+    dev = fmax(dev, dense_comp(x[d * Lp + j] - xm, y[d * Lp + j] - ym));
   }
-  return wave_max_shfl(dev);
+  return (float)wave_max_f64(dev);
 }
 
 // flags[c] = dist(x[c], y[c + off]) > tol; a failing boundary snapshots y into x
-__global__ void __launch_bounds__(256) k_dense_verify(float* __restrict__ x, const float* __restrict__ y, int first,
+__global__ void __launch_bounds__(256) k_dense_verify(double* __restrict__ x, const double* __restrict__ y, int first,
                                                       int last, int off, int L, int Lp, float tol,
                                                       int* __restrict__ flags, const float* __restrict__ w, int C,
                                                       int* __restrict__ pending) {
   const int c = first + blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c > last) return;
   const size_t SZ = (size_t)2 * Lp;
-  const float* yc = y + (size_t)(c + off) * SZ;
-  float* xc = x + (size_t)c * SZ;
+  const double* yc = y + (size_t)(c + off) * SZ;
+  double* xc = x + (size_t)c * SZ;
   const float* wc = w ? w + (size_t)(c + 1) * C * 2 * L : nullptr;
   const float d = dense_hilbert(xc, yc, L, Lp, wc);
   const bool bad = !(d <= tol);
@@ -449,7 +478,7 @@ __global__ void __launch_bounds__(256) k_dense_verify(float* __restrict__ x, con
 // ---------------------------------------------------------------------------
 // relaxation plumbing at workgroup granularity (fb_kernels.h protocol)
 // ---------------------------------------------------------------------------
-__device__ bool dense_barrier(int* ctl, int target, int* okword) {
+__device__ bool dense_barrier(int* ctl, int target, int* okword, uint64_t spin) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -461,7 +490,7 @@ __device__ bool dense_barrier(int* ctl, int target, int* okword) {
     while (__hip_atomic_load(ctl + kDArrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(2);
       if (__hip_atomic_load(ctl + kDErr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
-          __builtin_amdgcn_s_memrealtime() - t0 > kDSpinTicks) {
+          __builtin_amdgcn_s_memrealtime() - t0 > spin) {
         __hip_atomic_store(ctl + kDErr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok = 0;
         break;
@@ -521,33 +550,33 @@ __device__ int dense_find_flag(const int* flags, int lo, int hi) {
 // per-thread partial max/min, block reductions
 template <int JD>
 __device__ float dense_hilbert_reg(const DenseParams& p, DenseShared<JD>& sh, Slots<JD>& sl, const double x0[JD],
-                                   const double x1[JD], const float* y) {
-  float xm = -INFINITY, ym = -INFINITY;
-  float a[2 * JD], b[2 * JD];
+                                   const double x1[JD], const double* y) {
+  double xm = -INFINITY, ym = -INFINITY;
+  double a[2 * JD], b[2 * JD];
 #pragma unroll
   for (int k = 0; k < JD; ++k) {
     const int j = threadIdx.x + kDNT * k;
     const bool in = j < p.L;
-    a[k] = in ? (float)x0[k] : -INFINITY;
-    a[JD + k] = in ? (float)x1[k] : -INFINITY;
+    a[k] = in ? x0[k] : -INFINITY;
+    a[JD + k] = in ? x1[k] : -INFINITY;
     b[k] = in ? y[j] : -INFINITY;
     b[JD + k] = in ? y[p.Lp + j] : -INFINITY;
   }
 #pragma unroll
   for (int k = 0; k < 2 * JD; ++k) {
-    xm = fmaxf(xm, a[k]);
-    ym = fmaxf(ym, b[k]);
+    xm = fmax(xm, a[k]);
+    ym = fmax(ym, b[k]);
   }
-  xm = block_max(xm, sl.f(sh));
-  ym = block_max(ym, sl.f(sh));
+  xm = block_max_d(xm, sl.d(sh));
+  ym = block_max_d(ym, sl.d(sh));
   if (!(xm > kDEmpty) || !(ym > kDEmpty)) return INFINITY;
-  float dev = 0.f;
+  double dev = 0.0;
 #pragma unroll
   for (int k = 0; k < 2 * JD; ++k) {
     const int j = threadIdx.x + kDNT * (k % JD);
-    if (j < p.L) dev = fmaxf(dev, dense_comp(a[k] - xm, b[k] - ym));
+    if (j < p.L) dev = fmax(dev, dense_comp(a[k] - xm, b[k] - ym));
   }
-  return block_max(dev, sl.f(sh));
+  return (float)block_max_d(dev, sl.d(sh));
 }
 
 template <int JD>
@@ -561,7 +590,7 @@ __device__ bool dfwd_segment(const DenseParams& p, DFwd<JD>& st, DenseShared<JD>
     const double lz = dfwd_run<JD, true>(p, st, sh, t_c, t_e);
     if (threadIdx.x == 0) p.chunk_logz[c] = lz;
     ++nrep;
-    float* so = p.s_out + (size_t)c * SZ;
+    double* so = p.s_out + (size_t)c * SZ;
     const float d = dense_hilbert_reg<JD>(p, sh, st.sl, st.x0, st.x1, so);
     __syncthreads();
     st.save(p, so);
@@ -598,11 +627,11 @@ __global__ void __launch_bounds__(kDNT) k_dense_forward_relax(DenseParams p) {
       if (changed) st.save(p, p.seg_end + ((size_t)(k & 1) * p.S + s) * SZ);
       dense_publish(p, k, s, changed);
       ++rounds;
-      if (!dense_barrier(p.ctl, (k + 1) * p.S, &word)) break;
+      if (!dense_barrier(p.ctl, (k + 1) * p.S, &word, p.spin)) break;
       if (dense_ctl(p.ctl, kDChanged + k % 3, &word) == 0) break;
       changed = false;
       if (s > 0 && p.seg_chg[(k & 1) * p.S + s - 1]) {
-        const float* X = p.seg_end + ((size_t)(k & 1) * p.S + s - 1) * SZ;
+        const double* X = p.seg_end + ((size_t)(k & 1) * p.S + s - 1) * SZ;
         if (threadIdx.x < 64) {
           const float d = dense_hilbert(X, p.s_in + (size_t)a * SZ, p.L, p.Lp, nullptr);
           if (threadIdx.x == 0) word = !(d <= p.tol);
@@ -644,21 +673,21 @@ struct DBwd {
       b0[k] = b1[k] = j < p.L ? 0.0 : -INFINITY;
     }
   }
-  __device__ void load(const DenseParams& p, const float* src) {
+  __device__ void load(const DenseParams& p, const double* src) {
 #pragma unroll
     for (int k = 0; k < JD; ++k) {
       const int j = threadIdx.x + kDNT * k;
-      b0[k] = j < p.L ? (double)src[j] : -INFINITY;
-      b1[k] = j < p.L ? (double)src[p.Lp + j] : -INFINITY;
+      b0[k] = j < p.L ? src[j] : -INFINITY;
+      b1[k] = j < p.L ? src[p.Lp + j] : -INFINITY;
     }
   }
-  __device__ void save(const DenseParams& p, float* dst) const {
+  __device__ void save(const DenseParams& p, double* dst) const {
 #pragma unroll
     for (int k = 0; k < JD; ++k) {
       const int j = threadIdx.x + kDNT * k;
       if (j < p.L) {
-        dst[j] = (float)b0[k];
-        dst[p.Lp + j] = (float)b1[k];
+        dst[j] = b0[k];
+        dst[p.Lp + j] = b1[k];
       }
     }
   }
@@ -681,14 +710,15 @@ struct DBwd {
     }
     const double A = block_max_d(vm, sl.d(sh));
     float* vec = sh.vec[buf];
+    float* veclo = sh.veclo[buf];
 #pragma unroll
-    for (int k = 0; k < JD; ++k) vec[threadIdx.x + kDNT * k] = (float)(v0[k] - A);
+    for (int k = 0; k < JD; ++k) put_vec(vec, veclo, threadIdx.x + kDNT * k, v0[k] - A);
     const double w1 = block_lse_d<JD, JD>(v1, sh, sl) - (double)p.logL;   // barriers: vec visible
 #pragma unroll
     for (int k = 0; k < JD; ++k) {
       const int i = threadIdx.x + kDNT * k;
       if (i < p.L) {
-        const double w0 = A + matvec_lse(vec, p.KT + i, p.KTlo + i, p.L);   // KT[j][i] = logK0[i][j]
+        const double w0 = A + matvec_lse(vec, veclo, p.KT + i, p.KTlo + i, p.L);   // KT[j][i] = logK0[i][j]
         b0[k] = lse2d(p.lA00 + w0, p.lA01 + w1);
         b1[k] = lse2d(p.lA10 + w0, p.lA11 + w1);
       } else {
@@ -709,8 +739,8 @@ __device__ void dbwd_out(const DenseParams& p, DBwd<JD>& st, DenseShared<JD>& sh
     for (int k = 0; k < JD; ++k) {
       const int j = threadIdx.x + kDNT * k;
       const size_t o = (size_t)t * 2 * p.L + j;
-      la[k] = j < p.L ? (double)p.log_alpha_in[o] + st.b0[k] : -INFINITY;
-      la[JD + k] = j < p.L ? (double)p.log_alpha_in[o + p.L] + st.b1[k] : -INFINITY;
+      la[k] = j < p.L ? p.log_alpha_in[o] + st.b0[k] : -INFINITY;
+      la[JD + k] = j < p.L ? p.log_alpha_in[o + p.L] + st.b1[k] : -INFINITY;
     }
     const double G = block_lse_d<JD, 2 * JD>(la, sh, st.sl);
 #pragma unroll
@@ -736,8 +766,8 @@ __device__ void dbwd_out(const DenseParams& p, DBwd<JD>& st, DenseShared<JD>& sh
             p.rho[o1 + p.L] = (float)exp(vp1[k] - G);
           }
           if (p.log_rho) {
-            p.log_rho[o1] = (float)(vp0[k] - G);
-            p.log_rho[o1 + p.L] = (float)(vp1[k] - G);
+            p.log_rho[o1] = vp0[k] - G;
+            p.log_rho[o1 + p.L] = vp1[k] - G;
           }
         }
       }
@@ -796,7 +826,7 @@ __device__ bool dbwd_segment(const DenseParams& p, DBwd<JD>& st, DenseShared<JD>
     st.step_back(p, sh, (int)(t_e & 1), e, vp0, vp1);
     dbwd_out<JD>(p, st, sh, t_c, t_e, vp0, vp1, true);
     ++nrep;
-    float* bf = p.b_first + (size_t)c * SZ;
+    double* bf = p.b_first + (size_t)c * SZ;
     const float d = dense_hilbert_reg<JD>(p, sh, st.sl, st.b0, st.b1, bf);
     __syncthreads();
     st.save(p, bf);
@@ -833,11 +863,11 @@ __global__ void __launch_bounds__(kDNT) k_dense_backward_relax(DenseParams p) {
       if (changed) st.save(p, p.seg_end + ((size_t)(k & 1) * p.S + s) * SZ);
       dense_publish(p, k, s, changed);
       ++rounds;
-      if (!dense_barrier(p.ctl, (k + 1) * p.S, &word)) break;
+      if (!dense_barrier(p.ctl, (k + 1) * p.S, &word, p.spin)) break;
       if (dense_ctl(p.ctl, kDChanged + k % 3, &word) == 0) break;
       changed = false;
       if (s + 1 < p.S && p.seg_chg[(k & 1) * p.S + s + 1]) {
-        const float* X = p.seg_end + ((size_t)(k & 1) * p.S + s + 1) * SZ;
+        const double* X = p.seg_end + ((size_t)(k & 1) * p.S + s + 1) * SZ;
         if (threadIdx.x < 64) {
           const float d = dense_hilbert(p.b_in + (size_t)(b - 1) * SZ, X, p.L, p.Lp, nullptr);
           if (threadIdx.x == 0) word = !(d <= p.tol);
@@ -868,18 +898,20 @@ __global__ void __launch_bounds__(kDNT) k_dense_backward_relax(DenseParams p) {
 // ---------------------------------------------------------------------------
 constexpr int kJT = 64, kJS = 32;
 
-__global__ void __launch_bounds__(256) k_joint_log(const float* __restrict__ la, const float* __restrict__ lr,
+__global__ void __launch_bounds__(256) k_joint_log(const double* __restrict__ la, const double* __restrict__ lr,
                                                    int64_t T, int L2, double* __restrict__ logS) {
-  __shared__ float sa[kJS][kJT], sr[kJS][kJT];
+  // f64 operands and sums: an entry of a rarely visited row is a ratio of sums of terms
+  // far below the total (log values like -1000, whose f32 rounding is 6e-5 absolute)
+  __shared__ double sa[kJS][kJT], sr[kJS][kJT];
   const int x0 = blockIdx.x * kJT, y0 = blockIdx.y * kJT;
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  float m[4][4], sm[4][4];
+  double m[4][4], sm[4][4];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
-      m[a][b] = kNegBig;
-      sm[a][b] = 0.f;
+      m[a][b] = -INFINITY;
+      sm[a][b] = 0.0;
     }
   for (int64_t t0 = 0; t0 < T - 1; t0 += kJS) {
     for (int k = threadIdx.x; k < kJS * kJT; k += 256) {
@@ -890,8 +922,16 @@ __global__ void __launch_bounds__(256) k_joint_log(const float* __restrict__ la,
       sr[tt][c] = (ok && y0 + c < L2) ? lr[(t + 1) * L2 + y0 + c] : -INFINITY;
     }
     __syncthreads();
+    // two passes over the staged block: its max per pair, then the exps relative to the
+    // new max (branch-free; the block's f32 exps of f64 differences are exact to
+    // ~|x| 6e-8 of a term e^x of the sum)
+    double bm[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) bm[a][b] = m[a][b];
     for (int tt = 0; tt < kJS; ++tt) {
-      float av[4], rv[4];
+      double av[4], rv[4];
 #pragma unroll
       for (int a = 0; a < 4; ++a) av[a] = sa[tt][ty * 4 + a];
 #pragma unroll
@@ -899,15 +939,28 @@ __global__ void __launch_bounds__(256) k_joint_log(const float* __restrict__ la,
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const float v = av[a] + rv[b];
-          if (v > m[a][b]) {
-            sm[a][b] = sm[a][b] * exp_lg(m[a][b] - v) + 1.f;
-            m[a][b] = v;
-          } else {
-            sm[a][b] += exp_lg(v - m[a][b]);
-          }
+        for (int b = 0; b < 4; ++b) bm[a][b] = fmax(bm[a][b], av[a] + rv[b]);
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        if (bm[a][b] > m[a][b]) {
+          sm[a][b] *= (double)exp_lg((float)(m[a][b] - bm[a][b]));
+          m[a][b] = bm[a][b];
         }
+      }
+    for (int tt = 0; tt < kJS; ++tt) {
+      double av[4], rv[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) av[a] = sa[tt][ty * 4 + a];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) rv[b] = sr[tt][tx * 4 + b];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          if (m[a][b] > -INFINITY) sm[a][b] += (double)exp_lg((float)((av[a] + rv[b]) - m[a][b]));
     }
     __syncthreads();
   }
@@ -916,8 +969,7 @@ __global__ void __launch_bounds__(256) k_joint_log(const float* __restrict__ la,
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int x = x0 + ty * 4 + a, y = y0 + tx * 4 + b;
-      if (x < L2 && y < L2)
-        logS[(size_t)x * L2 + y] = sm[a][b] > 0.f ? (double)m[a][b] + log((double)sm[a][b]) : -INFINITY;
+      if (x < L2 && y < L2) logS[(size_t)x * L2 + y] = sm[a][b] > 0.0 ? m[a][b] + log(sm[a][b]) : -INFINITY;
     }
 }
 
@@ -926,10 +978,10 @@ __global__ void __launch_bounds__(256) k_joint_log(const float* __restrict__ la,
 // ---------------------------------------------------------------------------
 struct DenseWork {
   int* ctl;
-  float *s_in, *s_out, *b_in, *b_first;
+  double *s_in, *s_out, *b_in, *b_first;
   double* chunk_logz;
   int* flags;
-  float* seg_end;
+  double* seg_end;
   int* seg_chg;
 };
 
@@ -940,13 +992,13 @@ static DenseWork carve_dense(void* ws, int64_t T, int Lp, int C, size_t* total =
   Carver c(ws);
   DenseWork w;
   w.ctl = c.take<int>(64);
-  w.s_in = c.take<float>((size_t)M * 2 * Lp);
-  w.s_out = c.take<float>((size_t)M * 2 * Lp);
-  w.b_in = c.take<float>((size_t)M * 2 * Lp);
-  w.b_first = c.take<float>((size_t)M * 2 * Lp);
+  w.s_in = c.take<double>((size_t)M * 2 * Lp);
+  w.s_out = c.take<double>((size_t)M * 2 * Lp);
+  w.b_in = c.take<double>((size_t)M * 2 * Lp);
+  w.b_first = c.take<double>((size_t)M * 2 * Lp);
   w.chunk_logz = c.take<double>(M);
   w.flags = c.take<int>(M);
-  w.seg_end = c.take<float>((size_t)2 * kDMaxSeg * 2 * Lp);
+  w.seg_end = c.take<double>((size_t)2 * kDMaxSeg * 2 * Lp);
   w.seg_chg = c.take<int>(2 * kDMaxSeg);
   if (total) *total = c.off + 256;
   return w;
@@ -991,6 +1043,7 @@ static int dense_params(DenseParams& p, const pmg_dense_transition* tr, int64_t 
   if (S > p.M) S = p.M;
   p.G = (p.M + S - 1) / S;
   p.S = (p.M + p.G - 1) / p.G;
+  p.spin = spin_ticks(kDSpinTicks);
   return PMG_OK;
 }
 
@@ -1018,9 +1071,9 @@ size_t pmg_dense_workspace_size(int64_t T, int32_t L, int32_t chunk) {
   return total;
 }
 
-int pmg_dense_forward(const float* delta, const float* phi, const double* m, int64_t T,
+int pmg_dense_forward(const float* delta, const float* phi, const double* ll64, const double* m, int64_t T,
                       const pmg_dense_transition* tr, double likelihood_scale, int32_t chunk, int32_t warmup,
-                      double tol, float* alpha, float* log_alpha, double* logc, double* logz, void* workspace,
+                      double tol, float* alpha, double* log_alpha, double* logc, double* logz, void* workspace,
                       size_t workspace_bytes, void* stream) {
   DenseParams p;
   int rc = dense_params(p, tr, T, chunk, warmup, likelihood_scale, tol);
@@ -1031,6 +1084,7 @@ int pmg_dense_forward(const float* delta, const float* phi, const double* m, int
   DenseWork w = carve_dense(workspace, T, p.Lp, chunk);
   p.delta = delta;
   p.phi = phi;
+  p.ll64 = ll64;
   p.m = m;
   p.alpha = alpha;
   p.log_alpha = log_alpha;
@@ -1045,11 +1099,13 @@ int pmg_dense_forward(const float* delta, const float* phi, const double* m, int
   p.seg_chg = w.seg_chg;
   dense_kernel_t kf, kfr, kb, kbr;
   dense_kernels(p.Lp / kDNT, &kf, &kfr, &kb, &kbr);
-  PMG_HIP(hipMemsetAsync(p.ctl, 0, 16 * sizeof(int), st));
+  // per-call words; the timeout word (kDErr) is sticky until the host reads it
+  PMG_HIP(hipMemsetAsync(p.ctl, 0, kDErr * sizeof(int), st));
+  PMG_HIP(hipMemsetAsync(p.ctl + kDErr + 1, 0, (16 - kDErr - 1) * sizeof(int), st));
   hipLaunchKernelGGL(kf, dim3(p.M), dim3(kDNT), 0, st, p);
   PMG_LAUNCH_CHECK();
   if (p.M > 1) {
-    hipLaunchKernelGGL(k_dense_verify, dim3((p.M - 1 + 3) / 4), dim3(256), 0, st, w.s_in, (const float*)w.s_out, 1,
+    hipLaunchKernelGGL(k_dense_verify, dim3((p.M - 1 + 3) / 4), dim3(256), 0, st, w.s_in, (const double*)w.s_out, 1,
                        p.M - 1, -1, p.L, p.Lp, p.tol, w.flags, (const float*)nullptr, 0, p.ctl + kDPending);
     PMG_LAUNCH_CHECK();
   }
@@ -1058,9 +1114,9 @@ int pmg_dense_forward(const float* delta, const float* phi, const double* m, int
   return PMG_OK;
 }
 
-int pmg_dense_backward(const float* delta, const float* phi, const float* log_alpha, int64_t T,
+int pmg_dense_backward(const float* delta, const float* phi, const double* ll64, const double* log_alpha, int64_t T,
                        const pmg_dense_transition* tr, double likelihood_scale, int32_t chunk, int32_t warmup,
-                       double tol, float* P, float* gamma, float* log_gamma, float* rho, float* log_rho,
+                       double tol, float* P, float* gamma, float* log_gamma, float* rho, double* log_rho,
                        void* workspace, size_t workspace_bytes, void* stream) {
   DenseParams p;
   int rc = dense_params(p, tr, T, chunk, warmup, likelihood_scale, tol);
@@ -1071,6 +1127,7 @@ int pmg_dense_backward(const float* delta, const float* phi, const float* log_al
   DenseWork w = carve_dense(workspace, T, p.Lp, chunk);
   p.delta = delta;
   p.phi = phi;
+  p.ll64 = ll64;
   p.log_alpha_in = log_alpha;
   p.P = P;
   p.gamma = gamma;
@@ -1085,11 +1142,13 @@ int pmg_dense_backward(const float* delta, const float* phi, const float* log_al
   p.seg_chg = w.seg_chg;
   dense_kernel_t kf, kfr, kb, kbr;
   dense_kernels(p.Lp / kDNT, &kf, &kfr, &kb, &kbr);
-  PMG_HIP(hipMemsetAsync(p.ctl, 0, 16 * sizeof(int), st));
+  // per-call words; the timeout word (kDErr) is sticky until the host reads it
+  PMG_HIP(hipMemsetAsync(p.ctl, 0, kDErr * sizeof(int), st));
+  PMG_HIP(hipMemsetAsync(p.ctl + kDErr + 1, 0, (16 - kDErr - 1) * sizeof(int), st));
   hipLaunchKernelGGL(kb, dim3(p.M), dim3(kDNT), 0, st, p);
   PMG_LAUNCH_CHECK();
   if (p.M > 1) {
-    hipLaunchKernelGGL(k_dense_verify, dim3((p.M - 1 + 3) / 4), dim3(256), 0, st, w.b_in, (const float*)w.b_first, 0,
+    hipLaunchKernelGGL(k_dense_verify, dim3((p.M - 1 + 3) / 4), dim3(256), 0, st, w.b_in, (const double*)w.b_first, 0,
                        p.M - 2, 1, p.L, p.Lp, p.tol, w.flags, (const float*)nullptr, p.C, p.ctl + kDPending);
     PMG_LAUNCH_CHECK();
     hipLaunchKernelGGL(kbr, dim3(p.S), dim3(kDNT), 0, st, p);
@@ -1098,7 +1157,7 @@ int pmg_dense_backward(const float* delta, const float* phi, const float* log_al
   return PMG_OK;
 }
 
-int pmg_joint_log_accumulate(const float* log_alpha, const float* log_rho, int64_t T, int32_t L, double* logS,
+int pmg_joint_log_accumulate(const double* log_alpha, const double* log_rho, int64_t T, int32_t L, double* logS,
                              void* stream) {
   PMG_REQUIRE(log_alpha && log_rho && logS && T > 0 && L > 0, "pmg_joint_log_accumulate: bad argument");
   const int L2 = 2 * L;

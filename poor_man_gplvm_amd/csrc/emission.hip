@@ -97,7 +97,7 @@ __global__ void __launch_bounds__(512, 4) k_emission_i8(
     const int8_t* __restrict__ yq, const int8_t* __restrict__ qd,
     const double* __restrict__ lamsum, const double* __restrict__ gconst,
     const uint8_t* __restrict__ ma_latent, int64_t T, int64_t Tp, int L, int Lp, int Kp, int nLT,
-    float* __restrict__ delta, double* __restrict__ rblk) {
+    float* __restrict__ delta, double* __restrict__ rblk, double* __restrict__ ll64) {
   __shared__ __attribute__((aligned(16))) int8_t sY[2][ET][EROW];
   __shared__ __attribute__((aligned(16))) int8_t sQ[2][kDig][EL][EROW];
   const int tid = threadIdx.x;
@@ -197,6 +197,9 @@ __global__ void __launch_bounds__(512, 4) k_emission_i8(
                                                                        nrow * nblk * 8, 0x00020000);
   const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(gconst + t0), (short)0,
                                                                        nrow * 8, 0x00020000);
+  // optional f64 ll rows (exact decodes): num_records 0 drops every store when absent
+  const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+      ll64 ? (void*)(ll64 + t0 * (int64_t)L) : (void*)delta, (short)0, ll64 ? nrow * L * 8 : 0, 0x00020000);
   const uint32_t kNoWrite = 0x80000000u;                // past any bound above
   const int trow0 = wt * 32 + 4 * h;
 #pragma unroll
@@ -214,6 +217,10 @@ __global__ void __launch_bounds__(512, 4) k_emission_i8(
     const float dv = (float)(v - mx);
     const uint32_t od = lvalid ? (uint32_t)(tr * L + l - l0 + l0) * 4u : kNoWrite;
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dv), rd, od, 0, 0);
+    const unsigned long long vu = (unsigned long long)__double_as_longlong(v);
+    const uint32_t ol = lvalid ? 2u * od : kNoWrite;
+    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)vu, rl, ol, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(vu >> 32), rl, ol + 4, 0, 0);
     const uint32_t orb = r == 0 ? (uint32_t)(tr * nblk + blk) * 8u : kNoWrite;
     const unsigned long long mu = (unsigned long long)__double_as_longlong(mx);
     __builtin_amdgcn_raw_buffer_store_b32((uint32_t)mu, rr, orb, 0, 0);
@@ -228,7 +235,7 @@ __global__ void __launch_bounds__(256) k_emission_f64(
     const float* __restrict__ y, const float* __restrict__ ma, int ma_2d,
     const double* __restrict__ tuning, double dt, const double* __restrict__ gconst,
     const uint8_t* __restrict__ ma_latent, int64_t T, int L, int N, int Lp,
-    float* __restrict__ delta, double* __restrict__ rblk) {
+    float* __restrict__ delta, double* __restrict__ rblk, double* __restrict__ ll64) {
   __shared__ double sYM[16][33];
   __shared__ double sM[16][33];
   __shared__ double sLG[32][65];
@@ -289,6 +296,7 @@ __global__ void __launch_bounds__(256) k_emission_f64(
     if (t < T) {
       if ((tx & 31) == 0 && l < Lp) rblk[t * nblk + (l >> 5)] = mx;
       if (l < L) delta[t * (int64_t)L + l] = (float)(v - mx);
+      if (ll64 && l < L) ll64[t * (int64_t)L + l] = v;
     }
   }
 }
@@ -359,7 +367,7 @@ int32_t* pmg_emission_range_flag(void* workspace, int64_t T, int32_t L, int32_t 
 int pmg_emission_poisson(const int8_t* yq, const double* gconst, const double* tuning64,
                          const float* ma_neuron_1d, const uint8_t* ma_latent, double dt,
                          int64_t T, int32_t L, int32_t N, int32_t Kp, float* delta,
-                         double* rblk, void* workspace, size_t workspace_bytes, void* stream) {
+                         double* rblk, double* ll64, void* workspace, size_t workspace_bytes, void* stream) {
   PMG_REQUIRE(T > 0 && L > 0 && N > 0, "pmg_emission_poisson: bad shape");
   PMG_REQUIRE(Kp == round_up(N, 128), "pmg_emission_poisson: Kp must be roundup(N,128)");
   PMG_REQUIRE(yq && gconst && tuning64 && delta && rblk && workspace, "pmg_emission_poisson: null");
@@ -378,7 +386,7 @@ int pmg_emission_poisson(const int8_t* yq, const double* gconst, const double* t
   const int64_t nTT = (T + ET - 1) / ET;
   const int64_t Tp = round_up(T, 64);   // rows of yq (pmg_spikes_prepare zero-pads to Tp)
   hipLaunchKernelGGL(k_emission_i8, dim3((unsigned)(nLT * nTT)), dim3(512), 0, st, yq, qd, lamsum,
-                     gconst, ma_latent, T, Tp, L, Lp, Kp, nLT, delta, rblk);
+                     gconst, ma_latent, T, Tp, L, Lp, Kp, nLT, delta, rblk, ll64);
   PMG_LAUNCH_CHECK();
   return PMG_OK;
 }
@@ -386,7 +394,7 @@ int pmg_emission_poisson(const int8_t* yq, const double* gconst, const double* t
 int pmg_emission_poisson_f64(const float* y, const double* gconst, const double* tuning64,
                              const float* ma_neuron, int32_t ma_is_2d, const uint8_t* ma_latent,
                              double dt, int64_t T, int32_t L, int32_t N, float* delta,
-                             double* rblk, void* workspace, size_t workspace_bytes, void* stream) {
+                             double* rblk, double* ll64, void* workspace, size_t workspace_bytes, void* stream) {
   (void)workspace;
   (void)workspace_bytes;
   PMG_REQUIRE(T > 0 && L > 0 && N > 0 && y && gconst && tuning64 && delta && rblk,
@@ -394,7 +402,7 @@ int pmg_emission_poisson_f64(const float* y, const double* gconst, const double*
   const int Lp = (int)round_up(L, 32);
   dim3 grid((unsigned)((T + 15) / 16), (unsigned)((L + 63) / 64));
   hipLaunchKernelGGL(k_emission_f64, grid, dim3(256), 0, as_stream(stream), y, ma_neuron,
-                     ma_is_2d, tuning64, dt, gconst, ma_latent, T, L, N, Lp, delta, rblk);
+                     ma_is_2d, tuning64, dt, gconst, ma_latent, T, L, N, Lp, delta, rblk, ll64);
   PMG_LAUNCH_CHECK();
   return PMG_OK;
 }

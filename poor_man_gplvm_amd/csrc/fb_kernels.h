@@ -61,7 +61,10 @@ template <int J> constexpr int pf_relax_bwd() { return J >= 16 ? 2 : (J >= 8 ? 4
 
 // Control words at the start of the scan workspace (int32), one block per direction
 // (forward at word 0, backward at word kCtlStride):
-//   +0 chunks recomputed, +1 relaxation rounds, +2 timeout flag   (zeroed by the main pass)
+//   +0 chunks recomputed, +1 relaxation rounds   (zeroed by the main pass)
+//   +2 timeout flag: sticky -- set by a relaxation whose grid barrier timed out, left
+//      set by later calls (whose relaxations then fail fast), cleared by the host after
+//      it has read it (DeviceEM.scan_status)
 //   +3 warm-up of the next main pass (adaptive scans; written by the relaxation kernel)
 //   +4 boundaries flagged by k_verify, +5 barrier arrivals,
 //   +6..+8 segment-end changes of rounds k % 3, +9 relaxation exits
@@ -125,6 +128,7 @@ struct FBParams {
   float* b_first;
   int* flags;
   int* ctl;       // this direction's control block
+  uint64_t spin;  // grid-barrier spin bound (real-time clock ticks; kSpinTicks unless a debug override)
   // relaxation: segments of G chunks, S segments; end states double-buffered by round
   float* seg_end;  // [2][S][2*Lpad]
   int* seg_chg;    // [2][S]
@@ -661,7 +665,6 @@ __device__ __forceinline__ void main_pass_reset(const FBParams& p) {
   if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) {
     p.ctl[kCtlRepairs] = 0;
     p.ctl[kCtlRounds] = 0;
-    p.ctl[kCtlErr] = 0;
   }
 }
 
@@ -689,7 +692,7 @@ __global__ void __launch_bounds__(64) k_forward(FBParams p_arg) {
 // counter): drain this wave's stores, agent-scope release, arrive, relaxed poll,
 // agent-scope acquire.  The spin is bounded (kSpinTicks of the real-time clock, or
 // another wave's timeout): on expiry the timeout word is set and false returned.
-__device__ __forceinline__ bool relax_barrier(int* ctl, int target) {
+__device__ __forceinline__ bool relax_barrier(int* ctl, int target, uint64_t spin) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   int ok = 1;
   if ((threadIdx.x & 63) == 0) {
@@ -700,7 +703,7 @@ __device__ __forceinline__ bool relax_barrier(int* ctl, int target) {
     while (__hip_atomic_load(ctl + kCtlArrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(2);
       if (__hip_atomic_load(ctl + kCtlErr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
-          __builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
+          __builtin_amdgcn_s_memrealtime() - t0 > spin) {
         __hip_atomic_store(ctl + kCtlErr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok = 0;
         break;
@@ -836,7 +839,7 @@ __device__ __forceinline__ void forward_relax(const FBParams& p, int j0, const f
       if (changed) st.save_state(p, p.seg_end + ((size_t)(k & 1) * p.S + s) * SZ, j0);
       relax_publish(p, k, s, changed);
       ++rounds;
-      if (!relax_barrier(p.ctl, (k + 1) * p.S)) break;
+      if (!relax_barrier(p.ctl, (k + 1) * p.S, p.spin)) break;
       if (ctl_load(p.ctl, kCtlChanged + k % 3) == 0) break;  // no segment end moved: all verified
       // round k+1: re-verify the first boundary against the left neighbour's new end state
       changed = false;
@@ -1208,7 +1211,7 @@ __device__ __forceinline__ void backward_relax(const FBParams& p, int j0, const 
       if (changed) st.save_state(p, p.seg_end + ((size_t)(k & 1) * p.S + s) * SZ, j0);
       relax_publish(p, k, s, changed);
       ++rounds;
-      if (!relax_barrier(p.ctl, (k + 1) * p.S)) break;
+      if (!relax_barrier(p.ctl, (k + 1) * p.S, p.spin)) break;
       if (ctl_load(p.ctl, kCtlChanged + k % 3) == 0) break;
       changed = false;
       if (s + 1 < p.S && p.seg_chg[(k & 1) * p.S + s + 1]) {

@@ -172,6 +172,7 @@ static int fill_params(FBParams& p, const pmg_transition* tr, int64_t T, int C, 
   p.ldm = 1;
   p.ws_stride = 0;
   p.adapt = 0;
+  p.spin = spin_ticks(kSpinTicks);
   for (int k = 0; k <= kMaxBand; ++k) p.g[k] = (k <= tr->band) ? tr->g[k] : 0.f;
   return PMG_OK;
 }
@@ -197,6 +198,18 @@ static int batch_params(FBParams& p, int R, int64_t T, int chunk, size_t workspa
   p.G = (p.M + S - 1) / S;
   p.S = (p.M + p.G - 1) / p.G;
   return PMG_OK;
+}
+
+// PMG_PHASE_SEGMENTS: an explicit relaxation segment count per sequence
+static void requested_segments(FBParams& p, int phase, int R) {
+  int S = (phase >> 16) & 0xfff;
+  if (S <= 0) return;
+  if (S > kRelaxMaxSeg) S = kRelaxMaxSeg;
+  const int cap = 2 * device_cus() / (R > 1 ? R : 1);   // all R S single-wave groups co-resident
+  if (S > cap) S = cap > 0 ? cap : 1;
+  if (S > p.M) S = p.M;
+  p.G = (p.M + S - 1) / S;
+  p.S = (p.M + p.G - 1) / p.G;
 }
 
 }  // namespace pmg
@@ -274,6 +287,7 @@ static int forward_impl(const float* delta, const float* phi, const double* m, i
   size_t slab = 0;
   rc = batch_params(p, R, T, chunk, workspace_bytes, &slab);
   if (rc) return rc;
+  requested_segments(p, phase, R);
   const int J = p.Lpad / 64, WP = pick_WP(tr->band);
   FBKernelSet ks;
   const bool have = fb_set(J, WP, &ks);
@@ -309,7 +323,7 @@ int pmg_forward_filter_phase(const float* delta, const float* phi, const double*
                              const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                              int32_t warmup, double tol, float* alpha, double* logc, double* logz,
                              void* workspace, size_t workspace_bytes, void* stream, int32_t phase) {
-  PMG_REQUIRE((phase & 3) != 0 && (phase & ~(7 | PMG_PHASE_ADAPTIVE_WARMUP)) == 0, "pmg_forward_filter_phase: phase %d",
+  PMG_REQUIRE((phase & 3) != 0 && (phase & ~PMG_PHASE_FLAG_BITS) == 0, "pmg_forward_filter_phase: phase %d",
               phase);
   return forward_impl(delta, phi, m, T, tr, likelihood_scale, chunk, warmup, tol, alpha, logc, logz,
                       workspace, workspace_bytes, stream, phase);
@@ -347,6 +361,7 @@ static int backward_impl(const float* delta, const float* phi, const float* alph
   size_t slab = 0;
   rc = batch_params(p, R, T, chunk, workspace_bytes, &slab);
   if (rc) return rc;
+  requested_segments(p, phase, R);
   const int J = p.Lpad / 64, WP = pick_WP(tr->band);
   FBKernelSet ks;
   const bool have = fb_set(J, WP, &ks);
@@ -380,7 +395,7 @@ int pmg_backward_smoother_phase(const float* delta, const float* phi, const floa
                                 const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                                 int32_t warmup, double tol, float* P, float* gamma, float* rho,
                                 void* workspace, size_t workspace_bytes, void* stream, int32_t phase) {
-  PMG_REQUIRE((phase & 3) != 0 && (phase & ~(3 | PMG_PHASE_ADAPTIVE_WARMUP)) == 0,
+  PMG_REQUIRE((phase & 3) != 0 && (phase & ~(PMG_PHASE_FLAG_BITS & ~4)) == 0,
               "pmg_backward_smoother_phase: phase %d", phase);
   return backward_impl(delta, phi, alpha, T, tr, likelihood_scale, chunk, warmup, tol, P, gamma, rho,
                        workspace, workspace_bytes, stream, phase);
@@ -396,7 +411,7 @@ int pmg_forward_filter_batched(const float* delta, const float* phi, const doubl
                                const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                                int32_t warmup, double tol, float* alpha, double* logc, double* logz,
                                void* workspace, size_t workspace_bytes, void* stream, int32_t phase) {
-  PMG_REQUIRE((phase & 3) != 0 && (phase & ~(7 | PMG_PHASE_ADAPTIVE_WARMUP)) == 0,
+  PMG_REQUIRE((phase & 3) != 0 && (phase & ~PMG_PHASE_FLAG_BITS) == 0,
               "pmg_forward_filter_batched: phase %d", phase);
   return forward_impl(delta, phi, m, T, tr, likelihood_scale, chunk, warmup, tol, alpha, logc, logz,
                       workspace, workspace_bytes, stream, phase, R);
@@ -406,7 +421,7 @@ int pmg_backward_smoother_batched(const float* delta, const float* phi, const fl
                                   const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                                   int32_t warmup, double tol, float* P, float* gamma, void* workspace,
                                   size_t workspace_bytes, void* stream, int32_t phase) {
-  PMG_REQUIRE((phase & 3) != 0 && (phase & ~(3 | PMG_PHASE_ADAPTIVE_WARMUP)) == 0,
+  PMG_REQUIRE((phase & 3) != 0 && (phase & ~(PMG_PHASE_FLAG_BITS & ~4)) == 0,
               "pmg_backward_smoother_batched: phase %d", phase);
   return backward_impl(delta, phi, alpha, T, tr, likelihood_scale, chunk, warmup, tol, P, gamma, nullptr,
                        workspace, workspace_bytes, stream, phase, R);

@@ -40,7 +40,8 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 __global__ void __launch_bounds__(256) k_emission_gaussian(
     const float* __restrict__ y, const float* __restrict__ ma, int ma_2d, const double* __restrict__ tuning,
     const uint8_t* __restrict__ ma_latent, double inv_s, double c0, double dt, const double* __restrict__ dt_t,
-    int64_t T, int L, int N, int Lp, float* __restrict__ delta, double* __restrict__ rblk) {
+    int64_t T, int L, int N, int Lp, float* __restrict__ delta, double* __restrict__ rblk,
+    double* __restrict__ ll64) {
   __shared__ float sY[64][33];     // y and m stay f32 (their f64 product is exact)
   __shared__ float sM[64][33];
   __shared__ double sTu[32][65];   // mu = tuning * dt (f64); mu^2 is formed at use
@@ -133,6 +134,7 @@ __global__ void __launch_bounds__(256) k_emission_gaussian(
         for (int u = 0; u < 2; ++u) {
           const int l = lb + 16 * u + (lane & 15);
           if (l < L) delta[t * (int64_t)L + l] = (float)(v[u] - mx);
+          if (ll64 && l < L) ll64[t * (int64_t)L + l] = v[u];
         }
       }
     }
@@ -254,14 +256,14 @@ int pmg_tuning_linear(const float* basis, const double* W, int32_t L, int32_t NB
 
 int pmg_emission_gaussian(const float* y, const double* tuning64, const float* ma_neuron, int32_t ma_is_2d,
                           const uint8_t* ma_latent, double noise_std, double dt, int64_t T, int32_t L, int32_t N,
-                          float* delta, double* rblk, void* stream) {
+                          float* delta, double* rblk, double* ll64, void* stream) {
   PMG_REQUIRE(T > 0 && L > 0 && N > 0 && y && tuning64 && delta && rblk, "pmg_emission_gaussian: bad args");
   PMG_REQUIRE(noise_std > 0.0, "pmg_emission_gaussian: noise_std must be > 0");
   const int Lp = (int)round_up(L, 32);
   const double c0 = -log(noise_std) - 0.5 * log(2.0 * M_PI);
   dim3 grid((unsigned)((T + 63) / 64), (unsigned)((L + 63) / 64));
   hipLaunchKernelGGL(k_emission_gaussian, grid, dim3(256), 0, as_stream(stream), y, ma_neuron, ma_is_2d, tuning64,
-                     ma_latent, 1.0 / noise_std, c0, dt, nullptr, T, L, N, Lp, delta, rblk);
+                     ma_latent, 1.0 / noise_std, c0, dt, nullptr, T, L, N, Lp, delta, rblk, ll64);
   PMG_LAUNCH_CHECK();
   return PMG_OK;
 }
@@ -276,7 +278,7 @@ int pmg_emission_gaussian_dt(const float* y, const double* tuning64, const float
   const double c0 = -log(noise_std) - 0.5 * log(2.0 * M_PI);
   dim3 grid((unsigned)((T + 63) / 64), (unsigned)((L + 63) / 64));
   hipLaunchKernelGGL(k_emission_gaussian, grid, dim3(256), 0, as_stream(stream), y, ma_neuron, ma_is_2d, tuning64,
-                     ma_latent, 1.0 / noise_std, c0, 1.0, dt_t, T, L, N, Lp, delta, rblk);
+                     ma_latent, 1.0 / noise_std, c0, 1.0, dt_t, T, L, N, Lp, delta, rblk, nullptr);
   PMG_LAUNCH_CHECK();
   return PMG_OK;
 }

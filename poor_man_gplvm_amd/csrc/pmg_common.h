@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "../../include/pmg.h"
@@ -43,6 +44,15 @@ void set_error(const char* fmt, ...);
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 static inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+// Spin bound of the persistent kernels' grid barriers, in 100 MHz real-time clock
+// ticks: `def` (2 s) unless PMG_DEBUG_SPIN_TICKS overrides it (tests force a timeout
+// with a tiny bound to check that the host raises on the sticky timeout word).
+static inline uint64_t spin_ticks(uint64_t def) {
+  const char* e = getenv("PMG_DEBUG_SPIN_TICKS");
+  if (!e || !*e) return def;
+  return (uint64_t)strtoull(e, nullptr, 10);
+}
 
 // workspace carving: 256-byte aligned slices
 struct Carver {

@@ -70,6 +70,17 @@ class ScanConfig:
     device_adaptive: bool = True  # PMG_PHASE_ADAPTIVE_WARMUP: after a pass where > 1/8 of the chunk
                                   # boundaries failed (the first EM iterations), the next main pass
                                   # of that direction warms up 256 steps (device-side decision)
+    relax_segments: int = 0       # relaxation segments per sequence (0: #CUs, or #CUs / R for R
+                                  # batched restarts; PMG_PHASE_SEGMENTS).  The repaired states depend
+                                  # on the segment grid, so a single fit with #CUs / R segments
+                                  # reproduces restart r of an R-restart batch bit for bit
+    decode_exact: bool = True     # decode_latent / _decode_latent (the calls that return the pairwise
+                                  # joint) run the dense log-domain scans with the full kernel: every
+                                  # row of p_transition_* is then the reference's conditional, also for
+                                  # latents the posterior never visits (their linear-space counts
+                                  # underflow, and the far kernel entries the band drops decide them).
+                                  # False: the banded linear-space scans (faster; those rows fall back
+                                  # to the prior transition, core.JOINT_COUNT_FLOOR)
 
     def chunk_for(self, T):
         if self.chunk:
@@ -271,7 +282,8 @@ class DeviceEM:
         self._invz = None
         self.dense = False          # transition held by the dense log-domain scans
         self.ws_dense = None
-        self.log_alpha = None       # (T, 2, L) log filter state (dense scans)
+        self.log_alpha = None       # (T, 2, L) f64 log filter state (dense scans)
+        self.ll64 = None            # (T, L) f64 unsplit ll (dense scans; None: not written)
         self.alpha_bits = 0         # phase bits of the last forward (PHASE_NO_JUMP_ROWS or 0)
         # device-side adaptive warm-up across the E-steps of ONE fit (run_em sets it; a
         # decode is a single E-step whose result must not depend on earlier calls)
@@ -286,6 +298,10 @@ class DeviceEM:
 
     def _t(self, name):
         return self.timer(name) if self.timer is not None else _NO_TIMER
+
+    def _seg_bits(self):
+        """PMG_PHASE_SEGMENTS of ScanConfig.relax_segments (0: the library default)."""
+        return nat.phase_segments(self.scan.relax_segments)
 
     # ------------------------------------------------------------------ setup
     def set_transition(self, tr):
@@ -334,9 +350,12 @@ class DeviceEM:
         if need == 0:
             raise nat.NativeError(f"n_latent_bin={self.L} unsupported by the dense scans (max 1024)")
         if self.ws_dense is None or self.ws_dense.numel() < need:
-            self.ws_dense = torch.empty(need, dtype=torch.uint8, device=self.dev)
+            # zero-filled: it holds the sticky relaxation timeout words (include/pmg.h)
+            self.ws_dense = torch.zeros(need, dtype=torch.uint8, device=self.dev)
         if self.log_alpha is None:
-            self.log_alpha = torch.empty((self.T, 2, self.L), dtype=torch.float32, device=self.dev)
+            self.log_alpha = torch.empty((self.T, 2, self.L), dtype=torch.float64, device=self.dev)
+        if self.ll64 is None:   # the emission writes the unsplit f64 ll for the dense scans
+            self.ll64 = torch.empty((self.T, self.L), dtype=torch.float64, device=self.dev)
 
     def set_ma_latent(self, ma_latent):
         if ma_latent is None:
@@ -488,19 +507,20 @@ class DeviceEM:
             nat.check(self.lib.pmg_emission_gaussian(nat.ptr(sp.y), nat.ptr(self.tuning64), nat.ptr(sp.ma),
                                                      int(sp.ma_2d), nat.ptr(self.ma_latent), float(self.noise_std),
                                                      float(dt), self.T, self.L, self.N, nat.ptr(self.delta),
-                                                     nat.ptr(self.rblk), sh), "pmg_emission_gaussian")
+                                                     nat.ptr(self.rblk), nat.ptr(self.ll64), sh),
+                      "pmg_emission_gaussian")
         elif sp.int_path:
             ma1 = sp.ma if (sp.ma is not None and not sp.ma_2d) else None
             nat.check(self.lib.pmg_emission_poisson(nat.ptr(sp.yq), nat.ptr(sp.gconst), nat.ptr(self.tuning64),
                                                     nat.ptr(ma1), nat.ptr(self.ma_latent), float(dt), self.T,
                                                     self.L, self.N, sp.Kp, nat.ptr(self.delta),
-                                                    nat.ptr(self.rblk), nat.ptr(self.ws_em),
+                                                    nat.ptr(self.rblk), nat.ptr(self.ll64), nat.ptr(self.ws_em),
                                                     self.ws_em.numel(), sh), "pmg_emission_poisson")
         else:
             nat.check(self.lib.pmg_emission_poisson_f64(nat.ptr(sp.y), nat.ptr(sp.gconst), nat.ptr(self.tuning64),
                                                         nat.ptr(sp.ma), int(sp.ma_2d), nat.ptr(self.ma_latent),
                                                         float(dt), self.T, self.L, self.N, nat.ptr(self.delta),
-                                                        nat.ptr(self.rblk), nat.ptr(self.ws_em),
+                                                        nat.ptr(self.rblk), nat.ptr(self.ll64), nat.ptr(self.ws_em),
                                                         self.ws_em.numel(), sh), "pmg_emission_poisson_f64")
 
     def _adapt_warmup(self):
@@ -553,7 +573,8 @@ class DeviceEM:
         if self.dense:
             with self._t('forward_filter'):      # main pass + verify + relaxation + logZ
                 nat.check(self.lib.pmg_dense_forward(
-                    nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.mref), self.T, ctypes.byref(self._tr_d),
+                    nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.ll64), nat.ptr(self.mref), self.T,
+                    ctypes.byref(self._tr_d),
                     float(likelihood_scale), self.Cd, int(self.warm[0]), float(self.scan.tol),
                     nat.ptr(self.alpha), nat.ptr(self.log_alpha), nat.ptr(self.logc), nat.ptr(logz_out),
                     nat.ptr(self.ws_dense), self.ws_dense.numel(), nat.stream_handle()), "pmg_dense_forward")
@@ -569,15 +590,17 @@ class DeviceEM:
         with self._t('forward_filter'):          # main chunk-parallel pass (k_forward)
             nat.check(self.lib.pmg_forward_filter_phase(*args, 1 | ad | self.alpha_bits), "pmg_forward_filter")
         with self._t('forward_repair'):          # verify / relaxation / logZ
-            nat.check(self.lib.pmg_forward_filter_phase(*args, 2 | ad | self.alpha_bits), "pmg_forward_filter")
+            nat.check(self.lib.pmg_forward_filter_phase(*args, 2 | ad | self.alpha_bits | self._seg_bits()),
+                      "pmg_forward_filter")
 
     def backward(self, likelihood_scale, P=True, gamma=None, rho=None, log_gamma=None):
-        """rho: the joint partner; with the dense scans it is written as log(rho)
+        """rho: the joint partner; with the dense scans it is written as log(rho), f64
         (see joint_log)."""
         if self.dense:
             with self._t('backward_smoother'):
                 nat.check(self.lib.pmg_dense_backward(
-                    nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.log_alpha), self.T, ctypes.byref(self._tr_d),
+                    nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.ll64), nat.ptr(self.log_alpha), self.T,
+                    ctypes.byref(self._tr_d),
                     float(likelihood_scale), self.Cd, int(self.warm[1]), float(self.scan.tol),
                     nat.ptr(self.P) if P else None, nat.ptr(gamma), nat.ptr(log_gamma), None, nat.ptr(rho),
                     nat.ptr(self.ws_dense), self.ws_dense.numel(), nat.stream_handle()), "pmg_dense_backward")
@@ -593,7 +616,7 @@ class DeviceEM:
         with self._t('backward_smoother'):       # main chunk-parallel pass (k_backward)
             nat.check(self.lib.pmg_backward_smoother_phase(*args, 1 | ad), "pmg_backward_smoother")
         with self._t('backward_repair'):         # verify / relaxation
-            nat.check(self.lib.pmg_backward_smoother_phase(*args, 2 | ad), "pmg_backward_smoother")
+            nat.check(self.lib.pmg_backward_smoother_phase(*args, 2 | ad | self._seg_bits()), "pmg_backward_smoother")
 
     def e_step(self, likelihood_scale, logz_out, gamma=None, rho=None, log_gamma=None, keep_alpha=None):
         """keep_alpha (default: whenever a posterior output is requested): write alpha in full."""
@@ -607,11 +630,26 @@ class DeviceEM:
 
     def repairs(self):
         """(forward, backward) chunks recomputed by the last scans' relaxation (device
-        read: syncs).  Raises if a relaxation kernel's bounded grid barrier timed out."""
-        r = self.ctl_words().cpu().numpy()
-        if r[nat.CTL_FWD + nat.CTL_ERR] or r[nat.CTL_BWD + nat.CTL_ERR]:
-            raise nat.NativeError("scan relaxation: grid barrier timed out (results invalid)")
+        read: syncs).  Raises if a relaxation kernel's bounded grid barrier timed out
+        since the last check (the sticky timeout words; cleared here)."""
+        w = self.ctl_words()
+        r = w.cpu().numpy()
+        _raise_on_timeout(w, r, "scan relaxation")
         return int(r[nat.CTL_FWD + nat.CTL_REPAIRS]), int(r[nat.CTL_BWD + nat.CTL_REPAIRS])
+
+    def scan_status(self):
+        """Raise if any scan relaxation since the last check timed out in its bounded grid
+        barrier (its outputs are invalid); the sticky timeout words are cleared.  Device
+        read: syncs."""
+        w = self.ctl_words()
+        _raise_on_timeout(w, w.cpu().numpy(), "scan relaxation")
+
+    def check_status(self):
+        """Every sticky device error of the calls since the last check: the scans'
+        timeout words and (integer-path Poisson emission) the digit-range flag."""
+        self.scan_status()
+        if self.noise_std is None:
+            self.emission_status()
 
     def relax_rounds(self):
         """(forward, backward) relaxation rounds of the last scans (device read: syncs)."""
@@ -639,6 +677,17 @@ class DeviceEM:
                                                 nat.ptr(ws), ws.numel(), nat.stream_handle()),
                   "pmg_joint_accumulate")
         return S
+
+
+def _raise_on_timeout(words, host, what):
+    """words: a (CTL_WORDS,) int32 device view of a scan control block pair; host: its
+    values.  A set timeout word is cleared (it is sticky on the device) and raised."""
+    bad = [d for d in (nat.CTL_FWD, nat.CTL_BWD) if host[d + nat.CTL_ERR]]
+    if bad:
+        for d in bad:
+            words[d + nat.CTL_ERR] = 0
+        raise nat.NativeError(f"{what}: grid barrier timed out (results of the calls since the last check are "
+                              "invalid)")
 
 
 def _flag_view(lib, ws, T, L, N):
@@ -734,6 +783,7 @@ class RestartBatchEM:
         self.ma_latent = None
 
     _t = DeviceEM._t
+    _seg_bits = DeviceEM._seg_bits
 
     def set_transition(self, tr):
         if isinstance(tr, DenseTransition):
@@ -819,13 +869,13 @@ class RestartBatchEM:
                 ma1 = sp.ma if (sp.ma is not None and not sp.ma_2d) else None
                 nat.check(self.lib.pmg_emission_poisson(nat.ptr(sp.yq), nat.ptr(sp.gconst), nat.ptr(self.tuning64),
                                                         nat.ptr(ma1), nat.ptr(self.ma_latent), 1.0, T, LA, N, sp.Kp,
-                                                        nat.ptr(self.delta), nat.ptr(self.rblk), nat.ptr(self.ws_em),
+                                                        nat.ptr(self.delta), nat.ptr(self.rblk), None, nat.ptr(self.ws_em),
                                                         self.ws_em.numel(), sh), "pmg_emission_poisson")
             else:
                 nat.check(self.lib.pmg_emission_poisson_f64(nat.ptr(sp.y), nat.ptr(sp.gconst), nat.ptr(self.tuning64),
                                                             nat.ptr(sp.ma), int(sp.ma_2d), nat.ptr(self.ma_latent),
                                                             1.0, T, LA, N, nat.ptr(self.delta), nat.ptr(self.rblk),
-                                                            nat.ptr(self.ws_em), self.ws_em.numel(), sh),
+                                                            None, nat.ptr(self.ws_em), self.ws_em.numel(), sh),
                           "pmg_emission_poisson_f64")
         with self._t('emission_rowref'):
             nat.check(self.lib.pmg_emission_rowref_batched(nat.ptr(self.rblk), T, self.R * self.nblk, self.R,
@@ -843,7 +893,8 @@ class RestartBatchEM:
         with self._t('forward_filter'):
             nat.check(self.lib.pmg_forward_filter_batched(*args, 1 | bits), "pmg_forward_filter_batched")
         with self._t('forward_repair'):
-            nat.check(self.lib.pmg_forward_filter_batched(*args, 2 | bits), "pmg_forward_filter_batched")
+            nat.check(self.lib.pmg_forward_filter_batched(*args, 2 | bits | self._seg_bits()),
+                      "pmg_forward_filter_batched")
 
     def backward(self, likelihood_scale, gamma=None):
         """gamma: optional (R, T, 2, L) f32 posterior output."""
@@ -854,7 +905,8 @@ class RestartBatchEM:
         with self._t('backward_smoother'):
             nat.check(self.lib.pmg_backward_smoother_batched(*args, 1 | ad), "pmg_backward_smoother_batched")
         with self._t('backward_repair'):
-            nat.check(self.lib.pmg_backward_smoother_batched(*args, 2 | ad), "pmg_backward_smoother_batched")
+            nat.check(self.lib.pmg_backward_smoother_batched(*args, 2 | ad | self._seg_bits()),
+                      "pmg_backward_smoother_batched")
 
     def e_step(self, likelihood_scale, logz_out, gamma=None):
         self.emission(likelihood_scale)
@@ -879,8 +931,8 @@ class RestartBatchEM:
         """[(forward, backward) chunks recomputed] per restart (device read: syncs)."""
         out = []
         for r in range(self.R):
-            w = self.ctl_words(r).cpu().numpy()
-            if w[nat.CTL_FWD + nat.CTL_ERR] or w[nat.CTL_BWD + nat.CTL_ERR]:
-                raise nat.NativeError(f"scan relaxation (restart {r}): grid barrier timed out (results invalid)")
+            words = self.ctl_words(r)
+            w = words.cpu().numpy()
+            _raise_on_timeout(words, w, f"scan relaxation (restart {r})")
             out.append((int(w[nat.CTL_FWD + nat.CTL_REPAIRS]), int(w[nat.CTL_BWD + nat.CTL_REPAIRS])))
         return out

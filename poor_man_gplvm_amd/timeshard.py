@@ -284,7 +284,7 @@ def speculative_adam(run, snapshot, restore, allreduce, maxiter, tol, batch=16):
     """Neuron-sharded Adam loop with the reference's global stop rule.
 
     Every rank runs its own neuron slice (the loss and the gradient norm are sums over
-    neurons plus per-weight prior terms), `batch` bodies per launch with tol = 0, then
+    neurons plus per-weight prior terms), `batch` bodies per launch with tol < 0 (no local stop), then
     ONE all-reduce of the batch's per-body loss / squared-gradient partials decides on
     the global sums, in the same order on every rank.  A stop inside the batch restores
     the batch-start snapshot and re-runs the bodies up to the stopping one, so every rank
@@ -292,7 +292,7 @@ def speculative_adam(run, snapshot, restore, allreduce, maxiter, tol, batch=16):
     persistent kernel's exact-F refresh, every 16 bodies, on the same bodies).
 
       run(kmax) -> list over local slices of (n_iter, loss_hist, err_hist) host arrays
-                   (the kernel's outputs for maxiter = kmax, tol = 0)
+                   (the kernel's outputs for maxiter = kmax, tol < 0)
       snapshot() / restore(): all local slices' (W, mu, nu, count)
       allreduce(x) -> sum over ranks of the local sum x (host float64 arrays)
     Returns dict(n_iter, final_loss, final_error, loss_history, error_history, loss0)."""
@@ -307,7 +307,9 @@ def speculative_adam(run, snapshot, restore, allreduce, maxiter, tol, batch=16):
     while True:
         snap = snapshot()
         outs = run(batch + 1)
-        nb = min(int(o[0]) for o in outs) - 1          # bodies this launch ran (batch unless rel == 0)
+        nb = int(outs[0][0]) - 1                        # bodies this launch ran: exactly `batch` (tol < 0)
+        if any(int(o[0]) - 1 != nb for o in outs):
+            raise RuntimeError("speculative_adam: local slices ran different body counts")
         loc = np.zeros((2, nb))
         for n_iter, lhist, ehist in outs:
             loc[0] += np.asarray(lhist[1:nb + 1], np.float64)
@@ -386,7 +388,8 @@ class ShardEM(DeviceEM):
                 nat.ptr(self.logc), nat.ptr(logz_scratch), nat.ptr(self.ws_fb), self.ws_fb.numel(),
                 nat.stream_handle())
         with self._t('forward_carry'):
-            nat.check(self.lib.pmg_forward_filter_phase(*args, 2 | self.alpha_bits), "pmg_forward_filter")
+            nat.check(self.lib.pmg_forward_filter_phase(*args, 2 | self.alpha_bits | self._seg_bits()),
+                      "pmg_forward_filter")
 
     def backward_phase2(self, likelihood_scale, P=True, gamma=None):
         args = (nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.alpha), self.T, ctypes.byref(self._tr_c),
@@ -394,7 +397,7 @@ class ShardEM(DeviceEM):
                 nat.ptr(self.P) if P else None, nat.ptr(gamma), None, nat.ptr(self.ws_fb),
                 self.ws_fb.numel(), nat.stream_handle())
         with self._t('backward_carry'):
-            nat.check(self.lib.pmg_backward_smoother_phase(*args, 2), "pmg_backward_smoother")
+            nat.check(self.lib.pmg_backward_smoother_phase(*args, 2 | self._seg_bits()), "pmg_backward_smoother")
 
     def repair_count(self):
         """(forward, backward) chunk-recompute counters (device tensor)."""
@@ -520,7 +523,10 @@ class TimeShardedEM:
         eh_dev = torch.zeros_like(lh_dev)
 
         def run(kmax):
-            c = AdamConfig(lr=cfg.lr, maxiter=kmax, tol=0.0, prior_std=cfg.prior_std, b1=cfg.b1, b2=cfg.b2,
+            # tol < 0: the local stop rule (rel > tol) never fires, so every rank runs exactly
+            # kmax - 1 bodies (a repeated partial loss, rel == 0, would stop a tol = 0 loop
+            # early on one rank only and desynchronise the loss all-reduce)
+            c = AdamConfig(lr=cfg.lr, maxiter=kmax, tol=-1.0, prior_std=cfg.prior_std, b1=cfg.b1, b2=cfg.b2,
                            eps=cfg.eps, eps_root=cfg.eps_root)
             outs = []
             for s, d in zip(self.shards, sl):
@@ -599,6 +605,8 @@ def run_em_timesharded(y, params, basis, log_posterior_init, n_iter, transition,
     parts = comm.gather_rank0(own) if gather else [o.cpu() for o in own]
     s_ = stats.cpu().numpy()
     lhn, ehn, lz = lh.cpu().numpy(), eh.cpu().numpy(), logz.cpu().numpy()
+    for s in eng.shards:            # sticky device errors of every shard's calls
+        s.emission_status()
     info = {'layouts': lays, 'carry_rounds': rounds, 'params64': Ws[0].cpu().numpy(),
             'repairs': [s.repairs() for s in eng.shards], 'chunk': lays[0].chunk,
             'warmup': [list(s.warm) for s in eng.shards]}

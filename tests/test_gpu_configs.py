@@ -68,7 +68,11 @@ def test_c2_decode_vs_oracle(c2):
     _argmax_rows_match(r['posterior_latent_marg'], f['dec_argmax'], f['dec_posterior_latent_rows'], rows)
     np.testing.assert_allclose(r['log_one_step_predictive_marginals_all'], f['dec_log_one_step'], rtol=1e-5,
                                atol=1e-5)
-    np.testing.assert_allclose(r['p_transition_dynamics'], f['dec_p_transition_dynamics'], rtol=1e-4)
+    # every transition row is the reference's conditional, also the latents the posterior
+    # never visits (ScanConfig.decode_exact: dense log-domain scans, f64 joint)
+    np.testing.assert_allclose(r['p_transition_dynamics'], f['dec_p_transition_dynamics'], rtol=1e-5, atol=1e-12)
+    for k in ('p_transition_latent', 'p_transition_full', 'p_joint_latent', 'p_joint_dynamics'):
+        np.testing.assert_allclose(r[k], f['dec_' + k].astype(np.float64), rtol=1e-5, atol=1e-12, err_msg=k)
 
 
 def test_c2_one_em_iteration_vs_oracle(c2):
@@ -89,6 +93,74 @@ def test_c2_one_em_iteration_vs_oracle(c2):
     assert dev < 1e-5 and dev < 0.1 * ref_noise, (dev, ref_noise)
     _argmax_rows_match(plm, f['em_argmax'], exact, rows)
     np.testing.assert_allclose(plm.sum(0), f['em_tw'], rtol=1e-5)
+
+
+@pytest.fixture(scope="module")
+def c3():
+    f = np.load(os.path.join(HERE, 'golden', 'c3_sample.npz'))
+    d = make(int(f['N']), int(f['L']), int(f['T']))
+    assert float(d['y'].astype(np.float64).sum()) == float(f['y_sum'])
+    assert abs(float(d['lp0'].astype(np.float64).sum()) - float(f['lp0_sum'])) <= 1e-9 * abs(float(f['lp0_sum']))
+    assert abs(float(d['tuning'].sum()) - float(f['tuning_true_sum'])) <= 1e-12 * abs(float(f['tuning_true_sum']))
+    return f, d
+
+
+def test_c3_decode_vs_oracle(c3):
+    """The headline shape (N=512, L=512, 79 basis columns) at T=5000 against the f64
+    oracle: log marginal, one-step marginals, posteriors on 512 sampled rows, argmax of
+    every row, and every row of p_transition_latent / _dynamics plus the full transition
+    rows of 32 sampled source latents at 1e-5."""
+    import poor_man_gplvm_amd as P
+    f, d = c3
+    L = int(f['L'])
+    m = P.PoissonGPLVMJump1D(int(f['N']), n_latent_bin=L, tuning_lengthscale=10.)
+    r = m.decode_latent(d['y'], tuning=d['tuning'])
+    rows, src = f['rows'], f['src']
+    assert abs(r['log_marginal_final'] - float(f['dec_log_marginal_final'])) <= 1e-7 * abs(float(f['dec_log_marginal_final']))
+    close_prob(r['posterior_latent_marg'][rows], f['dec_posterior_latent_rows'].astype(np.float64))
+    close_prob(r['posterior_dynamics_marg'][rows], f['dec_posterior_dynamics_rows'].astype(np.float64))
+    _argmax_rows_match(r['posterior_latent_marg'], f['dec_argmax'], f['dec_posterior_latent_rows'], rows)
+    np.testing.assert_allclose(r['log_one_step_predictive_marginals_all'], f['dec_log_one_step'], rtol=1e-5,
+                               atol=1e-5)
+    np.testing.assert_allclose(r['p_transition_dynamics'], f['dec_p_transition_dynamics'], rtol=1e-5, atol=1e-12)
+    np.testing.assert_allclose(r['p_joint_dynamics'], f['dec_p_joint_dynamics'], rtol=1e-5, atol=1e-12)
+    np.testing.assert_allclose(r['p_transition_latent'], f['dec_p_transition_latent'].astype(np.float64),
+                               rtol=1e-5, atol=1e-12)
+    np.testing.assert_allclose(r['p_transition_full'][:, :, src, :], f['dec_p_transition_full_src'].astype(np.float64),
+                               rtol=1e-5, atol=1e-12)
+
+
+def test_c3_one_em_iteration_vs_oracle(c3):
+    """One EM iteration at the headline shape from (W0, lp0) under the reference's stop
+    rule (maxiter 1000, tol 1e-6): identical Adam iteration count, tuning rel 1e-5, log
+    marginal rel 1e-7, posterior within 1e-5 and 10 % of the fp32 reference-mimic's own
+    deviation (the bar of test_fit_em_fixed_iterations_golden), argmax exact."""
+    import poor_man_gplvm_amd as P
+    f, d = c3
+    L = int(f['L'])
+    m = P.PoissonGPLVMJump1D(int(f['N']), n_latent_bin=L, tuning_lengthscale=10.)
+    m.params = d['W0'].astype(np.float32)
+    res = m.fit_em(d['y'], n_iter=1, log_posterior_init=d['lp0'])
+    rows = f['rows']
+    assert res['m_step_res_l']['n_iter'] == list(f['em_m_n_iter'])
+    np.testing.assert_allclose(res['m_step_res_l']['final_loss'], f['em_m_final_loss'], rtol=1e-6)
+    np.testing.assert_allclose(res['log_marginal_l'], f['em_log_marginal_l'], rtol=1e-7)
+    plm = np.asarray(res['posterior_latent_marg'], np.float64)
+    exact = f['em_posterior_latent_rows'].astype(np.float64)
+    ref_noise = np.abs(f['mimic32_posterior_latent_rows'].astype(np.float64) - exact).max()
+    dev = np.abs(plm[rows] - exact).max()
+    assert dev < 1e-5 and dev < 0.1 * ref_noise, (dev, ref_noise)
+    _argmax_rows_match(plm, f['em_argmax'], exact, rows)
+    np.testing.assert_allclose(plm.sum(0), f['em_tw'], rtol=1e-5)
+    # Tuning: at this shape the 864-body Adam loop is chaotic at the f64 ulp: perturbing
+    # y_w by 1e-15 relative moves the f64 oracle's own tuning by 1.8e-5 (1e-13: 9e-6,
+    # 1e-9: 7.4e-5; tools/diag_mstep_conditioning.py, profiles/r03_mstep_conditioning.txt)
+    # and the fp32 reference-mimic lands 4.1e-2 away, so no implementation that is not
+    # the oracle's own f64 summation order can meet 1e-5 here.  Bar: 1e-4 (the f64
+    # perturbation floor) and 1 % of the reference-mimic's deviation.
+    tun_dev = np.max(np.abs(res['tuning'] / f['em_tuning'] - 1))
+    mimic_dev = np.max(np.abs(f['mimic32_tuning'].astype(np.float64) / f['em_tuning'] - 1))
+    assert tun_dev < 1e-4 and tun_dev < 0.01 * mimic_dev, (tun_dev, mimic_dev)
 
 
 def test_c4_time_sharded_vs_single():
@@ -118,19 +190,22 @@ def test_c5_restarts():
     for a, b in zip(ems, ems_again):
         np.testing.assert_array_equal(a['tuning'], b['tuning'])
         np.testing.assert_array_equal(a['posterior_latent_marg'], b['posterior_latent_marg'])
-    # restart 3 alone (one fit_em, same chunk grid as the batch): the same fit up to the
-    # relaxation's segment grid (CUs / 8 segments per restart in the batch, CUs alone),
-    # which moves repaired boundaries within the scan tolerance; after the second
-    # M-step that reaches the posterior through its tuning sensitivity,
-    # hence the multi-iteration EM bar of test_fit_em_fixed_iterations_golden
+    # restart 3 alone (one fit_em) on the batch's scan grid -- the same chunks and the same
+    # relaxation segment grid (#CUs / 8 segments per restart, ScanConfig.relax_segments):
+    # batching (stacked emission / suff-stats GEMMs, blockIdx.y scans, batched Adam) must
+    # not change the fit beyond f64 summation-order noise of the suff-stats split
     import poor_man_gplvm_amd as P
     C = models[0].fit_info['chunk']
-    cfg1 = dict(cfg, scan_config=P.ScanConfig(chunk=C, chunk_bwd=2 * C))
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    cfg1 = dict(cfg, scan_config=P.ScanConfig(chunk=C, chunk_bwd=2 * C, relax_segments=max(1, cus // R)))
     _, ems2 = MS.fit_model_one_config(cfg1, d['y'], key=[keys[3]], fit_kwargs=kw)
     assert ems2[0]['m_step_res_l']['n_iter'] == ems[3]['m_step_res_l']['n_iter']
-    np.testing.assert_allclose(ems2[0]['tuning'], ems[3]['tuning'], rtol=1e-5)
-    assert np.abs(ems2[0]['posterior_latent_marg'] - ems[3]['posterior_latent_marg']).max() <= 1e-5
+    np.testing.assert_allclose(ems2[0]['tuning'], ems[3]['tuning'], rtol=1e-5, atol=0)
+    close_prob(ems2[0]['posterior_latent_marg'], ems[3]['posterior_latent_marg'])
     argmax_match(ems2[0]['posterior_latent_marg'], ems[3]['posterior_latent_marg'])
+    print("c5 batched vs single: tuning max rel",
+          float(np.max(np.abs(ems2[0]['tuning'] / ems[3]['tuning'] - 1))),
+          "posterior max abs", float(np.abs(ems2[0]['posterior_latent_marg'] - ems[3]['posterior_latent_marg']).max()))
 
 
 def test_c5_restart_vs_oracle():

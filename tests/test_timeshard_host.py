@@ -152,7 +152,7 @@ def test_speculative_adam_matches_unsharded(maxiter, tol, world):
           for x, y in bnd]
 
     def run(kmax):
-        return [_kernel_mimic(d['W'], d['mu'], d['nu'], d['cnt'], kmax, 0.0, d['a'], d['c']) for d in sl]
+        return [_kernel_mimic(d['W'], d['mu'], d['nu'], d['cnt'], kmax, -1.0, d['a'], d['c']) for d in sl]
 
     def snapshot():
         return [(d['W'].copy(), d['mu'].copy(), d['nu'].copy(), list(d['cnt'])) for d in sl]
@@ -168,3 +168,15 @@ def test_speculative_adam_matches_unsharded(maxiter, tol, world):
     np.testing.assert_allclose(res['loss_history'], lh_ref, rtol=1e-13)
     np.testing.assert_allclose(res['error_history'], eh_ref, rtol=1e-13)
     assert res['final_loss'] == pytest.approx(lh_ref[-1], rel=1e-13)
+
+
+def test_speculative_adam_rejects_desynchronised_slices():
+    """Every local slice must run exactly `batch` bodies (tol < 0); a slice that stops
+    early would desynchronise the ranks' loss all-reduce, so it raises instead."""
+    from poor_man_gplvm_amd.timeshard import speculative_adam
+
+    def run(kmax):
+        return [(kmax, np.ones(kmax), np.ones(kmax)), (kmax - 3, np.ones(kmax - 3), np.ones(kmax - 3))]
+
+    with pytest.raises(RuntimeError):
+        speculative_adam(run, lambda: None, lambda s: None, lambda x: x, 1000, 1e-6)
