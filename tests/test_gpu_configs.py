@@ -14,8 +14,10 @@ C4 (N=1024, L=1024; a T=1e5 slice of the T=1e6 job): 8 time shards (virtual, one
 C5 (8 restarts, N=256, T=5e4, L=256 through model_selection_helper.fit_model_one_config,
   which batches a rank's restarts in one fit, core.fit_em_restarts): properties of every
   restart (finite, normalised, restarts differ, re-running the keys reproduces them bit
-  for bit, one restart alone on the same chunk grid gives the same fit) and one restart
-  against the f64 oracle at T=1500.
+  for bit, one restart alone on the batch's chunk and relaxation grid gives the same fit
+  bit for bit) and one restart against the f64 oracle at T=1500.
+C3 (N=512, L=512; T=5000): decode and one EM iteration against the f64 oracle fixture
+  (tests/golden/make_golden.py c3).
 """
 import os
 
@@ -145,22 +147,27 @@ def test_c3_one_em_iteration_vs_oracle(c3):
     assert res['m_step_res_l']['n_iter'] == list(f['em_m_n_iter'])
     np.testing.assert_allclose(res['m_step_res_l']['final_loss'], f['em_m_final_loss'], rtol=1e-6)
     np.testing.assert_allclose(res['log_marginal_l'], f['em_log_marginal_l'], rtol=1e-7)
+    # Tuning: at this shape the 864-body Adam loop is chaotic at the f64 ulp: perturbing
+    # y_w by 1e-15 relative moves the f64 oracle's own tuning by 1.8e-5 (1e-13: 9e-6,
+    # 1e-9: 2.7e-5; tools/diag_mstep_conditioning.py, profiles/r03_mstep_conditioning.txt)
+    # and the fp32 reference-mimic lands 4.1e-2 away, so no implementation that is not
+    # the oracle's own f64 summation order can meet 1e-5 here (measured: 3.4e-5).  Bar:
+    # 1e-4 (the f64 perturbation floor) and 1 % of the reference-mimic's deviation.
+    tun_dev = np.max(np.abs(res['tuning'] / f['em_tuning'] - 1))
+    mimic_dev = np.max(np.abs(f['mimic32_tuning'].astype(np.float64) / f['em_tuning'] - 1))
+    assert tun_dev < 1e-4 and tun_dev < 0.01 * mimic_dev, (tun_dev, mimic_dev)
+    # The posterior inherits that tuning spread (measured 6.5e-5 max abs against the
+    # mimic's 2.0e-2); the E-step itself is exact at this shape (test_c3_decode_vs_oracle,
+    # rel 1e-5 with the oracle's tuning).  Bar: 2e-4 and 1 % of the mimic's deviation.
     plm = np.asarray(res['posterior_latent_marg'], np.float64)
     exact = f['em_posterior_latent_rows'].astype(np.float64)
     ref_noise = np.abs(f['mimic32_posterior_latent_rows'].astype(np.float64) - exact).max()
     dev = np.abs(plm[rows] - exact).max()
-    assert dev < 1e-5 and dev < 0.1 * ref_noise, (dev, ref_noise)
-    _argmax_rows_match(plm, f['em_argmax'], exact, rows)
-    np.testing.assert_allclose(plm.sum(0), f['em_tw'], rtol=1e-5)
-    # Tuning: at this shape the 864-body Adam loop is chaotic at the f64 ulp: perturbing
-    # y_w by 1e-15 relative moves the f64 oracle's own tuning by 1.8e-5 (1e-13: 9e-6,
-    # 1e-9: 7.4e-5; tools/diag_mstep_conditioning.py, profiles/r03_mstep_conditioning.txt)
-    # and the fp32 reference-mimic lands 4.1e-2 away, so no implementation that is not
-    # the oracle's own f64 summation order can meet 1e-5 here.  Bar: 1e-4 (the f64
-    # perturbation floor) and 1 % of the reference-mimic's deviation.
-    tun_dev = np.max(np.abs(res['tuning'] / f['em_tuning'] - 1))
-    mimic_dev = np.max(np.abs(f['mimic32_tuning'].astype(np.float64) / f['em_tuning'] - 1))
-    assert tun_dev < 1e-4 and tun_dev < 0.01 * mimic_dev, (tun_dev, mimic_dev)
+    assert dev < 2e-4 and dev < 0.01 * ref_noise, (dev, ref_noise)
+    srt = np.sort(exact, axis=1)
+    clear = (srt[:, -1] - srt[:, -2]) > 1e-3
+    assert np.all(np.argmax(plm[rows], 1)[clear] == np.argmax(exact, 1)[clear])
+    np.testing.assert_allclose(plm.sum(0), f['em_tw'], rtol=1e-4)
 
 
 def test_c4_time_sharded_vs_single():
@@ -200,12 +207,10 @@ def test_c5_restarts():
     cfg1 = dict(cfg, scan_config=P.ScanConfig(chunk=C, chunk_bwd=2 * C, relax_segments=max(1, cus // R)))
     _, ems2 = MS.fit_model_one_config(cfg1, d['y'], key=[keys[3]], fit_kwargs=kw)
     assert ems2[0]['m_step_res_l']['n_iter'] == ems[3]['m_step_res_l']['n_iter']
-    np.testing.assert_allclose(ems2[0]['tuning'], ems[3]['tuning'], rtol=1e-5, atol=0)
-    close_prob(ems2[0]['posterior_latent_marg'], ems[3]['posterior_latent_marg'])
-    argmax_match(ems2[0]['posterior_latent_marg'], ems[3]['posterior_latent_marg'])
-    print("c5 batched vs single: tuning max rel",
-          float(np.max(np.abs(ems2[0]['tuning'] / ems[3]['tuning'] - 1))),
-          "posterior max abs", float(np.abs(ems2[0]['posterior_latent_marg'] - ems[3]['posterior_latent_marg']).max()))
+    # measured bit-identical (tuning, posterior, log marginals)
+    np.testing.assert_array_equal(ems2[0]['tuning'], ems[3]['tuning'])
+    np.testing.assert_array_equal(ems2[0]['posterior_latent_marg'], ems[3]['posterior_latent_marg'])
+    np.testing.assert_array_equal(ems2[0]['log_marginal_l'], ems[3]['log_marginal_l'])
 
 
 def test_c5_restart_vs_oracle():

@@ -43,10 +43,11 @@ def test_log_marginal_masked_vs_oracle(model, N, L, T, frac):
         _, logK = O.create_transition_prob_latent_1d(L, 1.0)
         ref = np.array([O.smooth_latent_only(d['y'], d['tuning'], logK, ma_latent=mk)[1] for mk in masks])
     np.testing.assert_allclose(got, ref, rtol=1e-7)
-    # the batched path (one emission, per-mask pmg_emission_latent_mask) vs one full
-    # masked decode per mask: the same up to delta's f32 rounding
+    # the batched path (one emission, per-mask pmg_emission_latent_mask, banded forward on
+    # (delta, rblk)) vs one full masked decode per mask (the exact decode: dense scans on
+    # the f64 ll): the same up to delta's f32 rounding (measured 3.3e-9 relative)
     full = [m.decode_latent(d['y'], tuning=d['tuning'], ma_latent=mk)['log_marginal_final'] for mk in masks]
-    np.testing.assert_allclose(got, full, rtol=1e-9)
+    np.testing.assert_allclose(got, full, rtol=2e-8)
     if model == "jump":
         ds = MS.get_downsampled_lml(m, d['y'], downsample_frac=frac, n_repeat=4, key=3, tuning=d['tuning'])
         np.testing.assert_allclose(ds['value'], np.mean(ref), rtol=1e-7)
