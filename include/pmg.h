@@ -109,6 +109,14 @@ int pmg_emission_poisson_f64(const float* y, const double* gconst, const double*
 /* 243-260) share one emission contraction.  Out of place.                                */
 int pmg_emission_latent_mask(const float* delta0, const double* rblk0, int64_t T, int32_t L,
                              const uint8_t* ma_latent, float* delta, double* rblk, void* stream);
+/* R masks at once (ma_latent (R, L) uint8, one row per mask), written side by side */
+/* as R stacked latent sets: delta (T, R*L), rblk (T, R*nblk), nblk = ceil(L/32):   */
+/* the layout of the batched scans (pmg_emission_rowref_batched, then              */
+/* pmg_forward_filter_batched).  Mask r's columns equal pmg_emission_latent_mask's  */
+/* output for ma_latent[r] bit for bit.  L % 32 == 0.                              */
+int pmg_emission_latent_mask_batched(const float* delta0, const double* rblk0, int64_t T, int32_t L,
+                                     const uint8_t* ma_latent, int32_t R, float* delta, double* rblk,
+                                     void* stream);
 /* Per-time reference: m[t] = max_b rblk[t,b], phi[t,b] = f32(s*(rblk[t,b]-m[t])) so that  */
 /* exp(s*ll[t,l] - s*m[t]) = exp(s*delta[t,l] + phi[t,l/32]).                              */
 int pmg_emission_rowref(const double* rblk, int64_t T, int32_t nblk, double likelihood_scale,
@@ -224,6 +232,11 @@ int pmg_backward_smoother(const float* delta, const float* phi, const float* alp
 /* d = 1 rows unwritten (their values are jump_t * e_t / S_t; the backward */
 /* rebuilds them), for callers that read only P / logZ (an EM iteration). */
 #define PMG_PHASE_NO_JUMP_ROWS 4
+/* Forward only: OR PMG_PHASE_NO_ALPHA into both phase calls to write no alpha at */
+/* all (logc / logZ only; no backward may follow on this workspace).  For the    */
+/* log-marginal-only passes of model_selection_helper.get_downsampled_lml        */
+/* (model_selection_helper.py:243-260, which reads log_marginal_final only).     */
+#define PMG_PHASE_NO_ALPHA 16
 /* Either direction: OR PMG_PHASE_ADAPTIVE_WARMUP into the phase-1 and the  */
 /* phase-2 call of each E-step to let the device pick the warm-up: when    */
 /* more than 1/8 of a pass's chunk boundaries failed verification (a slowly */
@@ -238,7 +251,7 @@ int pmg_backward_smoother(const float* delta, const float* phi, const float* alp
 /* so two calls agree bit for bit only on the same segment grid: a single fit    */
 /* run with S = #CUs / R reproduces restart r of an R-restart batch.             */
 #define PMG_PHASE_SEGMENTS(S) ((int32_t)((S) & 0xfff) << 16)
-#define PMG_PHASE_FLAG_BITS (7 | PMG_PHASE_ADAPTIVE_WARMUP | (0xfff << 16))
+#define PMG_PHASE_FLAG_BITS (7 | PMG_PHASE_ADAPTIVE_WARMUP | PMG_PHASE_NO_ALPHA | (0xfff << 16))
 int pmg_forward_filter_phase(const float* delta, const float* phi, const double* m, int64_t T,
                              const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                              int32_t warmup, double tol, float* alpha, double* logc, double* logz,

@@ -14,7 +14,8 @@ import os
 import torch  # noqa: F401  (loads the HIP runtime before the library)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "csrc", "libpmg_hip.so")
+# PMG_LIB_PATH: an alternative build of the same ABI (experiment variants, tools/build_variant.sh)
+LIB_PATH = os.environ.get("PMG_LIB_PATH") or os.path.join(_HERE, "csrc", "libpmg_hip.so")
 
 PMG_MAX_BAND = 32
 # pmg_fwdbwd_state slots (include/pmg.h)
@@ -27,6 +28,8 @@ CTL_REPAIRS, CTL_ROUNDS, CTL_ERR, CTL_WARM = 0, 1, 2, 3
 PHASE_NO_JUMP_ROWS = 4
 # both phase calls of an E-step: the device lengthens the next warm-up after a cascade (PMG_PHASE_ADAPTIVE_WARMUP)
 PHASE_ADAPTIVE_WARMUP = 8
+# forward, both phase calls: no alpha written at all (logc / logZ only; PMG_PHASE_NO_ALPHA)
+PHASE_NO_ALPHA = 16
 ABI_VERSION = 2
 
 
@@ -45,7 +48,7 @@ EXPORTED_SYMBOLS = (
     "pmg_forward_filter", "pmg_backward_smoother", "pmg_fwdbwd_repair_counter_offset",
     "pmg_forward_filter_phase", "pmg_backward_smoother_phase",
     "pmg_suffstats_workspace_size", "pmg_suffstats", "pmg_exp", "pmg_log", "pmg_roll_columns",
-    "pmg_emission_latent_mask", "pmg_emission_gaussian_dt",
+    "pmg_emission_latent_mask", "pmg_emission_latent_mask_batched", "pmg_emission_gaussian_dt",
     "pmg_spikes_bf16t", "pmg_suffstats_bf16_workspace_size", "pmg_suffstats_bf16",
     "pmg_mstep_workspace_size", "pmg_mstep_adam_supported", "pmg_mstep_adam", "pmg_joint_workspace_size",
     "pmg_joint_accumulate", "pmg_fwdbwd_lpad", "pmg_fwdbwd_state",
@@ -124,6 +127,7 @@ _SIGS = {
     "pmg_log": ([_P, _I64, _P, _P], _I32),
     "pmg_roll_columns": ([_P, _I64, _I32, _P, _P, _P], _I32),
     "pmg_emission_latent_mask": ([_P, _P, _I64, _I32, _P, _P, _P, _P], _I32),
+    "pmg_emission_latent_mask_batched": ([_P, _P, _I64, _I32, _P, _I32, _P, _P, _P], _I32),
     "pmg_mstep_workspace_size": ([_I32, _I32], _SZ),
     "pmg_mstep_adam_supported": ([_I32, _I32, _I32], ctypes.c_int),
     "pmg_mstep_adam": ([_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, ctypes.POINTER(AdamCfg),

@@ -356,11 +356,20 @@ class PoissonGPLVMJump1D:
         eng.set_tuning(np.asarray(tuning))
         return eng
 
-    def _nb_on(self, eng, dt_l, t_l=None):
-        """decode_latent_naive_bayes over eng's current spikes."""
+    def _nb_on(self, eng, dt_l, t_l=None, n_split=1):
+        """decode_latent_naive_bayes over eng's current spikes.  n_split > 1: the spikes
+        are n_split equal-length recordings stacked in time (the batched shuffles of
+        test.shuffle_and_decode); dt_l is one recording's and a list of per-recording
+        result dicts is returned.  Every output row depends on its own time bin only, so
+        each dict equals the decode of that recording alone bit for bit."""
         sp = eng.sp
         T = sp.T
-        dt = np.broadcast_to(np.asarray(dt_l, np.float64), (T,))
+        if n_split > 1:
+            if T % n_split:
+                raise ValueError("stacked recordings must have equal length")
+            dt = np.tile(np.broadcast_to(np.asarray(dt_l, np.float64), (T // n_split,)), n_split)
+        else:
+            dt = np.broadcast_to(np.asarray(dt_l, np.float64), (T,))
         dev, L = eng.dev, self.n_latent_bin
         lib, sh = eng.lib, nat.stream_handle()
         if np.all(dt == dt[0]):
@@ -384,15 +393,14 @@ class PoissonGPLVMJump1D:
         if eng.noise_std is None:
             eng.emission_status()
         lp = _np(log_post)
+        pl = np.exp(lp)       # host exp: cheaper than a second (T, L) device-to-host copy
         lml_h = _np(lml)
-        posterior_latent = np.exp(lp)
-        if t_l is not None and nap is not None:
-            posterior_latent = nap.TsdFrame(d=posterior_latent, t=t_l)
-        return {'log_posterior_latent': lp,
-                'log_marginal_l': lml_h.astype(np.float32),
-                'log_marginal_total': float(lml_h.sum()),
-                'posterior_latent': posterior_latent,
-                'll_per_pos_l': _np(eng.loglik())}
+        ll = _np(eng.loglik())
+        if n_split > 1:
+            Ts = T // n_split
+            return [_nb_dict(lp[r * Ts:(r + 1) * Ts], pl[r * Ts:(r + 1) * Ts], lml_h[r * Ts:(r + 1) * Ts],
+                             ll[r * Ts:(r + 1) * Ts], t_l) for r in range(n_split)]
+        return _nb_dict(lp, pl, lml_h, ll, t_l)
 
     def log_marginal_masked(self, y, ma_latent_l, tuning=None, hyperparam={}, ma_neuron=None,
                             likelihood_scale=1.):
@@ -407,7 +415,10 @@ class PoissonGPLVMJump1D:
         references re-derived), the row reference and the forward filter (logZ is
         the filter's sum_t c_t, decoder.py:151-187).  The backward pass, the joint
         and the host copies of (T, D, L) tensors are skipped.  Every logZ stays on
-        the device until one copy at the end."""
+        the device until one copy at the end.  With the banded scans and L % 32 == 0
+        the masks run batched (DeviceEM.masked_logz_batched): one stacked mask
+        launch, one row-reference launch and one forward launch per group of masks,
+        no alpha written."""
         if _is_tsd(y):
             y = y.d
         if tuning is None:
@@ -435,9 +446,17 @@ class PoissonGPLVMJump1D:
         eng.set_ma_latent(None)
         delta0, rblk0 = eng.emission_unmasked()
         mu8 = torch.as_tensor((masks != 0).astype(np.uint8), device=eng.dev)
-        for r in range(len(masks)):
-            eng.emission_from(delta0, rblk0, mu8[r], likelihood_scale)
-            eng.forward(likelihood_scale, logz[r:r + 1])
+        R = len(masks)
+        if not eng.dense and self.n_latent_bin % 32 == 0 and R > 1:
+            # batched: Rg masks per pass (stacked masked emissions, one forward launch)
+            Rg = eng.mask_batch_size(R)
+            for r0 in range(0, R, Rg):
+                r1 = min(R, r0 + Rg)
+                eng.masked_logz_batched(delta0, rblk0, mu8[r0:r1], likelihood_scale, logz[r0:r1])
+        else:
+            for r in range(R):
+                eng.emission_from(delta0, rblk0, mu8[r], likelihood_scale)
+                eng.forward(likelihood_scale, logz[r:r + 1])
         eng.check_status()
         return _np(logz).astype(np.float64)
 
@@ -583,6 +602,17 @@ def log_joint_from_counts(S4, logK, logA, ml=None):
         sent = -1e20 * (nm[:, None] + nm[None, :])
         logS = np.where(zero & (sent < 0.0), sent[None, None], logS)
     return np.asarray(logA, np.float64)[:, :, None, None] + np.asarray(logK, np.float64)[None] + logS
+
+
+def _nb_dict(lp, posterior_latent, lml_h, ll, t_l=None):
+    """decode_latent_naive_bayes's returned dict (core.py:499-524)."""
+    if t_l is not None and nap is not None:
+        posterior_latent = nap.TsdFrame(d=posterior_latent, t=t_l)
+    return {'log_posterior_latent': lp,
+            'log_marginal_l': lml_h.astype(np.float32),
+            'log_marginal_total': float(lml_h.sum()),
+            'posterior_latent': posterior_latent,
+            'll_per_pos_l': ll}
 
 
 def _masked_log(logp, ml):

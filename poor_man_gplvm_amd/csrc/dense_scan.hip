@@ -1109,8 +1109,7 @@ int pmg_dense_forward(const float* delta, const float* phi, const double* ll64, 
                        p.M - 1, -1, p.L, p.Lp, p.tol, w.flags, (const float*)nullptr, 0, p.ctl + kDPending);
     PMG_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(kfr, dim3(p.S), dim3(kDNT), 0, st, p);
-  PMG_LAUNCH_CHECK();
+  PMG_HIP(launch_persistent(kfr, dim3(p.S), dim3(kDNT), 0, st, p));
   return PMG_OK;
 }
 
@@ -1151,8 +1150,7 @@ int pmg_dense_backward(const float* delta, const float* phi, const double* ll64,
     hipLaunchKernelGGL(k_dense_verify, dim3((p.M - 1 + 3) / 4), dim3(256), 0, st, w.b_in, (const double*)w.b_first, 0,
                        p.M - 2, 1, p.L, p.Lp, p.tol, w.flags, (const float*)nullptr, p.C, p.ctl + kDPending);
     PMG_LAUNCH_CHECK();
-    hipLaunchKernelGGL(kbr, dim3(p.S), dim3(kDNT), 0, st, p);
-    PMG_LAUNCH_CHECK();
+    PMG_HIP(launch_persistent(kbr, dim3(p.S), dim3(kDNT), 0, st, p));
   }
   return PMG_OK;
 }

@@ -80,7 +80,7 @@ __global__ void __launch_bounds__(256) k_rates_prepare(
 // A[row r][k = 16h .. 16h+15] and B[k = 16h ..][col r]; the same (h, byte) -> k
 // assignment on both operands keeps the K pairing consistent.
 // C/D: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*h.
-constexpr int ET = 128, EL = 64, EKC = 64, EROW = EKC + 16;
+constexpr int EL = 64, EKC = 64, EROW = EKC + 16;
 // EKC = 64: the double-buffered stage (sY 20 KB + sQ 51 KB) lets two workgroups share a
 // CU, so one workgroup's epilogue and first loads overlap the other's MFMAs (at 128 B
 // chunks the 129 KB stage held the CU alone).  Rows of 80 B: 16 consecutive rows still
@@ -93,11 +93,20 @@ __device__ __forceinline__ int xcd_group(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-__global__ void __launch_bounds__(512, 4) k_emission_i8(
+// MT time fragments per wave: the workgroup tile is ET = 128 MT time bins x 64 latents and
+// each wave 32 MT t x 32 l (5 MT accumulators).  MT = 2 halves the digit planes' L2 -> LDS
+// traffic per output (each plane chunk feeds twice the MFMAs) and the LDS reads per MFMA
+// (one B fragment per digit serves both A fragments): the digit planes are re-read once
+// per time tile, so their traffic is T / ET x 5 Lp Kp bytes.
+// MT = 1: 80 accumulator registers, <= 128 per lane so two workgroups share a CU (one's
+// epilogue beside the other's MFMAs); MT = 2: 160, one workgroup per CU.
+template <int MT>
+__global__ void __launch_bounds__(512, MT == 1 ? 4 : 2) k_emission_i8(
     const int8_t* __restrict__ yq, const int8_t* __restrict__ qd,
     const double* __restrict__ lamsum, const double* __restrict__ gconst,
     const uint8_t* __restrict__ ma_latent, int64_t T, int64_t Tp, int L, int Lp, int Kp, int nLT,
     float* __restrict__ delta, double* __restrict__ rblk, double* __restrict__ ll64) {
+  constexpr int ET = 128 * MT;
   __shared__ __attribute__((aligned(16))) int8_t sY[2][ET][EROW];
   __shared__ __attribute__((aligned(16))) int8_t sQ[2][kDig][EL][EROW];
   const int tid = threadIdx.x;
@@ -114,10 +123,14 @@ __global__ void __launch_bounds__(512, 4) k_emission_i8(
   // branch-free staging loads (Kp is a multiple of EKC): rows past Tp / Lp are
   // clamped -- their outputs are never written.  One spike segment and up to three
   // digit segments per thread.
-  const int ysr = tid / ESEG, ysc = (tid % ESEG) * 16;
-  int64_t ty = t0 + ysr;
-  ty = ty < Tp ? ty : Tp - 1;
-  const int8_t* yrow = yq + ty * Kp + ysc;
+  const int ysr = tid / ESEG, ysc = (tid % ESEG) * 16;   // + 128 m for segment m < MT
+  const int8_t* yrow[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    int64_t ty = t0 + ysr + 128 * m;
+    ty = ty < Tp ? ty : Tp - 1;
+    yrow[m] = yq + ty * Kp + ysc;
+  }
   const int8_t* qsrc[3];
   int qdst[3];
 #pragma unroll
@@ -133,20 +146,22 @@ __global__ void __launch_bounds__(512, 4) k_emission_i8(
   }
   const bool q2 = tid + 1024 < EQSEG;
 #define PMG_EM_LOAD(k0)                                                      \
-  ry0 = *reinterpret_cast<const uint4*>(yrow + (k0));                       \
+  _Pragma("unroll") for (int m = 0; m < MT; ++m) ry[m] = *reinterpret_cast<const uint4*>(yrow[m] + (k0)); \
   rq0 = *reinterpret_cast<const uint4*>(qsrc[0] + (k0));                    \
   rq1 = *reinterpret_cast<const uint4*>(qsrc[1] + (k0));                    \
   rq2 = *reinterpret_cast<const uint4*>(qsrc[2] + (k0));
 #define PMG_EM_STORE(b)                                                      \
-  *reinterpret_cast<uint4*>(&sY[b][ysr][ysc]) = ry0;                        \
+  _Pragma("unroll") for (int m = 0; m < MT; ++m) *reinterpret_cast<uint4*>(&sY[b][ysr + 128 * m][ysc]) = ry[m]; \
   *reinterpret_cast<uint4*>(&sQ[b][0][0][0] + qdst[0]) = rq0;               \
   *reinterpret_cast<uint4*>(&sQ[b][0][0][0] + qdst[1]) = rq1;               \
   if (q2) *reinterpret_cast<uint4*>(&sQ[b][0][0][0] + qdst[2]) = rq2;
-  uint4 ry0, rq0, rq1, rq2;
+  uint4 ry[MT], rq0, rq1, rq2;
 
-  v16i acc[kDig];
+  v16i acc[MT][kDig];
 #pragma unroll
-  for (int d = 0; d < kDig; ++d) acc[d] = (v16i){0};
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int d = 0; d < kDig; ++d) acc[m][d] = (v16i){0};
   const int nch = Kp / EKC;
   PMG_EM_LOAD(0)
   PMG_EM_STORE(0)
@@ -159,11 +174,14 @@ __global__ void __launch_bounds__(512, 4) k_emission_i8(
     }
 #pragma unroll
     for (int ks = 0; ks < EKC; ks += 32) {
-      const v4i a = *reinterpret_cast<const v4i*>(&sY[buf][wt * 32 + r][ks + 16 * h]);
+      v4i a[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) a[m] = *reinterpret_cast<const v4i*>(&sY[buf][wt * 32 * MT + 32 * m + r][ks + 16 * h]);
 #pragma unroll
       for (int d = 0; d < kDig; ++d) {
         const v4i b = *reinterpret_cast<const v4i*>(&sQ[buf][d][wl * 32 + r][ks + 16 * h]);
-        acc[d] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc[d], 0, 0, 0);
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[m][d] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[m], b, acc[m][d], 0, 0, 0);
       }
     }
     if (more) {
@@ -201,13 +219,14 @@ __global__ void __launch_bounds__(512, 4) k_emission_i8(
   const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
       ll64 ? (void*)(ll64 + t0 * (int64_t)L) : (void*)delta, (short)0, ll64 ? nrow * L * 8 : 0, 0x00020000);
   const uint32_t kNoWrite = 0x80000000u;                // past any bound above
-  const int trow0 = wt * 32 + 4 * h;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    const int tr = trow0 + (i & 3) + 8 * (i >> 2);      // row within the workgroup tile
-    double q = (double)acc[kDig - 1][i];
+    const int tr = wt * 32 * MT + 32 * m + 4 * h + (i & 3) + 8 * (i >> 2);   // row within the workgroup tile
+    double q = (double)acc[m][kDig - 1][i];
 #pragma unroll
-    for (int d = kDig - 2; d >= 0; --d) q = fma(q, 256.0, (double)acc[d][i]);
+    for (int d = kDig - 2; d >= 0; --d) q = fma(q, 256.0, (double)acc[m][d][i]);
     const uint32_t g0 = __builtin_amdgcn_raw_buffer_load_b32(rg, tr * 8, 0, 0);
     const uint32_t g1 = __builtin_amdgcn_raw_buffer_load_b32(rg, tr * 8 + 4, 0, 0);
     const double gc = __hiloint2double((int)g1, (int)g0);
@@ -309,9 +328,13 @@ __global__ void __launch_bounds__(256) k_emission_f64(
 // per (time bin, pair of 32-latent blocks); T * L * 8 bytes + rblk traffic per mask, no
 // contraction: this is what lets log_marginal_masked run the emission GEMM once for all
 // its masks (model_selection_helper.get_downsampled_lml, :243-260).
+// R masks (rows of ma_latent) from one read of (delta0, rblk0): mask r is written at
+// column r L of delta rows of ldo floats and column r nblk of rblk rows of ldr doubles
+// (R = 1: the plain layout).
 __global__ void __launch_bounds__(256) k_latent_mask_apply(
     const float* __restrict__ delta0, const double* __restrict__ rblk0, int64_t T, int L, int nblk,
-    const uint8_t* __restrict__ ma_latent, float* __restrict__ delta, double* __restrict__ rblk) {
+    const uint8_t* __restrict__ ma_latent, int R, float* __restrict__ delta, double* __restrict__ rblk,
+    int64_t ldo, int64_t ldr) {
   const int lane = threadIdx.x & 63;
   const int npair = (nblk + 1) >> 1;
   const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -321,20 +344,26 @@ __global__ void __launch_bounds__(256) k_latent_mask_apply(
   const int blk = l >> 5;
   const bool bvalid = blk < nblk;
   const bool lvalid = l < L;
-  const bool msk = lvalid && ma_latent[l] == 0;
   const double r0 = bvalid ? rblk0[t * nblk + blk] : 0.0;
   const float d0 = lvalid ? delta0[t * (int64_t)L + l] : 0.f;
-  double v = msk ? -1e20 : (double)d0 + r0;
-  v = lvalid ? v : -INFINITY;
-  const float anym = half_max32(msk ? 1.f : 0.f);
-  const double mx = (double)half_max32((float)v);
-  if (!bvalid) return;                      // after the cross-lane reductions
-  if (anym > 0.f) {
-    if ((lane & 31) == 0) rblk[t * nblk + blk] = mx;
-    if (lvalid) delta[t * (int64_t)L + l] = (float)(v - mx);
-  } else {
-    if ((lane & 31) == 0) rblk[t * nblk + blk] = r0;
-    if (lvalid) delta[t * (int64_t)L + l] = d0;
+  const double v0 = (double)d0 + r0;
+  for (int r = 0; r < R; ++r) {
+    const bool msk = lvalid && ma_latent[(int64_t)r * L + l] == 0;
+    double v = msk ? -1e20 : v0;
+    v = lvalid ? v : -INFINITY;
+    const float anym = half_max32(msk ? 1.f : 0.f);
+    const double mx = (double)half_max32((float)v);
+    if (bvalid) {
+      float* drow = delta + t * ldo + (int64_t)r * L;
+      double* rrow = rblk + t * ldr + (int64_t)r * nblk;
+      if (anym > 0.f) {
+        if ((lane & 31) == 0) rrow[blk] = mx;
+        if (lvalid) drow[l] = (float)(v - mx);
+      } else {
+        if ((lane & 31) == 0) rrow[blk] = r0;
+        if (lvalid) drow[l] = d0;
+      }
+    }
   }
 }
 
@@ -383,10 +412,17 @@ int pmg_emission_poisson(const int8_t* yq, const double* gconst, const double* t
                      ma_neuron_1d, dt, Lp, Kp, qd, lamsum, bad);
   PMG_LAUNCH_CHECK();
   const int nLT = (Lp + EL - 1) / EL;
-  const int64_t nTT = (T + ET - 1) / ET;
   const int64_t Tp = round_up(T, 64);   // rows of yq (pmg_spikes_prepare zero-pads to Tp)
-  hipLaunchKernelGGL(k_emission_i8, dim3((unsigned)(nLT * nTT)), dim3(512), 0, st, yq, qd, lamsum,
-                     gconst, ma_latent, T, Tp, L, Lp, Kp, nLT, delta, rblk, ll64);
+  // one time fragment per wave: two workgroups share a CU (one's epilogue beside the
+  // other's MFMAs).  MT = 2 (PMG_EMISSION_MT=2, env: tests / A/B timing) halves the
+  // digit-plane traffic but holds the CU alone: C3 emission 0.223 -> 0.284 ms, so it is
+  // not the default.
+  const char* mt_s = getenv("PMG_EMISSION_MT");
+  const int MT = (mt_s && atoi(mt_s) == 2) ? 2 : 1;
+  const int64_t ET = 128 * MT;
+  const int64_t nTT = (T + ET - 1) / ET;
+  hipLaunchKernelGGL(MT == 2 ? k_emission_i8<2> : k_emission_i8<1>, dim3((unsigned)(nLT * nTT)), dim3(512), 0, st,
+                     yq, qd, lamsum, gconst, ma_latent, T, Tp, L, Lp, Kp, nLT, delta, rblk, ll64);
   PMG_LAUNCH_CHECK();
   return PMG_OK;
 }
@@ -415,7 +451,94 @@ int pmg_emission_latent_mask(const float* delta0, const double* rblk0, int64_t T
   const int nblk = (int)(round_up(L, 32) / 32);
   const int64_t waves = T * ((nblk + 1) / 2);
   hipLaunchKernelGGL(k_latent_mask_apply, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, as_stream(stream),
-                     delta0, rblk0, T, L, nblk, ma_latent, delta, rblk);
+                     delta0, rblk0, T, L, nblk, ma_latent, 1, delta, rblk, (int64_t)L, (int64_t)nblk);
+  PMG_LAUNCH_CHECK();
+  return PMG_OK;
+}
+
+// R masks at once, R <= 64: one wave per (32-latent block pair, row group); every lane
+// turns its latent's R mask bytes into one bit word once, then walks the wave's rows
+// (stride gridDim.y), each row's (delta0, rblk0) read once for all R masks and the next
+// row's prefetched.  Mask r's outputs are bit-identical to k_latent_mask_apply's.
+__global__ void __launch_bounds__(256) k_latent_mask_apply_rows(
+    const float* __restrict__ delta0, const double* __restrict__ rblk0, int64_t T, int L, int nblk,
+    const uint8_t* __restrict__ ma_latent, int R, float* __restrict__ delta, double* __restrict__ rblk) {
+  const int lane = threadIdx.x & 63;
+  const int npair = (nblk + 1) >> 1;
+  const int pw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);   // block pair
+  if (pw >= npair) return;                  // uniform per wave
+  const int l = pw * 64 + lane;
+  const int blk = l >> 5;
+  const bool bvalid = blk < nblk;
+  const bool lvalid = l < L;
+  uint64_t keep = 0;                        // bit r: latent l kept by mask r
+  if (lvalid)
+    for (int r = 0; r < R; ++r) keep |= (uint64_t)(ma_latent[(int64_t)r * L + l] != 0) << r;
+  // bit r: latent l's 32-block has a bin mask r drops (else the block is copied as is)
+  uint64_t bmask = 0;
+  for (int r = 0; r < R; ++r)
+    bmask |= (uint64_t)(half_max32((lvalid && !((keep >> r) & 1)) ? 1.f : 0.f) > 0.f) << r;
+  const int64_t ldo = (int64_t)R * L, ldr = (int64_t)R * nblk;
+  int64_t t = blockIdx.y;
+  double r0 = 0.0;
+  float d0 = 0.f;
+  if (t < T) {
+    r0 = bvalid ? rblk0[t * nblk + blk] : 0.0;
+    d0 = lvalid ? delta0[t * (int64_t)L + l] : 0.f;
+  }
+  for (; t < T; t += gridDim.y) {
+    const int64_t tn = t + gridDim.y;       // prefetch the next row
+    double r1 = 0.0;
+    float d1 = 0.f;
+    if (tn < T) {
+      r1 = bvalid ? rblk0[tn * nblk + blk] : 0.0;
+      d1 = lvalid ? delta0[tn * (int64_t)L + l] : 0.f;
+    }
+    const double v0 = (double)d0 + r0;
+    float* drow = delta + t * ldo;
+    double* rrow = rblk + t * ldr;
+#pragma unroll 4
+    for (int r = 0; r < R; ++r) {
+      const bool msk = lvalid && !((keep >> r) & 1);
+      double v = msk ? -1e20 : v0;
+      v = lvalid ? v : -INFINITY;
+      const bool anym = (bmask >> r) & 1;
+      const double mx = (double)half_max32((float)v);
+      if (bvalid) {
+        if (anym) {
+          if ((lane & 31) == 0) rrow[(int64_t)r * nblk + blk] = mx;
+          if (lvalid) drow[(int64_t)r * L + l] = (float)(v - mx);
+        } else {
+          if ((lane & 31) == 0) rrow[(int64_t)r * nblk + blk] = r0;
+          if (lvalid) drow[(int64_t)r * L + l] = d0;
+        }
+      }
+    }
+    r0 = r1;
+    d0 = d1;
+  }
+}
+
+int pmg_emission_latent_mask_batched(const float* delta0, const double* rblk0, int64_t T, int32_t L,
+                                     const uint8_t* ma_latent, int32_t R, float* delta, double* rblk,
+                                     void* stream) {
+  PMG_REQUIRE(T > 0 && L > 0 && R >= 1 && R <= 65535 && delta0 && rblk0 && ma_latent && delta && rblk,
+              "pmg_emission_latent_mask_batched: bad args");
+  PMG_REQUIRE(L % 32 == 0, "pmg_emission_latent_mask_batched: L %% 32 == 0 (L=%d)", L);
+  PMG_REQUIRE(delta0 != delta && rblk0 != rblk, "pmg_emission_latent_mask_batched: in-place is not supported");
+  const int nblk = L / 32;
+  if (R <= 64) {
+    // ~32 waves per CU in total: block pairs x row groups
+    const int npair = (nblk + 1) / 2;
+    const int64_t groups64 = (int64_t)(8192 + npair - 1) / npair;
+    const unsigned groups = (unsigned)(groups64 < T ? groups64 : T);
+    hipLaunchKernelGGL(k_latent_mask_apply_rows, dim3((unsigned)((npair + 3) / 4), groups), dim3(256), 0,
+                       as_stream(stream), delta0, rblk0, T, L, nblk, ma_latent, R, delta, rblk);
+  } else {
+    const int64_t waves = T * ((nblk + 1) / 2);
+    hipLaunchKernelGGL(k_latent_mask_apply, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, as_stream(stream),
+                       delta0, rblk0, T, L, nblk, ma_latent, R, delta, rblk, (int64_t)R * L, (int64_t)R * nblk);
+  }
   PMG_LAUNCH_CHECK();
   return PMG_OK;
 }

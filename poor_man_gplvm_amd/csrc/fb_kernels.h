@@ -118,6 +118,7 @@ struct FBParams {
   // row is jump * e_t / S, so the backward rebuilds it bit-exactly from e_t and these
   float* jsc;
   uint32_t a1_bytes;  // bytes of alpha's d = 1 rows the forward stores (4 L, or 0: omitted)
+  uint32_t a0_bytes;  // bytes of alpha's d = 0 rows the forward stores (4 L, or 0: logZ-only passes)
   // backward
   const float* alpha_in;  // only the d = 0 rows are read
   float* w_first;         // per chunk: alpha at its first step, (2, Lpad) (boundary weights)
@@ -625,7 +626,7 @@ __device__ __forceinline__ double fwd_stream(const FBParams& p, Fwd<J, WP>& st, 
       float a0[J];
 #pragma unroll
       for (int j = 0; j < J; ++j) a0[j] = st.q0[j] * st.iS;
-      bstore_row<J, VEC>(arow, p.L, j0, a0);
+      bstore_row_n<J, VEC>(arow, p.a0_bytes, j0, a0);
       if constexpr (A1) {   // alpha's d = 1 row, as the backward rebuilds it
         float a1[J];
 #pragma unroll

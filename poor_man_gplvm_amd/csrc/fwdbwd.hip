@@ -275,7 +275,8 @@ static int forward_impl(const float* delta, const float* phi, const double* m, i
   p.logz = logz;
   p.chunk_logz = w.chunk_logz;
   p.jsc = w.jsc;
-  p.a1_bytes = (phase & 4) ? 0u : (uint32_t)p.L * 4u;
+  p.a1_bytes = (phase & (PMG_PHASE_NO_JUMP_ROWS | PMG_PHASE_NO_ALPHA)) ? 0u : (uint32_t)p.L * 4u;
+  p.a0_bytes = (phase & PMG_PHASE_NO_ALPHA) ? 0u : (uint32_t)p.L * 4u;
   p.adapt = (phase & PMG_PHASE_ADAPTIVE_WARMUP) ? 1 : 0;
   p.s_in = w.s_in;
   p.s_out = w.s_out;
@@ -305,8 +306,7 @@ static int forward_impl(const float* delta, const float* phi, const double* m, i
                          p.ws_stride);
       PMG_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(ks.forward_relax, dim3(p.S, R), dim3(64), 0, st, p);  // also sums logZ
-    PMG_LAUNCH_CHECK();
+    PMG_HIP(launch_persistent(ks.forward_relax, dim3(p.S, R), dim3(64), 0, st, p));  // also sums logZ
   }
   return PMG_OK;
 }
@@ -377,8 +377,7 @@ static int backward_impl(const float* delta, const float* phi, const float* alph
     hipLaunchKernelGGL(k_verify, dim3((nver + 3) / 4, R), dim3(256), 0, st, w.b_in, (const float*)w.b_first, 0,
                        p.M - 2, 1, 2 * p.Lpad, p.tol, w.flags, (const float*)w.w_first, p.Lpad, pend, p.ws_stride);
     PMG_LAUNCH_CHECK();
-    hipLaunchKernelGGL(ks.backward_relax, dim3(p.S, R), dim3(64), 0, st, p);
-    PMG_LAUNCH_CHECK();
+    PMG_HIP(launch_persistent(ks.backward_relax, dim3(p.S, R), dim3(64), 0, st, p));
   }
   return PMG_OK;
 }
@@ -395,7 +394,7 @@ int pmg_backward_smoother_phase(const float* delta, const float* phi, const floa
                                 const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                                 int32_t warmup, double tol, float* P, float* gamma, float* rho,
                                 void* workspace, size_t workspace_bytes, void* stream, int32_t phase) {
-  PMG_REQUIRE((phase & 3) != 0 && (phase & ~(PMG_PHASE_FLAG_BITS & ~4)) == 0,
+  PMG_REQUIRE((phase & 3) != 0 && (phase & ~(PMG_PHASE_FLAG_BITS & ~(PMG_PHASE_NO_JUMP_ROWS | PMG_PHASE_NO_ALPHA))) == 0,
               "pmg_backward_smoother_phase: phase %d", phase);
   return backward_impl(delta, phi, alpha, T, tr, likelihood_scale, chunk, warmup, tol, P, gamma, rho,
                        workspace, workspace_bytes, stream, phase);
@@ -421,7 +420,7 @@ int pmg_backward_smoother_batched(const float* delta, const float* phi, const fl
                                   const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                                   int32_t warmup, double tol, float* P, float* gamma, void* workspace,
                                   size_t workspace_bytes, void* stream, int32_t phase) {
-  PMG_REQUIRE((phase & 3) != 0 && (phase & ~(PMG_PHASE_FLAG_BITS & ~4)) == 0,
+  PMG_REQUIRE((phase & 3) != 0 && (phase & ~(PMG_PHASE_FLAG_BITS & ~(PMG_PHASE_NO_JUMP_ROWS | PMG_PHASE_NO_ALPHA))) == 0,
               "pmg_backward_smoother_batched: phase %d", phase);
   return backward_impl(delta, phi, alpha, T, tr, likelihood_scale, chunk, warmup, tol, P, gamma, nullptr,
                        workspace, workspace_bytes, stream, phase, R);

@@ -30,11 +30,16 @@ namespace pmg {
 // would drain vmcnt, cdna_hip_programming.md "Pipelining across barriers").
 #define PMG_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
+#ifndef PMG_ADAM_FASTSP
+#define PMG_ADAM_FASTSP 0
+#endif
+
 constexpr int kLag = 4;                 // bodies a workgroup runs ahead of the decision
 constexpr int kRing = kLag + 2;
 constexpr int kSMax = 4;                // neurons per workgroup
 constexpr int kThreads = 512;           // L <= 512
 constexpr int kPartPerLane = 4;         // G <= 256 workgroups -> 4 partials per lane
+constexpr int kBiasLds = 1024;          // bias corrections held in LDS (bodies)
 
 struct AdamParams {
   double* W;
@@ -53,7 +58,6 @@ struct AdamParams {
   const double* bias;         // [2][maxiter] 1/(1 - b1^(count0+k+1)), 1/(1 - b2^(count0+k+1))
   unsigned long long* lpart;  // [maxiter + kLag + 2][G] f64 bits, pre-filled with kSentinel
   unsigned long long* gpart;  // [..][G]
-  double* ring;               // [G][kRing][3][NBM*4] (W, mu, nu) after each body
   int* timeout;
   long long* prof;            // optional (PMG_ADAM_PROF): s_memtime stamps of WG 0, bodies < 64
   // batched restarts (blockIdx.y = restart r of this launch): per-restart strides of the
@@ -76,12 +80,14 @@ __device__ __forceinline__ AdamParams adam_view(const AdamParams& p0) {
   p.stats += 4 * r;
   p.loss_hist += r * p.rs_hist;
   p.err_hist += r * p.rs_hist;
-  const uintptr_t o = (uintptr_t)(r * p.rs_ws);
-  p.bias = reinterpret_cast<const double*>(reinterpret_cast<uintptr_t>(p.bias) + o);
-  p.lpart = reinterpret_cast<unsigned long long*>(reinterpret_cast<uintptr_t>(p.lpart) + o);
-  p.gpart = reinterpret_cast<unsigned long long*>(reinterpret_cast<uintptr_t>(p.gpart) + o);
-  p.ring = reinterpret_cast<double*>(reinterpret_cast<uintptr_t>(p.ring) + o);
-  p.timeout = reinterpret_cast<int*>(reinterpret_cast<uintptr_t>(p.timeout) + o);
+  // byte offsets as pointer arithmetic (not integer round trips): the compiler keeps the
+  // kernel arguments' global address space and emits global / buffer accesses, not flat
+  // ones (a flat store also counts in lgkmcnt, so every LDS barrier would wait for it)
+  const int64_t o = r * p.rs_ws;
+  p.bias = reinterpret_cast<const double*>(reinterpret_cast<const char*>(p.bias) + o);
+  p.lpart = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(p.lpart) + o);
+  p.gpart = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(p.gpart) + o);
+  p.timeout = reinterpret_cast<int*>(reinterpret_cast<char*>(p.timeout) + o);
   p.prof = nullptr;
   return p;
 }
@@ -320,11 +326,12 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
   }
   for (int q = tid; q < 32 * A * SP; q += blockDim.x) sG[q] = 0.f;
   if (tid < 4) sCtl[tid] = 0;
-  // element state (W, mu, nu) of this thread's weight, and its global ring
+  // element state (W, mu, nu) of this thread's weight, and its ring of the last kRing
+  // states in LDS (each slot written and read by its own thread: no barrier, no HBM)
   double w_cur = 0.0, mu_cur = 0.0, nu_cur = 0.0;
-  constexpr int RS = 128 * kSMax;                      // ring slab per state (adam_ws)
-  double* ring = p.ring + (size_t)g * kRing * 3 * RS;
-  const int e = eq * kSMax + es;
+  constexpr int RS = 128 * SP;                         // ring slab per state: NB <= 128 columns
+  __shared__ double sRing[kRing * 3 * RS];
+  const int e = eq * SP + es;
   const int ewo = es * QS + (eq / BC) * BCP + eq % BC; // this element's sW / sD slot
   __syncthreads();
   if (is_el) {
@@ -333,11 +340,19 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
     mu_cur = p.mu[o];
     nu_cur = p.nu[o];
     sW[ewo] = w_cur;
-    ring[(0 * 3 + 0) * RS + e] = w_cur;
-    ring[(0 * 3 + 1) * RS + e] = mu_cur;
-    ring[(0 * 3 + 2) * RS + e] = nu_cur;
+    sRing[(0 * 3 + 0) * RS + e] = w_cur;
+    sRing[(0 * 3 + 1) * RS + e] = mu_cur;
+    sRing[(0 * 3 + 2) * RS + e] = nu_cur;
   }
   const int64_t count0 = p.count[0];
+  // the bias-correction table of the first kBiasLds bodies in LDS (uniform reads, no
+  // memory wait inside the loop); later bodies read it from the workspace
+  const int mi = p.maxiter > 1 ? p.maxiter : 1;
+  __shared__ double sBias[2 * kBiasLds];
+  for (int q = tid; q < kBiasLds && q < mi; q += blockDim.x) {
+    sBias[q] = p.bias[q];
+    sBias[kBiasLds + q] = p.bias[mi + q];
+  }
   __syncthreads();
 
   // control-wave state
@@ -404,13 +419,26 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
       // exact residual r = F - Fh (|r| <= 2^-24 |F|): f = softplus(Fh) + sigmoid(Fh) r
       const float Fh = (float)F;
       const double r = F - (double)Fh;
+      const bool live = is_row && s < S;
+#if PMG_ADAM_FASTSP
+      // one exp for softplus and sigmoid, one reciprocal of f for G and the loss's
+      // first-order correction
+      const float ex = expf(-fabsf(Fh));
+      const float f32 = fmaxf(Fh, 0.f) + log1pf(ex);
+      const float sg = (Fh >= 0.f ? 1.f : ex) / (1.f + ex);
+      const double fd = (double)f32 + (double)sg * r;
+      const double ifd = rcp_nr(fd + 1e-20);
+      const float gv = live ? (float)((ywd * ifd - twd) * (double)sg) : 0.f;
+      if (owner) sG[(lb * A + slot) * SP + s] = gv;
+      const double xl = (ywd != 0.0) ? ywd * ((double)logf(f32 + 1e-20f) + (double)sg * r * ifd) : 0.0;
+#else
       const float f32 = fmaxf(Fh, 0.f) + log1pf(expf(-fabsf(Fh)));
       const float sg = 1.f / (1.f + expf(-Fh));
       const double fd = (double)f32 + (double)sg * r;
-      const bool live = is_row && s < S;
       const float gv = live ? (float)((ywd * rcp_nr(fd + 1e-20) - twd) * (double)sg) : 0.f;
       if (owner) sG[(lb * A + slot) * SP + s] = gv;
       const double xl = (ywd != 0.0) ? ywd * ((double)logf(f32 + 1e-20f) + (double)sg * r * rcp_nr((double)f32)) : 0.0;
+#endif
       lpart -= live ? xl - fd * twd : 0.0;
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -469,10 +497,6 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
     // ---- Adam element update ------------------------------------------------------
     double gsq = 0.0;
     if (is_el) {
-      // bias corrections (uniform); bodies run ahead of the decision past maxiter are discarded
-      const int mi = p.maxiter > 1 ? p.maxiter : 1;
-      const int kb = k < mi ? k : mi - 1;
-      const double c1 = p.bias[kb], c2 = p.bias[mi + kb];
       float gsum = 0.f;
 #pragma unroll
       for (int w = 0; w < kNW; ++w) gsum += sPart[(w * SP + es) * 16 * BC + eq];
@@ -483,6 +507,11 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
       if (!eval_only) {  // optax 0.2.2 scale_by_adam + scale(-lr)
         const double mu = (1.0 - p.b1) * gr + p.b1 * mu_cur;
         const double nu = (1.0 - p.b2) * gr * gr + p.b2 * nu_cur;
+        // this body's bias corrections (uniform); bodies run ahead of the decision past
+        // maxiter are discarded
+        const int kb = k < mi ? k : mi - 1;
+        const double c1 = kb < kBiasLds ? sBias[kb] : p.bias[kb];
+        const double c2 = kb < kBiasLds ? sBias[kBiasLds + kb] : p.bias[mi + kb];
         const double mh = mu * c1;
         const double nh = nu * c2;
         w_cur = w_cur - p.lr * (mh * rcp_nr(sqrt(nh + p.eps_root) + p.eps));
@@ -490,11 +519,11 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
         nu_cur = nu;
       }
       const int ns = (k + 1) % kRing;
-      ring[(ns * 3 + 0) * RS + e] = w_cur;
-      ring[(ns * 3 + 1) * RS + e] = mu_cur;
-      ring[(ns * 3 + 2) * RS + e] = nu_cur;
       sW[ewo] = w_cur;
       sD[ewo] = (float)(w_cur - w_old);
+      sRing[(ns * 3 + 0) * RS + e] = w_cur;
+      sRing[(ns * 3 + 1) * RS + e] = mu_cur;
+      sRing[(ns * 3 + 2) * RS + e] = nu_cur;
     }
     lpart = wave_sum_f64(lpart);
     gsq = wave_sum_f64(gsq);
@@ -598,9 +627,9 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
   const int fs = eval_only ? (1 % kRing) : ((stop_j + 1) % kRing);
   if (is_el && !sCtl[2]) {
     const size_t o = (size_t)eq * p.N + n0 + es;
-    p.W[o] = ring[(fs * 3 + 0) * RS + e];
-    p.mu[o] = ring[(fs * 3 + 1) * RS + e];
-    p.nu[o] = ring[(fs * 3 + 2) * RS + e];
+    p.W[o] = sRing[(fs * 3 + 0) * RS + e];
+    p.mu[o] = sRing[(fs * 3 + 1) * RS + e];
+    p.nu[o] = sRing[(fs * 3 + 2) * RS + e];
   }
   if (g == 0 && ctl && lane == 0 && !sCtl[2]) {
     const int n_iter = eval_only ? 1 : stop_j + 2;
@@ -639,7 +668,6 @@ __global__ void __launch_bounds__(64) k_adam_hist(AdamParams p_arg) {
 }
 
 struct AdamWork {
-  double* ring;
   unsigned long long* lpart;
   unsigned long long* gpart;
   double* bias;
@@ -650,7 +678,6 @@ static size_t adam_ws(int G, int maxiter, AdamWork* w, void* base) {
   Carver c(base);
   AdamWork ww;
   ww.timeout = c.take<int>(64);
-  ww.ring = c.take<double>((size_t)G * kRing * 3 * 128 * kSMax);
   ww.lpart = c.take<unsigned long long>(((size_t)maxiter + kLag + 2) * G);
   ww.gpart = c.take<unsigned long long>(((size_t)maxiter + kLag + 2) * G);
   ww.bias = c.take<double>(2 * (size_t)maxiter);
@@ -805,7 +832,6 @@ static int adam_run(double* W, double* mu, double* nu, int64_t* count, const flo
   p.lpart = w.lpart;
   p.gpart = w.gpart;
   p.timeout = w.timeout;
-  p.ring = w.ring;
   p.bias = w.bias;
   p.rs_W = (int64_t)NB * N;
   p.rs_yw = (int64_t)L * N;
@@ -838,13 +864,11 @@ static int adam_run(double* W, double* mu, double* nu, int64_t* count, const flo
     q.bias = reinterpret_cast<const double*>(reinterpret_cast<char*>(w.bias) + o);
     q.lpart = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(w.lpart) + o);
     q.gpart = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(w.gpart) + o);
-    q.ring = reinterpret_cast<double*>(reinterpret_cast<char*>(w.ring) + o);
     q.timeout = reinterpret_cast<int*>(reinterpret_cast<char*>(w.timeout) + o);
     hipLaunchKernelGGL(k_adam_prologue, dim3(256, rg), dim3(256), 0, st, q, n);
     PMG_LAUNCH_CHECK();
     // rg x G workgroups, at most one per CU (adam_batch_geometry): all co-resident
-    hipLaunchKernelGGL(kern.fn, dim3(G, rg), dim3(kThreads), kern.lds, st, q);
-    PMG_LAUNCH_CHECK();
+    PMG_HIP(launch_persistent(kern.fn, dim3(G, rg), dim3(kThreads), kern.lds, st, q));
     hipLaunchKernelGGL(k_adam_hist, dim3(64, rg), dim3(64), 0, st, q);
     PMG_LAUNCH_CHECK();
   }

@@ -19,6 +19,11 @@ namespace pmg {
 
 typedef float v16f __attribute__((ext_vector_type(16)));
 
+// PMG_SS_EARLY_LOAD: issue the next K-tile's loads right after the split that consumes
+// the staged values, two MFMA blocks before the barrier (C3: 0.182 -> 0.167 ms)
+#ifndef PMG_SS_EARLY_LOAD
+#define PMG_SS_EARLY_LOAD 1
+#endif
 constexpr int kFlush = 128;  // time steps per fp32 accumulation segment
 
 // Workgroup tile 128 (m) x 128 (n), 4 waves as 2 x 2 of 64 x 64 (2 x 2 MFMA tiles each).
@@ -331,6 +336,19 @@ __global__ void __launch_bounds__(512) k_ptb3(const float* __restrict__ P, int L
   }
 // one K-tile: MFMAs on buffer cur, the staged next tile split into buffer nxt between
 // them, then the loads of the tile after that (their latency spans a whole K-tile)
+#if PMG_SS_EARLY_LOAD
+// the next loads as soon as the staged values are consumed (a quarter tile earlier)
+#define PMG_SS_TILE(cur, nxt, tload)                                                      \
+  PMG_SS_MFMA_K(cur, 0)                                                                   \
+  PMG_SS_SPLIT(nxt, 0)                                                                    \
+  PMG_SS_MFMA_K(cur, 16)                                                                  \
+  PMG_SS_SPLIT(nxt, 1)                                                                    \
+  PMG_SS_STORE_B(nxt)                                                                     \
+  PMG_SS_LOAD(tload)                                                                      \
+  PMG_SS_MFMA_K(cur, 32)                                                                  \
+  PMG_SS_MFMA_K(cur, 48)                                                                  \
+  __syncthreads();
+#else
 #define PMG_SS_TILE(cur, nxt, tload)                                                      \
   PMG_SS_MFMA_K(cur, 0)                                                                   \
   PMG_SS_SPLIT(nxt, 0)                                                                    \
@@ -341,6 +359,7 @@ __global__ void __launch_bounds__(512) k_ptb3(const float* __restrict__ P, int L
   PMG_SS_MFMA_K(cur, 48)                                                                  \
   PMG_SS_LOAD(tload)                                                                      \
   __syncthreads();
+#endif
 
   if (kb < ke) {
     PMG_SS_LOAD(kb)

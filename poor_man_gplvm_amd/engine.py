@@ -502,6 +502,70 @@ class DeviceEM:
             nat.check(self.lib.pmg_emission_rowref(nat.ptr(self.rblk), self.T, self.nblk, float(likelihood_scale),
                                                    nat.ptr(self.phi), nat.ptr(self.mref), sh), "pmg_emission_rowref")
 
+    # masks per batched forward launch (log-marginal passes; ~13 device bytes per (t, l) each)
+    MASK_BATCH_MAX = 16
+    MASK_BATCH_BYTES = 16 << 30
+
+    def mask_batch_size(self, R):
+        per = 13 * self.T * self.L
+        return int(max(1, min(R, self.MASK_BATCH_MAX, self.MASK_BATCH_BYTES // max(per, 1))))
+
+    def masked_logz_batched(self, delta0, rblk0, masks_u8, likelihood_scale, logz_out):
+        """log_marginal_final of the forward filter under each of R latent masks
+        (masks_u8 (R, L) uint8 device tensor) in ONE pass per stage: the R masked
+        emissions are written side by side as R stacked latent sets
+        (pmg_emission_latent_mask_batched), one row reference per mask
+        (pmg_emission_rowref_batched) and one chunk-parallel forward launch covers every
+        mask (pmg_forward_filter_batched, blockIdx.y = mask, no alpha written:
+        PMG_PHASE_NO_ALPHA).  Chunks are sized so the R chains together number ~2048.
+        Mask r's logZ equals a single-mask forward on the same chunk and relaxation
+        segment grid (ScanConfig(chunk=C, relax_segments=#CUs / R)) bit for bit.
+        Banded transitions, L % 32 == 0."""
+        R = int(masks_u8.shape[0])
+        T, L, dev = self.T, self.L, self.dev
+        if self.dense or L % 32:
+            raise nat.NativeError("batched masks need the banded scans and n_latent_bin % 32 == 0")
+        nb = self.nblk
+        sc = self.scan
+        C = int(sc.chunk) if sc.chunk else max(32, int(math.ceil(R * T / 2048)))
+        key = (R, C)
+        if getattr(self, '_mb_key', None) != key:
+            f32, f64 = torch.float32, torch.float64
+            self._mb = dict(delta=torch.empty((T, R * L), dtype=f32, device=dev),
+                            rblk=torch.empty((T, R * nb), dtype=f64, device=dev),
+                            phi=torch.empty((T, R * nb), dtype=f32, device=dev),
+                            mref=torch.empty((T, R), dtype=f64, device=dev),
+                            logc=torch.empty((R, T), dtype=f64, device=dev),
+                            ws=torch.zeros(int(self.lib.pmg_fwdbwd_batched_workspace_size(T, L, C, R)),
+                                           dtype=torch.uint8, device=dev))
+            self._mb_key = key
+        b = self._mb
+        sh = nat.stream_handle()
+        with self._t('emission_mask'):
+            nat.check(self.lib.pmg_emission_latent_mask_batched(nat.ptr(delta0), nat.ptr(rblk0), T, L,
+                                                                nat.ptr(masks_u8), R, nat.ptr(b['delta']),
+                                                                nat.ptr(b['rblk']), sh),
+                      "pmg_emission_latent_mask_batched")
+        with self._t('emission_rowref'):
+            nat.check(self.lib.pmg_emission_rowref_batched(nat.ptr(b['rblk']), T, R * nb, R, float(likelihood_scale),
+                                                           nat.ptr(b['phi']), nat.ptr(b['mref']), sh),
+                      "pmg_emission_rowref_batched")
+        # no alpha is written (PMG_PHASE_NO_ALPHA); the kernels only need a valid pointer
+        args = (nat.ptr(b['delta']), nat.ptr(b['phi']), nat.ptr(b['mref']), T, R, ctypes.byref(self._tr_c),
+                float(likelihood_scale), C, int(sc.warmup), float(sc.tol), nat.ptr(self.alpha),
+                nat.ptr(b['logc']), nat.ptr(logz_out), nat.ptr(b['ws']), b['ws'].numel(), sh)
+        with self._t('forward_filter'):
+            nat.check(self.lib.pmg_forward_filter_batched(*args, 1 | nat.PHASE_NO_ALPHA), "pmg_forward_filter_batched")
+        with self._t('forward_repair'):
+            nat.check(self.lib.pmg_forward_filter_batched(*args, 2 | nat.PHASE_NO_ALPHA | self._seg_bits()),
+                      "pmg_forward_filter_batched")
+        w = b['ws']
+        slab = (w.numel() // R) & ~255 if R > 1 else w.numel()
+        views = [w[r * slab:r * slab + 4 * nat.CTL_WORDS].view(torch.int32) for r in range(R)]
+        host = torch.stack(views).cpu().numpy()   # one read of every mask's sticky timeout words
+        for r in range(R):
+            _raise_on_timeout(views[r], host[r], "masked forward relaxation")
+
     def _emission_call(self, sp, sh, dt):
         if self.noise_std is not None:
             nat.check(self.lib.pmg_emission_gaussian(nat.ptr(sp.y), nat.ptr(self.tuning64), nat.ptr(sp.ma),

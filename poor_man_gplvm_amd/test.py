@@ -80,6 +80,44 @@ class ShuffleDecoder:
         nat.check(self.lib.pmg_roll_columns(nat.ptr(self.y_src), self.T, self.N, nat.ptr(self.shift),
                                             nat.ptr(self.y_work), nat.stream_handle()), "pmg_roll_columns")
 
+    # naive-Bayes shuffles decoded per launch: the stacked copies' device bytes stay
+    # within this budget (delta, block references, log posterior, ll: ~13 bytes per (t, l))
+    NB_BATCH_BYTES = 8 << 30
+    NB_BATCH_MAX = 32
+
+    def nb_batch_size(self, n_shuffle):
+        per = 13 * self.T * self.model.n_latent_bin + 12 * self.T * self.N
+        return int(max(1, min(n_shuffle, self.NB_BATCH_MAX, self.NB_BATCH_BYTES // max(per, 1))))
+
+    def decode_naive_bayes_batch(self, shifts_l):
+        """Naive-Bayes decodes of len(shifts_l) shuffles in ONE pass: the rolled copies
+        are stacked in time (R T, N), so the spike preparation, the int8-MFMA emission
+        and the normaliser each run once for all of them.  Every output row depends on
+        its own time bin only, so each returned dict equals decode(shifts) bit for bit."""
+        m = self.model
+        R = len(shifts_l)
+        if R == 1:
+            return [self.decode(shifts_l[0])]
+        T, N = self.T, self.N
+        if getattr(self, '_stack_R', 0) != R:
+            self._stack = torch.empty((R * T, N), dtype=torch.float32, device=self.y_src.device)
+            self._stack_R = R
+            self._stack_eng = None
+        for r, s in enumerate(shifts_l):
+            s = np.asarray(s, dtype=np.int64)
+            if s.shape != (N,):
+                raise ValueError(f"shifts must have shape ({N},)")
+            self.shift.copy_(torch.as_tensor(s), non_blocking=False)
+            nat.check(self.lib.pmg_roll_columns(nat.ptr(self.y_src), T, N, nat.ptr(self.shift),
+                                                nat.ptr(self._stack[r * T:(r + 1) * T]), nat.stream_handle()),
+                      "pmg_roll_columns")
+        if self._stack_eng is None:
+            self._stack_eng = m._nb_engine(self._stack, m.tuning, self.hp, m.ma_neuron_default,
+                                           m.ma_latent_default)
+        else:
+            self._stack_eng.sp.refresh()
+        return m._nb_on(self._stack_eng, self.dt_l, n_split=R)
+
     def decode(self, shifts):
         """Decode the copy of y with column j rolled by shifts[j] (np.roll semantics)."""
         m = self.model
@@ -113,7 +151,16 @@ def shuffle_and_decode(model, spk_tsdf, n_time_per_chunk=10000, dt_l=1, n_shuffl
     if n_shuffle < 1:
         raise ValueError("n_shuffle must be >= 1")
     dec = ShuffleDecoder(model, y, decoder_type, dt_l)
-    res_l = [dec.decode(_shifts(*y.shape)) for _ in range(n_shuffle)]
+    if decoder_type == 'naive_bayes':
+        # batched: every shuffle's shifts drawn first, in the reference's order (the same
+        # np.random calls), then Rg shuffles decoded per pass
+        shifts = [_shifts(*y.shape) for _ in range(n_shuffle)]
+        Rg = dec.nb_batch_size(n_shuffle)
+        res_l = []
+        for i in range(0, n_shuffle, Rg):
+            res_l.extend(dec.decode_naive_bayes_batch(shifts[i:i + Rg]))
+    else:
+        res_l = [dec.decode(_shifts(*y.shape)) for _ in range(n_shuffle)]
     return {k: np.array([d[k] for d in res_l]) for k in res_l[0].keys()}
 
 

@@ -539,3 +539,24 @@ def test_emission_range_flag_raises():
     eng.set_tuning(d['tuning'])
     eng.emission(1.0)
     eng.emission_status()                       # cleared by the previous check
+
+
+@pytest.mark.parametrize("L,T", [(512, 3000), (100, 1000), (256, 700)])
+def test_emission_time_tile_invariant(L, T, monkeypatch):
+    """The int8-MFMA emission with one or two 32-step time fragments per wave (128- or
+    256-step workgroup tiles, PMG_EMISSION_MT) is the same exact integer contraction:
+    delta, block references and the f64 ll bit-identical, ragged T and L included."""
+    import torch
+    from poor_man_gplvm_amd.engine import DeviceEM, SpikeData
+    d = make(37, L, T)
+    out = {}
+    for mt in ("1", "2"):
+        monkeypatch.setenv("PMG_EMISSION_MT", mt)
+        eng = DeviceEM(SpikeData(d['y']), L)
+        eng.ll64 = torch.empty((T, L), dtype=torch.float64, device='cuda')
+        eng.set_tuning(d['tuning'])
+        eng.emission(1.0)
+        eng.emission_status()
+        out[mt] = [x.cpu().numpy() for x in (eng.delta, eng.rblk, eng.ll64)]
+    for a, b in zip(out["1"], out["2"]):
+        np.testing.assert_array_equal(a, b)

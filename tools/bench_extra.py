@@ -78,6 +78,48 @@ def main():
     s2 = timed(masked, 10, 0)
     out["masked_lml_ms_per_mask"] = 1e3 * s2
     out["masked_lml_kernels_ms"] = {k: round(v[1], 4) for k, v in e2.timer.summary().items()}
+
+    # get_downsampled_lml's default n_repeat = 10 masks, batched (one emission contraction,
+    # then per group: stacked masks, row references, one forward launch without alpha)
+    R = 10
+    rng = np.random.default_rng(1)
+    masks = np.zeros((R, L), np.uint8)
+    for r in range(R):
+        masks[r, rng.choice(L, int(0.2 * L), replace=False)] = 1
+    e2.set_ma_latent(None)
+    e2.timer = None
+    delta0, rblk0 = e2.emission_unmasked()
+    mu8 = torch.as_tensor(masks, device=dev)
+    lzR = torch.zeros(R, dtype=torch.float64, device=dev)
+    Rg = e2.mask_batch_size(R)
+
+    def masked_batch():
+        for r0 in range(0, R, Rg):
+            e2.masked_logz_batched(delta0, rblk0, mu8[r0:r0 + Rg], 1.0, lzR[r0:r0 + Rg])
+
+    timed(masked_batch, 1, 2)
+    e2.timer = KernelTimer()
+    s3 = timed(masked_batch, 5, 0)
+    out["masked_lml_batched_ms_per_mask"] = 1e3 * s3 / R
+    out["masked_lml_batched_kernels_ms"] = {k: round(v[1], 4) for k, v in e2.timer.summary().items()}
+
+    # naive-Bayes shuffles (test.shuffle_and_decode's default decoder), batched by stacking
+    from poor_man_gplvm_amd import PoissonGPLVMJump1D
+    from poor_man_gplvm_amd import test as PT
+    m = PoissonGPLVMJump1D(N, n_latent_bin=L)
+    m.tuning = tun
+    dec = PT.ShuffleDecoder(m, y, 'naive_bayes')
+    nsh = 8
+    shifts = [np.random.default_rng(10 + i).integers(0, T, size=N) for i in range(nsh)]
+    dec.decode_naive_bayes_batch(shifts)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    dec.decode_naive_bayes_batch(shifts)
+    out["nb_shuffle_batched_ms_per_shuffle_incl_host_copies"] = 1e3 * (time.perf_counter() - t0) / nsh
+    t0 = time.perf_counter()
+    for s in shifts[:2]:
+        dec.decode(s)
+    out["nb_shuffle_sequential_ms_per_shuffle_incl_host_copies"] = 1e3 * (time.perf_counter() - t0) / 2
     print(json.dumps(out), flush=True)
 
 
