@@ -100,7 +100,8 @@ __device__ __forceinline__ int xcd_group(int bid, int nwg) {
 // per time tile, so their traffic is T / ET x 5 Lp Kp bytes.
 // MT = 1: 80 accumulator registers, <= 128 per lane so two workgroups share a CU (one's
 // epilogue beside the other's MFMAs); MT = 2: 160, one workgroup per CU.
-template <int MT>
+// LL: the f64 ll rows are written (exact decodes); the EM passes skip those stores.
+template <int MT, bool LL>
 __global__ void __launch_bounds__(512, MT == 1 ? 4 : 2) k_emission_i8(
     const int8_t* __restrict__ yq, const int8_t* __restrict__ qd,
     const double* __restrict__ lamsum, const double* __restrict__ gconst,
@@ -236,10 +237,12 @@ __global__ void __launch_bounds__(512, MT == 1 ? 4 : 2) k_emission_i8(
     const float dv = (float)(v - mx);
     const uint32_t od = lvalid ? (uint32_t)(tr * L + l - l0 + l0) * 4u : kNoWrite;
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dv), rd, od, 0, 0);
-    const unsigned long long vu = (unsigned long long)__double_as_longlong(v);
-    const uint32_t ol = lvalid ? 2u * od : kNoWrite;
-    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)vu, rl, ol, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(vu >> 32), rl, ol + 4, 0, 0);
+    if constexpr (LL) {
+      const unsigned long long vu = (unsigned long long)__double_as_longlong(v);
+      const uint32_t ol = lvalid ? 2u * od : kNoWrite;
+      __builtin_amdgcn_raw_buffer_store_b32((uint32_t)vu, rl, ol, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(vu >> 32), rl, ol + 4, 0, 0);
+    }
     const uint32_t orb = r == 0 ? (uint32_t)(tr * nblk + blk) * 8u : kNoWrite;
     const unsigned long long mu = (unsigned long long)__double_as_longlong(mx);
     __builtin_amdgcn_raw_buffer_store_b32((uint32_t)mu, rr, orb, 0, 0);
@@ -421,8 +424,10 @@ int pmg_emission_poisson(const int8_t* yq, const double* gconst, const double* t
   const int MT = (mt_s && atoi(mt_s) == 2) ? 2 : 1;
   const int64_t ET = 128 * MT;
   const int64_t nTT = (T + ET - 1) / ET;
-  hipLaunchKernelGGL(MT == 2 ? k_emission_i8<2> : k_emission_i8<1>, dim3((unsigned)(nLT * nTT)), dim3(512), 0, st,
-                     yq, qd, lamsum, gconst, ma_latent, T, Tp, L, Lp, Kp, nLT, delta, rblk, ll64);
+  auto kern = MT == 2 ? (ll64 ? k_emission_i8<2, true> : k_emission_i8<2, false>)
+                      : (ll64 ? k_emission_i8<1, true> : k_emission_i8<1, false>);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(nLT * nTT)), dim3(512), 0, st, yq, qd, lamsum, gconst, ma_latent, T, Tp,
+                     L, Lp, Kp, nLT, delta, rblk, ll64);
   PMG_LAUNCH_CHECK();
   return PMG_OK;
 }

@@ -316,10 +316,18 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
       bb[i][k].x = (l < L && q < NB) ? p.basis[(size_t)l * NB + q] : 0.f;
       bb[i][k].y = (l + 1 < L && q < NB) ? p.basis[(size_t)(l + 1) * NB + q] : 0.f;
     }
-  double yws[SP];
+  // per-thread constants and the running F of the lane's row live in LDS, not in
+  // registers (each read once per slot per body): the kernel sits at the 256-VGPR cap
+  // and every register spilled instead costs a scratch reload + vmcnt wait per body
+  __shared__ double sYw[SP][kThreads];
+  __shared__ double sTw[kThreads];
+  __shared__ double sF[SP][kThreads];
 #pragma unroll
-  for (int s = 0; s < SP; ++s) yws[s] = (is_row && s < S) ? p.yw[(size_t)lrow * p.N + n0 + s] : 0.0;
-  const double twd = is_row ? p.tw[lrow] : 0.0;
+  for (int s = 0; s < SP; ++s) {
+    sYw[s][tid] = (is_row && s < S) ? p.yw[(size_t)lrow * p.N + n0 + s] : 0.0;
+    sF[s][tid] = 0.0;
+  }
+  sTw[tid] = is_row ? p.tw[lrow] : 0.0;
   for (int q = tid; q < kSMax * QS; q += blockDim.x) {
     sW[q] = 0.0;
     sD[q] = 0.f;
@@ -349,6 +357,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
   // memory wait inside the loop); later bodies read it from the workspace
   const int mi = p.maxiter > 1 ? p.maxiter : 1;
   __shared__ double sBias[2 * kBiasLds];
+  const double* bias2 = p.bias + mi;
   for (int q = tid; q < kBiasLds && q < mi; q += blockDim.x) {
     sBias[q] = p.bias[q];
     sBias[kBiasLds + q] = p.bias[mi + q];
@@ -364,9 +373,6 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
   double fin_loss = 0.0;
   const int maxiter = p.maxiter;
   const bool eval_only = maxiter <= 1;
-  double Fs[SP];                           // F of the lane's row, per neuron (f64)
-#pragma unroll
-  for (int s = 0; s < SP; ++s) Fs[s] = 0.0;
 
   for (int k = 0;; ++k) {
     // ---- phase A: F = B W_k on the lane's row, softplus, loss, G -----------------
@@ -411,10 +417,10 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
           x[2 * i] = a.x;
           x[2 * i + 1] = a.y;
         }
-        F = Fs[s] + (double)reduce_scatter16<A>(x);
+        F = sF[s][tid] + (double)reduce_scatter16<A>(x);
       }
-      Fs[s] = F;
-      const double ywd = yws[s];
+      sF[s][tid] = F;
+      const double ywd = sYw[s][tid], twd = sTw[tid];
       // softplus / sigmoid in f32 at Fh = f32(F), corrected to first order in the
       // exact residual r = F - Fh (|r| <= 2^-24 |F|): f = softplus(Fh) + sigmoid(Fh) r
       const float Fh = (float)F;
@@ -509,9 +515,15 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
         const double nu = (1.0 - p.b2) * gr * gr + p.b2 * nu_cur;
         // this body's bias corrections (uniform); bodies run ahead of the decision past
         // maxiter are discarded
-        const int kb = k < mi ? k : mi - 1;
-        const double c1 = kb < kBiasLds ? sBias[kb] : p.bias[kb];
-        const double c2 = kb < kBiasLds ? sBias[kBiasLds + kb] : p.bias[mi + kb];
+        const int kb = __builtin_amdgcn_readfirstlane(k < mi ? k : mi - 1);
+        double c1, c2;
+        if (kb < kBiasLds) {
+          c1 = sBias[kb];
+          c2 = sBias[kBiasLds + kb];
+        } else {
+          c1 = p.bias[kb];
+          c2 = bias2[kb];
+        }
         const double mh = mu * c1;
         const double nh = nu * c2;
         w_cur = w_cur - p.lr * (mh * rcp_nr(sqrt(nh + p.eps_root) + p.eps));

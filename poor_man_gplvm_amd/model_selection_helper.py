@@ -55,6 +55,41 @@ def _dist():
     return None
 
 
+_LOCAL_DEPTH = [0]     # > 0: inside a loop that is already sharded over ranks
+
+
+class _local_only:
+    """Inside an outer rank-sharded loop (e.g. evaluate_model_one_config's fits) the
+    inner loops run locally: ranks process different items, so no collective of theirs
+    may pair up."""
+
+    def __enter__(self):
+        _LOCAL_DEPTH[0] += 1
+
+    def __exit__(self, *exc):
+        _LOCAL_DEPTH[0] -= 1
+        return False
+
+
+def shard_map(n, fn):
+    """Items 0..n-1 spread over the torch.distributed ranks (item k on rank k % world):
+    fn(list of this rank's item indices) -> list of their results, in that order; the
+    results of every rank are gathered (all_gather_object) and returned in item order
+    on every rank.  Without an initialised process group: fn(range(n)).  The shard axis
+    of the embarrassingly parallel loops of model selection and the shuffle tests
+    (get_downsampled_lml's masks, shuffle_and_decode's shuffles)."""
+    dist = _dist() if _LOCAL_DEPTH[0] == 0 else None
+    rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)
+    idx = list(range(rank, n, world))
+    mine = list(zip(idx, fn(idx) if idx else []))
+    if dist and world > 1:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, mine)
+        mine = [item for part in gathered for item in part]
+    mine.sort(key=lambda r: r[0])
+    return [r for _, r in mine]
+
+
 def fit_model_one_config(config, y_train, key=0, fit_kwargs=default_fit_kwargs, model_class_str='poisson',
                          n_repeat=1, fit_fn=None):
     """model_selection_helper.py:35-60.  `fit_fn(model, y, key, fit_kwargs) -> em_res`
@@ -110,7 +145,9 @@ def get_downsampled_lml(model_fit, y_test, downsample_frac=0.2, n_repeat=10, key
     kwargs are decode_latent's (tuning, hyperparam, ma_neuron, likelihood_scale)."""
     masks = downsample_latent_masks(model_fit.n_latent_bin, downsample_frac, n_repeat, key)
     kw = {k: v for k, v in kwargs.items() if k in ('tuning', 'hyperparam', 'ma_neuron', 'likelihood_scale')}
-    lml_l = model_fit.log_marginal_masked(y_test, masks, **kw)
+    # masks sharded over ranks when a process group is up (each rank: one batched pass)
+    lml_l = np.asarray(shard_map(len(masks), lambda idx: list(model_fit.log_marginal_masked(y_test, masks[idx], **kw))),
+                       np.float64)
     return {'value': np.mean(lml_l), 'std': np.std(lml_l)}
 
 
@@ -161,16 +198,17 @@ def evaluate_model_one_config(model_fit_l, y_test, key=1, n_time_per_chunk=10000
     rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)
     mine = {}
     for k in range(rank, len(model_fit_l), world):
-        m = model_fit_l[k]
-        dec = m.decode_latent(y_test, n_time_per_chunk=n_time_per_chunk)
-        v = {'lml': dec['log_marginal_final'],
-             'os': np.asarray(dec['log_one_step_predictive_marginals_all']).sum()}
-        if want_ds:
-            v['ds'] = [get_downsampled_lml(m, y_test, downsample_frac=f, n_repeat=downsample_n_repeat, key=key)['value']
-                       for f in latent_downsample_frac]
-        if want_jump:
-            v['jp'] = np.asarray(dec['posterior_dynamics_marg'])[:, jump_dynamics_index]
-        mine[k] = v
+        with _local_only():          # the fits are the shard axis here
+            m = model_fit_l[k]
+            dec = m.decode_latent(y_test, n_time_per_chunk=n_time_per_chunk)
+            v = {'lml': dec['log_marginal_final'],
+                 'os': np.asarray(dec['log_one_step_predictive_marginals_all']).sum()}
+            if want_ds:
+                v['ds'] = [get_downsampled_lml(m, y_test, downsample_frac=f, n_repeat=downsample_n_repeat, key=key)['value']
+                           for f in latent_downsample_frac]
+            if want_jump:
+                v['jp'] = np.asarray(dec['posterior_dynamics_marg'])[:, jump_dynamics_index]
+            mine[k] = v
     if dist and world > 1:
         parts = [None] * world
         dist.all_gather_object(parts, mine)

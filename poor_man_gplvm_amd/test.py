@@ -150,17 +150,22 @@ def shuffle_and_decode(model, spk_tsdf, n_time_per_chunk=10000, dt_l=1, n_shuffl
     y = np.asarray(spk_tsdf.d if _is_tsd(spk_tsdf) else spk_tsdf)
     if n_shuffle < 1:
         raise ValueError("n_shuffle must be >= 1")
+    from .model_selection_helper import shard_map
     dec = ShuffleDecoder(model, y, decoder_type, dt_l)
-    if decoder_type == 'naive_bayes':
-        # batched: every shuffle's shifts drawn first, in the reference's order (the same
-        # np.random calls), then Rg shuffles decoded per pass
-        shifts = [_shifts(*y.shape) for _ in range(n_shuffle)]
-        Rg = dec.nb_batch_size(n_shuffle)
-        res_l = []
-        for i in range(0, n_shuffle, Rg):
-            res_l.extend(dec.decode_naive_bayes_batch(shifts[i:i + Rg]))
-    else:
-        res_l = [dec.decode(_shifts(*y.shape)) for _ in range(n_shuffle)]
+    # every shuffle's shifts drawn first, in the reference's order (the same np.random
+    # calls on every rank); the shuffles are then sharded over the torch.distributed ranks
+    # when a process group is up, and gathered back in order
+    shifts = [_shifts(*y.shape) for _ in range(n_shuffle)]
+
+    def run(idx):
+        if decoder_type != 'naive_bayes':
+            return [dec.decode(shifts[i]) for i in idx]
+        Rg = dec.nb_batch_size(len(idx))      # batched: Rg shuffles decoded per pass
+        out = []
+        for j in range(0, len(idx), Rg):
+            out.extend(dec.decode_naive_bayes_batch([shifts[i] for i in idx[j:j + Rg]]))
+        return out
+    res_l = shard_map(n_shuffle, run)
     return {k: np.array([d[k] for d in res_l]) for k in res_l[0].keys()}
 
 

@@ -80,3 +80,31 @@ def test_evaluation_sharding_world2_matches_single_process():
         for k in ref:
             np.testing.assert_array_equal(got[k]['value_per_fit'], ref[k]['value_per_fit'])
             np.testing.assert_equal(got[k]['best_index'], ref[k]['best_index'])
+
+
+def _shard_worker(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from poor_man_gplvm_amd import model_selection_helper as msh
+    seen = []
+
+    def fn(idx):
+        seen.extend(idx)
+        return [{'k': i, 'v': np.arange(3) * i} for i in idx]
+    res = msh.shard_map(7, fn)
+    out[rank] = ([r['k'] for r in res], [r['v'].tolist() for r in res], seen)
+    dist.destroy_process_group()
+
+
+def test_shard_map_world2():
+    """shard_map (the rank axis of get_downsampled_lml's masks and shuffle_and_decode's
+    shuffles): item k computed on rank k % 2 only, every rank gets all results in order."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_shard_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for rank in range(2):
+        keys, vals, seen = out[rank]
+        assert keys == list(range(7))
+        assert vals == [(np.arange(3) * i).tolist() for i in range(7)]
+        assert seen == list(range(rank, 7, 2))
