@@ -40,6 +40,7 @@ constexpr int kSMax = 4;                // neurons per workgroup
 constexpr int kThreads = 512;           // L <= 512
 constexpr int kPartPerLane = 4;         // G <= 256 workgroups -> 4 partials per lane
 constexpr int kBiasLds = 1024;          // bias corrections held in LDS (bodies)
+constexpr int kXSlots = 512;            // exchange slots per workgroup (NB S <= 512 elements)
 
 struct AdamParams {
   double* W;
@@ -59,6 +60,11 @@ struct AdamParams {
   unsigned long long* lpart;  // [maxiter + kLag + 2][G] f64 bits, pre-filled with kSentinel
   unsigned long long* gpart;  // [..][G]
   int* timeout;
+  // row blocks (L > 512): workgroup g = rb Gg + gg owns rows [rb 32 A, (rb + 1) 32 A) of
+  // neuron group gg; the RB row blocks of a group swap their B^T G partials every body
+  int RB, Gg;
+  float* xbuf;                // [2][G][kXSlots] partial B^T G (body parity)
+  int* xflag;                 // [G][kNW] bodies published per wave (monotone, zeroed per launch)
   long long* prof;            // optional (PMG_ADAM_PROF): s_memtime stamps of WG 0, bodies < 64
   // batched restarts (blockIdx.y = restart r of this launch): per-restart strides of the
   // operands (elements) and of the restart's workspace slab (bytes)
@@ -93,7 +99,7 @@ __device__ __forceinline__ AdamParams adam_view(const AdamParams& p0) {
 }
 
 #define PMG_ADAM_STAMP(k, i)                                                   \
-  if (p.prof && g == 0 && tid == 0 && (k) < 64) p.prof[(k) * 8 + (i)] = __builtin_amdgcn_s_memtime();
+  if (p.prof && g == 0 && tid == 0 && (k) < 64) p.prof[(k) * 16 + (i)] = __builtin_amdgcn_s_memtime();
 
 // signalling NaN with a payload: no arithmetic result has this bit pattern
 constexpr unsigned long long kSentinel = 0x7FF4DEADBEEF0001ull;
@@ -162,6 +168,8 @@ __global__ void k_adam_prologue(AdamParams p_arg, size_t n) {
   }
   if (i < 4) stats[i] = 0.0;
   if (i == 0) timeout[0] = 0;
+  if (p.xflag)
+    for (size_t q = i; q < (size_t)p.G * 8; q += stride) p.xflag[q] = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -284,10 +292,12 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
   __shared__ int sCtl[4];
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wid = tid >> 6;
+  const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index: uniform (SGPR)
   const bool ctl = wid == kNW - 1;                     // runs the decision pipeline
   const int g = blockIdx.x;
-  const int n0 = g * p.S;
+  const int rb = g / p.Gg, gg = g - rb * p.Gg;         // row block, neuron group
+  const int r0 = rb * 32 * A;                          // first row of this workgroup
+  const int n0 = gg * p.S;
   const int S = (p.N - n0) < p.S ? (p.N - n0) : p.S;  // neurons owned (<= SP)
   const int L = p.L, NB = p.NB;
   const double sd = p.prior_std, isd2 = 1.0 / (sd * sd);
@@ -297,7 +307,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
   const int lb = wid * 4 + (lane >> 4);                // l-block (rows lb*A ..)
   const int qb = lane & 15;                            // q-block (cols qb*BC ..)
   const int slot = scatter_slot<A>(lane);
-  const int lrow = lb * A + slot;                      // the row this lane evaluates
+  const int lrow = r0 + lb * A + slot;                 // the row this lane evaluates
   const bool owner = (lane & 15) < A;                  // one lane per row slot
   const bool is_row = owner && lrow < L;
   // element (q, s) of the Adam update
@@ -312,7 +322,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
   for (int i = 0; i < A / 2; ++i)
 #pragma unroll
     for (int k = 0; k < BC; ++k) {
-      const int l = lb * A + 2 * i, q = qb * BC + k;
+      const int l = r0 + lb * A + 2 * i, q = qb * BC + k;
       bb[i][k].x = (l < L && q < NB) ? p.basis[(size_t)l * NB + q] : 0.f;
       bb[i][k].y = (l + 1 < L && q < NB) ? p.basis[(size_t)(l + 1) * NB + q] : 0.f;
     }
@@ -337,7 +347,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
   // element state (W, mu, nu) of this thread's weight, and its ring of the last kRing
   // states in LDS (each slot written and read by its own thread: no barrier, no HBM)
   double w_cur = 0.0, mu_cur = 0.0, nu_cur = 0.0;
-  constexpr int RS = 128 * SP;                         // ring slab per state: NB <= 128 columns
+  constexpr int RS = 16 * BC * SP;                     // ring slab per state: NB <= 16 BC columns
   __shared__ double sRing[kRing * 3 * RS];
   const int e = eq * SP + es;
   const int ewo = es * QS + (eq / BC) * BCP + eq % BC; // this element's sW / sD slot
@@ -502,13 +512,66 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
     PMG_ADAM_STAMP(k, 2)
     // ---- Adam element update ------------------------------------------------------
     double gsq = 0.0;
+    float gsum = 0.f;
+    // the element's LDS indices re-derived here from an opaque copy of tid (a few VALU
+    // per body) instead of being held across the loop: at the 256-VGPR cap the
+    // allocator would spill them, and each scratch reload waits on vmcnt
+    int tq = tid;
+    asm volatile("" : "+v"(tq));
+    const int eq_ = tq / SP, es_ = tq % SP;
+    const int e_ = eq_ * SP + es_;
+    const int ewo_ = es_ * QS + (eq_ / BC) * BCP + eq_ % BC;
     if (is_el) {
-      float gsum = 0.f;
 #pragma unroll
-      for (int w = 0; w < kNW; ++w) gsum += sPart[(w * SP + es) * 16 * BC + eq];
+      for (int w = 0; w < kNW; ++w) gsum += sPart[(w * SP + es_) * 16 * BC + eq_];
+    }
+    // (row blocks exist only with A = 8, L in (512, 1024]: the other instances carry no
+    // exchange code, which would cost them registers)
+    if (A == 8 && p.RB > 1 && wid * 64 < NB * SP) {
+      // row blocks: this workgroup's partial B^T G (its rows) to the other row blocks of
+      // the group, theirs back; every block sums the RB partials in block order, so all
+      // of them run the identical update.  Message passing per wave: the data as
+      // agent-scope (sc1, cache-bypassing) stores, vmcnt(0) so they are performed, then the
+      // flag = bodies published; the partner polls the flag, then reads the data with sc1
+      // loads.  Data and flags never sit in the non-coherent L2, so no agent-scope fence
+      // (an XCD-wide L2 writeback / invalidate per wave and body) is needed.  Two body-
+      // parity buffers suffice: a block publishes body k + 2 only after every partner has
+      // published body k + 1, i.e. after each has read its body-k partials.
+      float* xb = p.xbuf + (size_t)(k & 1) * p.G * kXSlots;
+      if (is_el) __hip_atomic_store(&xb[(size_t)g * kXSlots + e_], gsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(&p.xflag[g * kNW + wid], k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      float tot = 0.f;
+      for (int rr = 0; rr < p.RB; ++rr) {
+        const int gp = rr * p.Gg + gg;
+        if (rr != rb) {
+          unsigned spins = 0;
+          while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&p.xflag[gp * kNW + wid], __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_AGENT)) < k + 1) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 24)) {
+              if (lane == 0) {
+                atomicOr(p.timeout, 1);
+                sCtl[2] = 1;
+              }
+              break;
+            }
+          }
+          asm volatile("" ::: "memory");
+        }
+        const float v = rr == rb ? gsum
+                                 : (is_el ? __hip_atomic_load(&xb[(size_t)gp * kXSlots + e_], __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT)
+                                          : 0.f);
+        tot += v;
+      }
+      gsum = tot;
+    }
+    if (is_el) {
       const double gr = -(double)gsum + w_cur * isd2;
-      gsq = gr * gr;
-      lpart += 0.5 * w_cur * w_cur * isd2 + lconst;
+      // the prior and |g|^2 terms once per neuron group (row block 0)
+      gsq = rb == 0 ? gr * gr : 0.0;
+      lpart += rb == 0 ? 0.5 * w_cur * w_cur * isd2 + lconst : 0.0;
       const double w_old = w_cur;
       if (!eval_only) {  // optax 0.2.2 scale_by_adam + scale(-lr)
         const double mu = (1.0 - p.b1) * gr + p.b1 * mu_cur;
@@ -531,11 +594,11 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
         nu_cur = nu;
       }
       const int ns = (k + 1) % kRing;
-      sW[ewo] = w_cur;
-      sD[ewo] = (float)(w_cur - w_old);
-      sRing[(ns * 3 + 0) * RS + e] = w_cur;
-      sRing[(ns * 3 + 1) * RS + e] = mu_cur;
-      sRing[(ns * 3 + 2) * RS + e] = nu_cur;
+      sW[ewo_] = w_cur;
+      sD[ewo_] = (float)(w_cur - w_old);
+      sRing[(ns * 3 + 0) * RS + e_] = w_cur;
+      sRing[(ns * 3 + 1) * RS + e_] = mu_cur;
+      sRing[(ns * 3 + 2) * RS + e_] = nu_cur;
     }
     lpart = wave_sum_f64(lpart);
     gsq = wave_sum_f64(gsq);
@@ -543,7 +606,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
       sSum[wid] = lpart;
       sSum[kNW + wid] = gsq;
     }
-    if (p.prof && g == 0 && tid == kThreads - 64 && k < 64) p.prof[k * 8 + 5] = __builtin_amdgcn_s_memtime();
+    if (p.prof && g == 0 && tid == kThreads - 64 && k < 64) p.prof[k * 16 + 5] = __builtin_amdgcn_s_memtime();
     if (ctl && k > 0) {
       // ---- decision pipeline (control wave) over bodies dj .. k-1 ---------------
       // Partials are pre-filled with a signalling-NaN sentinel (never produced by
@@ -559,6 +622,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
 #pragma unroll
         for (int q = 0; q < kPartPerLane; ++q) ok &= (lv0[q] != kSentinel);
         ok = __all(ok);
+        if (p.prof && g == 0 && lane == 0 && k < 64 && rep == 0) p.prof[k * 16 + 8] = __builtin_amdgcn_s_memtime();
         if (!ok && must) {  // blocking re-poll of body dj
           unsigned spins = 0;
           while (!ok) {
@@ -568,7 +632,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
 #pragma unroll
             for (int q = 0; q < kPartPerLane; ++q) ok &= (lv0[q] != kSentinel);
             ok = __all(ok);
-            if (p.prof && g == 0 && lane == 0 && k < 64) p.prof[k * 8 + 7] += 1;
+            if (p.prof && g == 0 && lane == 0 && k < 64) p.prof[k * 16 + 7] += 1;
             if (++spins > (1u << 24)) {
               if (lane == 0) {
                 atomicOr(p.timeout, 1);
@@ -584,6 +648,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
           break;
         }
         const double loss = sum_parts(lv0);
+        if (p.prof && g == 0 && lane == 0 && k < 64 && rep == 0) p.prof[k * 16 + 9] = __builtin_amdgcn_s_memtime();
         const int j = dj;
         if (j == 0) {
           loss0 = loss;
@@ -608,6 +673,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
         issued0 = issued1;
         issued1 = false;
       }
+      if (p.prof && g == 0 && lane == 0 && k < 64) p.prof[k * 16 + 10] = __builtin_amdgcn_s_memtime();
       if (!sCtl[0]) {  // keep bodies dj and dj+1 in flight (both <= last)
         if (!issued0 && dj <= last) {
           load_parts(p, dj, lane, lv0);
@@ -619,7 +685,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
         }
       }
     }
-    if (p.prof && g == 0 && tid == kThreads - 64 && k < 64) p.prof[k * 8 + 6] = __builtin_amdgcn_s_memtime();
+    if (p.prof && g == 0 && tid == kThreads - 64 && k < 64) p.prof[k * 16 + 6] = __builtin_amdgcn_s_memtime();
     PMG_ADAM_STAMP(k, 3)
     PMG_LDS_BARRIER();
     if (sCtl[0] || sCtl[2]) break;
@@ -634,6 +700,13 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
     }
     PMG_ADAM_STAMP(k, 4)
   }
+  // Row blocks: the blocks of a group learn the stop at bodies up to kLag apart (each
+  // control wave decides as soon as the partials are there), so a block that leaves
+  // first releases its partners: a flag no body index reaches.  They finish their (at
+  // most kLag) speculative bodies past the stop on stale partials, which the ring
+  // discards: the state written below is the one after the stop body.
+  if (A == 8 && p.RB > 1 && wid * 64 < NB * SP && lane == 0)
+    __hip_atomic_store(&p.xflag[g * kNW + wid], 0x7fffffff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int stop_j = sCtl[1];
   // ---- write the state after body stop_j (W_{stop_j+1}) from the ring ---------
   const int fs = eval_only ? (1 % kRing) : ((stop_j + 1) % kRing);
@@ -684,15 +757,25 @@ struct AdamWork {
   unsigned long long* gpart;
   double* bias;
   int* timeout;
+  float* xbuf;
+  int* xflag;
 };
 
+static int num_cus();
+
+// G <= #CUs workgroups (all co-resident): the partial arrays and the row-block exchange
+// are sized for #CUs, so one size serves every row-block split of a shape
 static size_t adam_ws(int G, int maxiter, AdamWork* w, void* base) {
+  const int cus = num_cus();
+  const size_t Gw = (size_t)(G > cus ? G : cus);
   Carver c(base);
   AdamWork ww;
   ww.timeout = c.take<int>(64);
-  ww.lpart = c.take<unsigned long long>(((size_t)maxiter + kLag + 2) * G);
-  ww.gpart = c.take<unsigned long long>(((size_t)maxiter + kLag + 2) * G);
+  ww.lpart = c.take<unsigned long long>(((size_t)maxiter + kLag + 2) * Gw);
+  ww.gpart = c.take<unsigned long long>(((size_t)maxiter + kLag + 2) * Gw);
   ww.bias = c.take<double>(2 * (size_t)maxiter);
+  ww.xbuf = c.take<float>(2 * Gw * kXSlots);
+  ww.xflag = c.take<int>(Gw * kNW);
   if (w) *w = ww;
   return c.off + 256;
 }
@@ -708,11 +791,15 @@ template <int A, int BC>
 static AdamKernel pick_sp(int S) {
   if (S <= 1) return {k_adam<A, BC, 1>, 0};
   if (S <= 2) return {k_adam<A, BC, 2>, 0};
-  return {k_adam<A, BC, 4>, 0};
+  if constexpr (16 * BC * 4 <= kThreads) return {k_adam<A, BC, 4>, 0};   // NB S <= 512
+  return {nullptr, 0};
 }
 
 template <int A>
 static AdamKernel pick_bc(int NB, int S) {
+  if constexpr (A == 8) {    // row-block split (L > 512, BASELINE C4: NB = 154)
+    if (NB > 128 && NB <= 160) return pick_sp<A, 10>(S);
+  }
   if (NB <= 32) return pick_sp<A, 2>(S);
   if (NB <= 48) return pick_sp<A, 3>(S);
   if (NB <= 64) return pick_sp<A, 4>(S);
@@ -722,13 +809,17 @@ static AdamKernel pick_bc(int NB, int S) {
   return {nullptr, 0};
 }
 
-// rows per l-block A = ceil(L / 32) rounded up to 4 / 8 / 16
+// rows per l-block A = ceil(L / 32) rounded up to 4 / 8 / 16; L in (512, 1024]: row blocks
+// of 256 rows (A = 8), adam_row_blocks
 static AdamKernel pick_adam(int NB, int L, int S) {
   if (L <= 128) return pick_bc<4>(NB, S);
   if (L <= 256) return pick_bc<8>(NB, S);
   if (L <= 512) return pick_bc<16>(NB, S);
+  if (L <= 1024) return pick_bc<8>(NB, S);
   return {nullptr, 0};
 }
+
+static int adam_row_blocks(int L) { return L <= 512 ? 1 : (L + 255) / 256; }
 
 static int num_cus() {
   int dev = 0, cus = 0;
@@ -737,12 +828,19 @@ static int num_cus() {
   return cus > 0 ? cus : 256;
 }
 
-static void adam_geometry(int N, int L, int NB, int& S, int& G, int& ng, int& LG) {
+// RB row blocks x Gg neuron groups of S neurons, G = RB Gg <= #CUs
+static void adam_geometry(int N, int L, int NB, int& S, int& G, int& ng, int& LG, int* RBo = nullptr,
+                          int* Ggo = nullptr) {
   const int cus = num_cus();
-  S = (N + cus - 1) / cus;
+  const int RB = adam_row_blocks(L);
+  const int gmax = cus / RB > 0 ? cus / RB : 1;
+  S = (N + gmax - 1) / gmax;
   if (S < 1) S = 1;
   if (S == 3) S = 4;
-  G = (N + S - 1) / S;
+  const int Gg = (N + S - 1) / S;
+  G = RB * Gg;
+  if (RBo) *RBo = RB;
+  if (Ggo) *Ggo = Gg;
   ng = kThreads / NB;
   if (ng < 1) ng = 1;
   LG = (L + ng - 1) / ng;
@@ -784,10 +882,10 @@ size_t pmg_mstep_workspace_size(int32_t N, int32_t maxiter) {
 }
 
 int pmg_mstep_adam_supported(int32_t L, int32_t NB, int32_t N) {
-  if (L <= 0 || L > kThreads || NB <= 0 || N <= 0) return 0;
+  if (L <= 0 || L > 2 * kThreads || NB <= 0 || N <= 0) return 0;
   int S, G, ng, LG;
   adam_geometry(N, L, NB, S, G, ng, LG);
-  if (S > kSMax || NB * S > kThreads) return 0;
+  if (S > kSMax || NB * S > kThreads || G > num_cus()) return 0;
   AdamKernel kern = pick_adam(NB, L, S);
   return (kern.fn != nullptr && kern.lds <= 160 * 1024) ? 1 : 0;
 }
@@ -799,10 +897,14 @@ static int adam_run(double* W, double* mu, double* nu, int64_t* count, const flo
                     double* loss_hist, double* err_hist, void* workspace, size_t workspace_bytes, hipStream_t st) {
   PMG_REQUIRE(cfg && W && mu && nu && count && basis && yw && tw && stats && loss_hist && err_hist && workspace,
               "pmg_mstep_adam: null argument");
-  PMG_REQUIRE(L > 0 && L <= kThreads, "pmg_mstep_adam: L=%d must be in [1, %d]", L, kThreads);
+  PMG_REQUIRE(L > 0 && L <= 2 * kThreads, "pmg_mstep_adam: L=%d must be in [1, %d]", L, 2 * kThreads);
   PMG_REQUIRE(NB > 0 && N > 0 && R >= 1 && R <= 65535, "pmg_mstep_adam: bad shape");
+  PMG_REQUIRE(R == 1 || L <= kThreads, "pmg_mstep_adam: batched restarts need L <= %d", kThreads);
   int S, G, ng, LG, Rg;
   adam_batch_geometry(N, L, NB, R, S, G, ng, LG, Rg);
+  int RB = 1, Gg = G;
+  if (R == 1) adam_geometry(N, L, NB, S, G, ng, LG, &RB, &Gg);
+  PMG_REQUIRE(G <= num_cus(), "pmg_mstep_adam: %d workgroups (%d row blocks) exceed the %d CUs", G, RB, num_cus());
   PMG_REQUIRE(S <= kSMax, "pmg_mstep_adam: N=%d needs %d neurons per workgroup (> %d)", N, S, kSMax);
   PMG_REQUIRE(NB * S <= kThreads, "pmg_mstep_adam: NB*S=%d > %d", NB * S, kThreads);
   AdamKernel kern = pick_adam(NB, L, S);
@@ -850,11 +952,15 @@ static int adam_run(double* W, double* mu, double* nu, int64_t* count, const flo
   p.rs_tw = L;
   p.rs_hist = maxiter;
   p.rs_ws = (int64_t)slab;
+  p.RB = RB;
+  p.Gg = Gg;
+  p.xbuf = RB > 1 ? w.xbuf : nullptr;
+  p.xflag = RB > 1 ? w.xflag : nullptr;
   static long long* prof_buf = nullptr;   // debug: per-phase stamps (PMG_ADAM_PROF set)
   const bool prof = getenv("PMG_ADAM_PROF") != nullptr;
   if (prof) {
-    if (!prof_buf) PMG_HIP(hipMalloc(&prof_buf, 64 * 8 * sizeof(long long)));
-    PMG_HIP(hipMemsetAsync(prof_buf, 0, 64 * 8 * sizeof(long long), st));
+    if (!prof_buf) PMG_HIP(hipMalloc(&prof_buf, 64 * 16 * sizeof(long long)));
+    PMG_HIP(hipMemsetAsync(prof_buf, 0, 64 * 16 * sizeof(long long), st));
     p.prof = prof_buf;
   } else {
     p.prof = nullptr;
@@ -885,24 +991,32 @@ static int adam_run(double* W, double* mu, double* nu, int64_t* count, const flo
     PMG_LAUNCH_CHECK();
   }
   if (prof) {
-    long long h[64 * 8];
+    long long h[64 * 16];
     PMG_HIP(hipMemcpyAsync(h, prof_buf, sizeof(h), hipMemcpyDeviceToHost, st));
     PMG_HIP(hipStreamSynchronize(st));
     double acc[6] = {0, 0, 0, 0, 0, 0};
+    double acc6 = 0, acc7 = 0, acc8 = 0;
+    int n6 = 0, n7 = 0, n8 = 0;
     long long spins = 0;
     int cnt = 0;
     for (int k = 8; k + 1 < 64; ++k) {   // skip the pipeline fill
-      if (h[k * 8 + 4] == 0 || h[(k + 1) * 8] == 0) break;
-      for (int i = 0; i < 4; ++i) acc[i] += (double)(h[k * 8 + i + 1] - h[k * 8 + i]);
-      acc[4] += (double)(h[(k + 1) * 8] - h[k * 8 + 4]);
-      acc[5] += (double)(h[k * 8 + 6] - h[k * 8 + 5]);
-      spins += h[k * 8 + 7];
+      if (h[k * 16 + 4] == 0 || h[(k + 1) * 16] == 0) break;
+      for (int i = 0; i < 4; ++i) acc[i] += (double)(h[k * 16 + i + 1] - h[k * 16 + i]);
+      acc[4] += (double)(h[(k + 1) * 16] - h[k * 16 + 4]);
+      acc[5] += (double)(h[k * 16 + 6] - h[k * 16 + 5]);
+      if (h[k * 16 + 8]) acc6 += (double)(h[k * 16 + 8] - h[k * 16 + 5]), ++n6;
+      if (h[k * 16 + 9]) acc7 += (double)(h[k * 16 + 9] - h[k * 16 + 8]), ++n7;
+      if (h[k * 16 + 10]) acc8 += (double)(h[k * 16 + 6] - h[k * 16 + 10]), ++n8;
+      spins += h[k * 16 + 7];
       ++cnt;
     }
     if (cnt > 0)
       fprintf(stderr, "[pmg adam prof] bodies=%d ticks/body: rows %.0f | bar1 %.0f | update %.0f | "
               "sums+bar2+publish %.0f | loop %.0f | decision (ctl wave) %.0f, blocking polls %lld\n", cnt,
               acc[0] / cnt, acc[1] / cnt, acc[2] / cnt, acc[3] / cnt, acc[4] / cnt, acc[5] / cnt, spins);
+    if (cnt > 0)
+      fprintf(stderr, "[pmg adam prof] decision: to first check %.0f (%d) | first sum %.0f (%d) | after loop %.0f (%d)\n",
+              n6 ? acc6 / n6 : 0.0, n6, n7 ? acc7 / n7 : 0.0, n7, n8 ? acc8 / n8 : 0.0, n8);
   }
   return PMG_OK;
 }

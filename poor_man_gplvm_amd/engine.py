@@ -419,9 +419,11 @@ class DeviceEM:
             if bad:
                 raise nat.NativeError("pmg_gaussian_mstep: normal-equation matrix is not positive definite")
 
-    # shapes the persistent one-launch Adam kernel holds (a latent row per thread, the
-    # basis row in registers + LDS); larger ones use the tiled per-body kernels
-    PERSISTENT_MAX_L, PERSISTENT_MAX_NB = 512, 128
+    # shapes the persistent one-launch Adam kernel holds (the basis block in registers;
+    # L in (512, 1024] as 256-row blocks of one neuron group exchanging their B^T G partials
+    # each body, which needs row blocks x neuron groups <= #CUs, pmg_mstep_adam_supported);
+    # the others use the tiled per-body kernels
+    PERSISTENT_MAX_L, PERSISTENT_MAX_NB = 1024, 160
 
     def adam(self, W, mu, nu, count, cfg: AdamConfig, stats_out, lh_out, eh_out, yw=None):
         """The Adam loop on W (NB, n) f64 with sufficient statistics yw (L, n) (default:

@@ -290,18 +290,22 @@ def test_suffstats_nonint_spikes_use_f32_path():
                                                    (30, 100, 40, 0.0, True), (30, 100, 1000, 1e-6, True),
                                                    (7, 48, 1, 1e-6, True), (7, 48, 2, 1e-6, True),
                                                    (64, 1024, 30, 0.0, True), (40, 700, 1000, 1e-6, True),
-                                                   (20, 100, 40, 0.0, False)])
+                                                   (20, 100, 40, 0.0, False),
+                                                   (64, 1024, 30, 0.0, False), (40, 700, 1000, 1e-6, False),
+                                                   (128, 1024, 200, 1e-6, False)])
 def test_adam_vs_oracle(N, L, maxiter, tol, tiled):
-    """tiled: pmg_mstep_adam_tiled (forced for small shapes; L > 512 / NB > 128 always).
-    (20, 100, ..., False) is the class default basis (ls = 1 => NB = 101): the
-    persistent kernel does not hold it and pmg_mstep_adam_supported routes it to
-    the tiled kernel."""
+    """tiled: pmg_mstep_adam_tiled (forced).  (20, 100, ..., False) is the class
+    default basis (ls = 1 => NB = 101): the persistent kernel does not hold it and
+    pmg_mstep_adam_supported routes it to the tiled kernel.  L = 700 / 1024 untiled:
+    the persistent kernel's row blocks (3 / 4 blocks of 256 rows per neuron group,
+    partial B^T G exchanged every body; 1024 with NB = 154, the C4 basis)."""
     from poor_man_gplvm_amd.engine import AdamConfig
     d = make(N, L, 500)
     sp, eng = _engine(d, L)
     if tiled:
         eng.PERSISTENT_MAX_L = 0
-    assert eng.L <= 512 or tiled
+    elif L > 512:
+        assert eng.lib.pmg_mstep_adam_supported(eng.L, eng.NB, N) == 1
     P = np.exp(d['lp0'].astype(np.float64))
     yw, tw = O.get_statistics(d['lp0'].astype(np.float64), d['y'])
     eng.yw.copy_(torch.as_tensor(yw, device='cuda'))
