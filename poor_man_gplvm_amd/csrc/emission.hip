@@ -22,6 +22,8 @@
 // exp(s*(ll - max_l ll)) = exp(s*delta + phi) with 1-ulp accuracy near the max.
 #include "pmg_common.h"
 
+#include <vector>
+
 namespace pmg {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -31,10 +33,13 @@ constexpr int kDig = 5;
 constexpr double kQScale = 4294967296.0;  // 2^32
 constexpr double kQInv = 1.0 / 4294967296.0;
 
-// One wave per latent row: log(lam) -> 5 int8 digits, lamsum = sum_n m_n lam.
+// One wave per latent row: log(lam) -> 5 int8 digits, lamsum = sum_n m_n lam, and the
+// pipelined kernel's per-latent constant lconst = -lamsum (+inf: latent masked by
+// ma_latent, -inf: padding row l >= L).
 __global__ void __launch_bounds__(256) k_rates_prepare(
     const double* __restrict__ tuning, int L, int N, const float* __restrict__ ma, double dt,
-    int Lp, int Kp, int8_t* __restrict__ qd, double* __restrict__ lamsum, int* __restrict__ bad) {
+    int Lp, int Kp, int8_t* __restrict__ qd, double* __restrict__ lamsum, int* __restrict__ bad,
+    const uint8_t* __restrict__ ma_latent, double* __restrict__ lconst) {
   const int lane = threadIdx.x & 63;
   const int l = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (l >= Lp) return;
@@ -63,7 +68,10 @@ __global__ void __launch_bounds__(256) k_rates_prepare(
     for (int d = 0; d < kDig; ++d) qd[d * plane + o] = dg[d];
   }
   ls = wave_sum_f64(ls);
-  if (lane == 0) lamsum[l] = ls;
+  if (lane == 0) {
+    lamsum[l] = ls;
+    lconst[l] = l >= L ? -INFINITY : (ma_latent && ma_latent[l] == 0) ? INFINITY : -ls;
+  }
   if (__ballot(flag)) {
     if (lane == 0) atomicOr(bad, 1);
   }
@@ -250,6 +258,549 @@ __global__ void __launch_bounds__(512, MT == 1 ? 4 : 2) k_emission_i8(
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Pipelined form (the default): the same digit GEMM and epilogue, reorganised around
+// the two limits measured on k_emission_i8 at C3 (r02/r03 PMC: MFMA busy 25 %, every
+// K-chunk waited for its own L2 round trip behind a barrier, and the 128 x 64 tile
+// moved 350 B from L2 per MFMA).
+// - Tiles of 256 time bins x 64 latents (16 waves as 8 (time) x 2 (latent), each wave
+//   32 t x 32 l x 5 digits): 225 B of staged operands per MFMA.
+// - One 1024-thread workgroup per CU walks its own list of tiles (the 8 latent tiles of a
+//   time tile on one XCD, so y rows are re-read from that XCD's L2).  The operands of
+//   each 64-neuron chunk (y: 256 rows x 64 B, digits: 5 x 64 rows x 64 B = 36 KiB) stream
+//   through a 4-slot LDS ring filled by LDS-DMA (buffer_load ... lds) three chunks ahead
+//   -- across tile boundaries, so the next tile's first chunks load during this tile's
+//   epilogue.  Each wave waits only for its own DMA pieces with a counted vmcnt, then one
+//   barrier publishes the chunk (and retires the reads of the slot the new DMA refills).
+// - The per-tile constants (gconst rows, lconst = -lamsum / +inf masked / -inf padding)
+//   arrive by the same DMA into 4 per-tile slots, so the epilogue issues no vector loads
+//   (a VGPR load would make hipcc drain the DMA queue with vmcnt(0)).
+// - LDS image: lane-linear 1 KiB pieces of 16 rows x 64 B; a row's 16-B segment s sits
+//   at s ^ ((row >> 2) & 3), applied on the DMA source address and on the read, so the
+//   ds_read_b128 fragment reads of 16 consecutive rows hit 16 distinct bank quads.
+// Bit-identical to k_emission_i8 (same integer accumulators, same f64 epilogue order).
+constexpr int PT = 256, PL = 64, PK = 64;          // tile time bins, tile latents, neurons per chunk
+constexpr int PNS = 4;                              // ring slots (3 chunks in flight)
+constexpr int PY = PT * PK;                         // y bytes per chunk
+constexpr int PSTAGE = PY + kDig * PL * PK;         // 36864 B per chunk
+constexpr int PPIECES = PSTAGE / 1024;              // 36 DMA pieces per chunk
+constexpr int PCONST = 3072;                        // per tile: 256 gconst + 64 (+64 pad) lconst doubles
+constexpr int PLDS = PNS * PSTAGE + 4 * PCONST;     // 159744 B
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 63] (the immediate must be a literal)
+__device__ __forceinline__ void vm_wait_upto(int n) {
+#define PMG_VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+#define PMG_VMW8(k) PMG_VMW(k) PMG_VMW(k + 1) PMG_VMW(k + 2) PMG_VMW(k + 3) PMG_VMW(k + 4) PMG_VMW(k + 5) \
+  PMG_VMW(k + 6) PMG_VMW(k + 7)
+  switch (n) {
+    PMG_VMW8(0) PMG_VMW8(8) PMG_VMW8(16) PMG_VMW8(24) PMG_VMW8(32) PMG_VMW8(40) PMG_VMW8(48) PMG_VMW8(56)
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+#undef PMG_VMW8
+#undef PMG_VMW
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pipe_rsrc(const void* base, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)(bytes > 0 ? bytes : 0),
+                                           0x00020000);
+}
+
+// k_emission_pipe's tile list and DMA issue (per workgroup / wave constants)
+struct PipeCtx {
+  const int8_t* yq;
+  const int8_t* qd;
+  const double* lconst;
+  const double* gconst;
+  int8_t* smem;
+  int64_t T, Tp;
+  int Lp, Kp, nLT, plane, rb, slot, nx, wid, lane, vlane;
+  bool cwave;
+
+  __device__ __forceinline__ void tile_of(int ti, int64_t& t0, int& l0) const {
+    const int g = rb + slot + ti * nx;
+    const int tt = g / nLT;
+    t0 = (int64_t)tt * PT;
+    l0 = (g - tt * nLT) * PL;
+  }
+  // DMA of chunk kc of tile ti into ring slot sl (and, for kc == 0, the tile's constants)
+  __device__ __forceinline__ void issue(int ti, int kc, int sl) const {
+    int64_t t0;
+    int l0;
+    tile_of(ti, t0, l0);
+    int8_t* dst = smem + sl * PSTAGE;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int p = wid + 16 * j;
+      if (p < PPIECES) {
+        if (p < PT / 16) {
+          const int64_t o = (t0 + 16 * p) * Kp + kc * PK;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(pipe_rsrc(yq + o, Tp * Kp - o), (lds_void_t*)(dst + p * 1024),
+                                                   16, vlane, 0, 0, 0);
+        } else {
+          const int pp = p - PT / 16, d = pp >> 2, rg = pp & 3;
+          const int o = (l0 + 16 * rg) * Kp + kc * PK;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(pipe_rsrc(qd + d * plane + o, (int64_t)plane - o),
+                                                   (lds_void_t*)(dst + p * 1024), 16, vlane, 0, 0, 0);
+        }
+      }
+    }
+    if (cwave && kc == 0) {
+      int8_t* cdst = smem + PNS * PSTAGE + (ti & 3) * PCONST + (wid - 4) * 1024;
+      if (wid < 6) {
+        const int64_t o = t0 + (wid - 4) * 128;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(pipe_rsrc(gconst + o, (T - o) * 8), (lds_void_t*)cdst, 16,
+                                                 lane * 16, 0, 0, 0);
+      } else {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(pipe_rsrc(lconst + l0, (int64_t)(Lp - l0) * 8), (lds_void_t*)cdst,
+                                                 16, (lane & 31) * 16, 0, 0, 0);
+      }
+    }
+  }
+};
+
+template <bool LL>
+__global__ void __launch_bounds__(1024) k_emission_pipe(
+    const int8_t* __restrict__ yq, const int8_t* __restrict__ qd, const double* __restrict__ lconst,
+    const double* __restrict__ gconst, int64_t T, int64_t Tp, int L, int Lp, int Kp, int nLT,
+    int ntile, float* __restrict__ delta, double* __restrict__ rblk, double* __restrict__ ll64,
+    unsigned long long* __restrict__ stamps) {
+#ifdef PMG_EM_STAMPS
+  // diagnostic build: s_memtime at 4 points of the first 64 chunks, waves 0 and 7, in the
+  // last 4 KiB of LDS, copied out per workgroup at the end
+  __shared__ __attribute__((aligned(16))) int8_t smem[PLDS + 4096];
+  unsigned long long* sst = reinterpret_cast<unsigned long long*>(smem + PLDS);
+#define PMG_EM_STAMP(x, k)                                                                        \
+  if ((wid == 0 || wid == 7) && lane == 0 && (x) < 64) {                                         \
+    sst[(wid == 7) * 256 + (x) * 4 + (k)] = __builtin_amdgcn_s_memtime();                        \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                           \
+  }
+#else
+  __shared__ __attribute__((aligned(16))) int8_t smem[PLDS];
+#define PMG_EM_STAMP(x, k)
+  (void)stamps;
+#endif
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wt = wid & 7, wl = wid >> 3;
+  const int r = lane & 31, h = lane >> 5;
+
+  // this workgroup's tiles: XCD x owns the contiguous range [x n / 8, (x + 1) n / 8) of the
+  // time-major tile order; its nx workgroups take every nx-th tile of it
+  const int nwg = gridDim.x, nx = nwg >> 3;
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int rb = (int)((int64_t)ntile * xcd / 8), re = (int)((int64_t)ntile * (xcd + 1) / 8);
+  const int mine = re - rb > slot ? (re - rb - slot + nx - 1) / nx : 0;
+  if (mine == 0) return;                                   // uniform per workgroup
+  const int nch = Kp / PK;                                 // >= 2 (Kp % 128 == 0)
+  const int S = mine * nch;                                // chunks this workgroup streams
+
+  const int plane = Lp * Kp;
+  // DMA lane map: lane i fills row i >> 2 of a 16-row piece, physical segment i & 3, i.e.
+  // logical segment (i & 3) ^ ((i >> 4) & 3).  Every wave-uniform part of a piece's source
+  // goes into its buffer descriptor (base and extent: rows past Tp / Lp / T read as 0), so
+  // the only per-lane operand is this offset.
+  const int vlane = (lane >> 2) * Kp + ((lane & 3) ^ ((lane >> 4) & 3)) * 16;
+  // fragment reads: logical segment h (k-step 0) of row 32 w + r; k-step 1 (segment 2 + h)
+  // is that address ^ 32
+  const int lrow = r * PK + (h ^ ((r >> 2) & 3)) * 16;
+  const int aoff = wt * 32 * PK + lrow;
+  const int boff = PY + wl * 32 * PK + lrow;
+  const int npieces_w = 2 + (wid < PPIECES - 32);          // pieces p = wid, wid + 16, wid + 32 < 36
+  const bool cwave = wid >= 4 && wid < 7;                  // carries one per-tile constant piece
+
+  PipeCtx cx{yq, qd, lconst, gconst, smem, T, Tp, Lp, Kp, nLT, plane, rb, slot, nx, wid, lane, vlane, cwave};
+
+  // VMEM stores one epilogue issues (at least: 16 delta + 16 rblk (+16 ll) instructions);
+  // they are younger than the DMA pieces of the following chunks, so counting them only
+  // lowers the wait (vmcnt retires in issue order: MI355X_MICROARCH.md, s_waitcnt)
+  constexpr int NST = LL ? 48 : 32;
+  // DMA cursor (chunk x + 3 as (tile, chunk))
+  int dti = 0, dkc = 0;
+  for (int x = 0; x < 3 && x < S; ++x) {
+    cx.issue(dti, dkc, x);
+    if (++dkc == nch) { dkc = 0; ++dti; }
+  }
+  v16i acc[kDig];
+  int ti = 0, kc = 0;
+  for (int x = 0; x < S; ++x) {
+    PMG_EM_STAMP(x, 0)
+    {
+      // my DMA pieces of chunks x + 1, x + 2 and the stores of epilogues at x - 3 .. x - 1
+      // may stay in flight
+      int n = 0;
+      if (x + 1 < S) n += npieces_w + (cwave && kc == nch - 1);
+      if (x + 2 < S) n += npieces_w + (cwave && kc == nch - 2);
+      n += NST * ((x >= 1 && kc == 0) + (x >= 2 && kc == 1 % nch) + (x >= 3 && kc == 2 % nch));
+      vm_wait_upto(n < 63 ? n : 63);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    PMG_EM_STAMP(x, 1)
+    if (x + 3 < S) {
+      cx.issue(dti, dkc, (x + 3) & (PNS - 1));
+      if (++dkc == nch) { dkc = 0; ++dti; }
+    }
+    PMG_EM_STAMP(x, 2)
+    if (kc == 0) {
+#pragma unroll
+      for (int d = 0; d < kDig; ++d) acc[d] = (v16i){0};
+    }
+    const int sbo = (x & (PNS - 1)) * PSTAGE;
+#ifdef PMG_EM_NOCOMPUTE
+    if (lane == 64) // never: keeps the loop's shape without the MFMAs (diagnostic build)
+#endif
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int8_t* sa = smem + sbo + (aoff ^ (32 * ks));
+      const int8_t* sq = smem + sbo + (boff ^ (32 * ks));
+      const v4i a = *reinterpret_cast<const v4i*>(sa);
+#pragma unroll
+      for (int d = 0; d < kDig; ++d) {
+        const v4i b = *reinterpret_cast<const v4i*>(sq + d * PL * PK);
+        acc[d] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc[d], 0, 0, 0);
+      }
+    }
+    const int cur = ti;
+    if (++kc < nch) {
+      PMG_EM_STAMP(x, 3)
+      continue;
+    }
+    kc = 0;
+    ++ti;
+#if defined(PMG_EM_NOCOMPUTE) || defined(PMG_EM_NOEPI)
+    if (lane < 64) {   // diagnostic builds: no epilogue
+      PMG_EM_STAMP(x, 3)
+      continue;
+    }
+#endif
+
+    // epilogue of tile cur (k_emission_i8's arithmetic, constants from the LDS slot)
+    int64_t t0;
+    int l0;
+    cx.tile_of(cur, t0, l0);
+    const int8_t* cs = smem + PNS * PSTAGE + (cur & 3) * PCONST;
+    const int nblk = Lp >> 5;
+    const int blk = (l0 >> 5) + wl;
+    const int l = l0 + wl * 32 + r;
+    const bool lvalid = l < L && blk < nblk;
+    const double lc = *reinterpret_cast<const double*>(cs + 2048 + (wl * 32 + r) * 8);
+    const int64_t nrow64 = T - t0 < PT ? T - t0 : PT;
+    const int nrow = (int)nrow64;
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(delta + t0 * (int64_t)L, (short)0,
+                                                                         nrow * L * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(rblk + t0 * (int64_t)nblk, (short)0,
+                                                                         nrow * nblk * 8, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+        LL ? (void*)(ll64 + t0 * (int64_t)L) : (void*)delta, (short)0, LL ? nrow * L * 8 : 0, 0x00020000);
+    // per-lane row bases (row 32 wt + 4 h); row i of the accumulator adds the uniform
+    // (i & 3) + 8 (i >> 2).  Lanes that must not write start past every bound.  The empty
+    // asm keeps the 16 per-row offsets from being hoisted out of the chunk loop.
+    const int trb = wt * 32 + 4 * h;
+    uint32_t od0 = lvalid ? (uint32_t)(trb * L + l) * 4u : 0x80000000u;
+    uint32_t ob0 = (r == 0 && blk < nblk) ? (uint32_t)(trb * nblk + blk) * 8u : 0x80000000u;
+    uint32_t ol0 = lvalid ? (uint32_t)(trb * L + l) * 8u : 0x80000000u;
+    int gco = trb * 8;
+    asm volatile("" : "+v"(od0), "+v"(ob0), "+v"(gco));
+    if constexpr (LL) asm volatile("" : "+v"(ol0));
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int ri = (i & 3) + 8 * (i >> 2);
+      double q = (double)acc[kDig - 1][i];
+#pragma unroll
+      for (int d = kDig - 2; d >= 0; --d) q = fma(q, 256.0, (double)acc[d][i]);
+      const double gc = *reinterpret_cast<const double*>(cs + gco + ri * 8);
+      double v = q * kQInv + lc - gc;   // lc = -lamsum: (q/2^32 - lamsum) - gc as k_emission_i8
+      v = v == INFINITY ? -1e20 : v;      // masked latent (lc = +inf); padding latents: -inf
+      const double mx = (double)half_max32((float)v);
+      const float dv = (float)(v - mx);
+      const uint32_t od = od0 + (uint32_t)(ri * L) * 4u;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dv), rd, od, 0, 0);
+      if constexpr (LL) {
+        const unsigned long long vu = (unsigned long long)__double_as_longlong(v);
+        const uint32_t ol = ol0 + (uint32_t)(ri * L) * 8u;
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)vu, rl, ol, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(vu >> 32), rl, ol + 4, 0, 0);
+      }
+      const uint32_t ob = ob0 + (uint32_t)(ri * nblk) * 8u;
+      const unsigned long long mu = (unsigned long long)__double_as_longlong(mx);
+      __builtin_amdgcn_raw_buffer_store_b32((uint32_t)mu, rr, ob, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(mu >> 32), rr, ob + 4, 0, 0);
+    }
+    PMG_EM_STAMP(x, 3)
+  }
+#ifdef PMG_EM_STAMPS
+  __syncthreads();
+  if (stamps && (wid == 0 || wid == 7) && lane == 0)
+    for (int i = 0; i < 256; ++i) stamps[blockIdx.x * 512 + (wid == 7) * 256 + i] = sst[(wid == 7) * 256 + i];
+#endif
+#undef PMG_EM_STAMP
+}
+
+// ---------------------------------------------------------------------------------
+// Register-resident spikes (N <= 512): the traffic form.  Measured on k_emission_i8 and
+// k_emission_pipe at C3, the operand delivery from L2 caps at ~6.6 TB/s chip-wide, so
+// time follows the staged bytes per output: 21.9 B (128 x 64 tiles), 17.6 B (256 x 64).
+// Here each wave keeps its 32 time bins' spikes for the WHOLE neuron range in VGPRs as
+// MFMA A fragments (Kp / 8 registers, loaded once per time tile) and only the digit
+// planes stream: a workgroup of 8 waves = 256 time bins walks 32-latent tiles, every
+// 128-neuron chunk of the tile's 5 digit planes (20 KiB, full 128-B rows) arriving by
+// LDS-DMA into a 5-slot ring four chunks ahead and read by all 8 waves.  Staged bytes
+// per output: 5 Kp / 256 = 10 (+ spikes once per time tile) -> 563 MB at C3.
+// - Work items (time tile, 32-latent tile) in time-major order, a contiguous range per
+//   workgroup (one per CU, persistent): the spikes and gconst of a time tile are loaded
+//   once per range segment.
+// - LDS image: 8-row x 128-B pieces; row segment s sits at s ^ ((row >> 1) & 7) (DMA
+//   source and read), so the ds_read_b128 B-fragment reads of 16 rows hit 16 distinct
+//   bank quads.
+// - Per-latent constants (lconst) live in LDS for the whole launch; gconst rows in VGPRs.
+// Bit-identical to k_emission_i8 (same int32 digit sums, same f64 epilogue).
+constexpr int RT = 256, RLW = 32;                       // time bins, latents per work item
+constexpr int RLC_MAX = 4096;                            // latents of the LDS lconst table
+// chunk of CK neurons (128 or 256 B digit rows): ring slots and DMA pieces
+template <int CK> struct YRing {
+  static constexpr int NS = CK == 256 ? 3 : 5;           // 2 or 4 chunks in flight (120 / 100 KiB)
+  static constexpr int STAGE = kDig * RLW * CK;          // 40960 / 20480 B
+  static constexpr int PIECES = STAGE / 1024;            // 40 / 20 pieces (8 waves: 5 / 2-3 each)
+  static constexpr int RPP = 1024 / CK;                  // digit rows per piece
+  static constexpr int NSEG = CK / 16;                   // 16-B segments per row
+};
+
+// 32-lane (half-wave) max of f32 values as order-preserving int keys: v_max_i32 folds the
+// DPP moves (no canonicalising max(x, x) as the f32 form needs); the key map is an involution
+__device__ __forceinline__ int fkey(float f) {
+  const int b = __float_as_int(f);
+  return b ^ (int)((unsigned)(b >> 31) >> 1);
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_imax(int v) {
+  return max(v, __builtin_amdgcn_update_dpp((int)0x80000000, v, CTRL, 0xf, 0xf, false));
+}
+
+template <int CK, int KC, bool LL, bool MASK>
+__global__ void __launch_bounds__(512) k_emission_yreg(
+    const int8_t* __restrict__ yq, const int8_t* __restrict__ qd, const double* __restrict__ lconst,
+    const double* __restrict__ gconst, int64_t T, int64_t Tp, int L, int Lp, int nitem,
+    float* __restrict__ delta, double* __restrict__ rblk, double* __restrict__ ll64,
+    unsigned long long* __restrict__ stamps) {
+  constexpr int Kp = KC * CK;
+  constexpr int RNS = YRing<CK>::NS, RSTAGE = YRing<CK>::STAGE, RPIECES = YRing<CK>::PIECES;
+  constexpr int RPP = YRing<CK>::RPP, NSEG = YRing<CK>::NSEG;
+#ifdef PMG_EM_STAMPS
+  __shared__ __attribute__((aligned(16))) int8_t smem[RNS * RSTAGE + RLC_MAX * 8 + 4096];
+  unsigned long long* sst = reinterpret_cast<unsigned long long*>(smem + RNS * RSTAGE + RLC_MAX * 8);
+#define PMG_YR_STAMP(x, k)                                                                        \
+  if ((wid == 0 || wid == 4) && lane == 0 && (x) < 48) {                                         \
+    sst[(wid == 4) * 256 + (x) * 5 + (k)] = __builtin_amdgcn_s_memtime();                        \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                           \
+  }
+#else
+  __shared__ __attribute__((aligned(16))) int8_t smem[RNS * RSTAGE + RLC_MAX * 8];
+#define PMG_YR_STAMP(x, k)
+  (void)stamps;
+#endif
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int nLT = Lp / RLW;
+  const int i0 = (int)((int64_t)nitem * blockIdx.x / gridDim.x);
+  const int i1 = (int)((int64_t)nitem * (blockIdx.x + 1) / gridDim.x);
+  const int mine = i1 - i0;
+  if (mine <= 0) return;                                  // uniform per workgroup
+  const int S = mine * KC;
+
+  // per-latent constants for the launch (plain loads; no DMA is in flight yet)
+  double* slc = reinterpret_cast<double*>(smem + RNS * RSTAGE);
+  for (int l = tid; l < Lp; l += 512) slc[l] = lconst[l];
+  __syncthreads();
+
+  const int plane = Lp * Kp;
+  // DMA lane map: lane i fills row i / NSEG of an RPP-row piece, physical segment i % NSEG,
+  // i.e. logical segment (i % NSEG) ^ f(row) with f = (row >> 1) & 7 (128-B rows) or
+  // row & 15 (256-B rows); for row = RPP pr + i / NSEG both read f = (4 pr + (i >> 4)) % NSEG,
+  // so a lane needs one offset per pr % (NSEG / 4)
+  int vl[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    vl[q] = (lane / NSEG) * Kp + (((lane % NSEG) ^ ((4 * q + (lane >> 4)) & (NSEG - 1))) * 16);
+  // B fragment of k-step ks (logical segment 2 ks + h of row r): bb ^ (32 ks)
+  const int fr = CK == 256 ? (r & 15) : ((r >> 1) & 7);
+  const int bb = r * CK + ((h ^ fr) * 16);
+  const int npw = RPIECES / 8 + (wid < RPIECES % 8);     // pieces p = wid + 8 j < RPIECES
+
+#define PMG_YR_ISSUE(x_)                                                                           \
+  {                                                                                                \
+    const int xi = (x_) / KC, xc = (x_) - xi * KC;                                                 \
+    const int it = i0 + xi;                                                                        \
+    const int tt = it / nLT;                                                                       \
+    const int l0 = (it - tt * nLT) * RLW;                                                          \
+    int8_t* dst = smem + ((x_) % RNS) * RSTAGE;                                                    \
+    _Pragma("unroll") for (int j = 0; j < (RPIECES + 7) / 8; ++j) {                                \
+      const int p = wid + 8 * j;                                                                   \
+      if (p < RPIECES) {                                                                           \
+        const int d = p / (RLW / RPP), pr = p % (RLW / RPP);                                       \
+        const int o = d * plane + (l0 + RPP * pr) * Kp + xc * CK;                                  \
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                  \
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(qd + o), (short)0, kDig * plane - o, \
+                                              0x00020000),                                         \
+            (lds_void_t*)(dst + p * 1024), 16, vl[pr & (NSEG / 4 - 1)], 0, 0, 0);                  \
+      }                                                                                            \
+    }                                                                                              \
+  }
+  for (int x = 0; x < RNS - 1 && x < S; ++x) PMG_YR_ISSUE(x)
+
+  v4i ya[Kp / 32];                  // A fragments: y[t0 + 32 wid + r][32 ks + 16 h .. +16]
+  double gcr[16];                   // gconst of the lane's 16 output rows
+  v16i acc[kDig];
+  int cur_tt = -1;
+  constexpr int NST = LL ? 48 : 32;  // VMEM stores per epilogue (k_emission_pipe's count)
+  for (int xi = 0; xi < mine; ++xi) {
+    const int it = i0 + xi;
+    const int tt = it / nLT;
+    const int l0 = (it - tt * nLT) * RLW;
+    const int64_t t0 = (int64_t)tt * RT;
+    if (tt != cur_tt) {
+      // new time tile: this wave's 32 spike rows and its rows' gconst into registers, then
+      // a full vmcnt drain (the pending DMA pieces retire with it; hipcc's own waits then
+      // know the loads are done)
+      int64_t ty = t0 + 32 * wid + r;
+      ty = ty < Tp ? ty : Tp - 1;
+      const int8_t* yrow = yq + ty * Kp + 16 * h;
+#pragma unroll
+      for (int ks = 0; ks < Kp / 32; ++ks) ya[ks] = *reinterpret_cast<const v4i*>(yrow + 32 * ks);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        int64_t tg = t0 + 32 * wid + 4 * h + (i & 3) + 8 * (i >> 2);
+        tg = tg < T ? tg : T - 1;
+        gcr[i] = gconst[tg];
+      }
+      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+      cur_tt = tt;
+    }
+#pragma unroll
+    for (int d = 0; d < kDig; ++d) acc[d] = (v16i){0};
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      const int x = xi * KC + c;
+      PMG_YR_STAMP(x, 0)
+      {
+        // my DMA pieces of chunks x + 1 .. x + RNS - 2 and the stores of the epilogues at
+        // chunks x - RNS + 1 .. x - 1 (younger than piece x) may stay in flight
+        int n = 0;
+#pragma unroll
+        for (int j = 1; j <= RNS - 2; ++j) n += (x + j < S) ? npw : 0;
+#pragma unroll
+        for (int j = 1; j <= RNS - 1; ++j) n += (x - j >= 0 && ((x - j) % KC) == KC - 1) ? NST : 0;
+        vm_wait_upto(n < 63 ? n : 63);
+        PMG_YR_STAMP(x, 4)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      }
+      PMG_YR_STAMP(x, 1)
+      const int8_t* sq = smem + (x % RNS) * RSTAGE;
+#pragma unroll
+      for (int ks = 0; ks < CK / 32; ++ks) {
+        const int bo = bb ^ (32 * ks);
+#pragma unroll
+        for (int d = 0; d < kDig; ++d) {
+          const v4i b = *reinterpret_cast<const v4i*>(sq + d * RLW * CK + bo);
+          acc[d] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ya[(CK / 32) * c + ks], b, acc[d], 0, 0, 0);
+        }
+        if (ks == 0) {
+          // the next DMA behind the first k-step's MFMAs (their issue hides its SALU work)
+          __builtin_amdgcn_sched_barrier(0);
+          if (x + RNS - 1 < S) PMG_YR_ISSUE(x + RNS - 1)
+          PMG_YR_STAMP(x, 2)
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+
+    PMG_YR_STAMP(xi * KC + KC - 1, 3)
+    // epilogue (k_emission_i8's arithmetic)
+    const int nblk = Lp >> 5;
+    const int blk = l0 >> 5;
+    const int l = l0 + r;
+    const bool lvalid = l < L;
+    const double lc = slc[l];
+    const int64_t nrow64 = T - t0 < RT ? T - t0 : RT;
+    const int nrow = (int)nrow64;
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(delta + t0 * (int64_t)L, (short)0,
+                                                                         nrow * L * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(rblk + t0 * (int64_t)nblk, (short)0,
+                                                                         nrow * nblk * 8, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+        LL ? (void*)(ll64 + t0 * (int64_t)L) : (void*)delta, (short)0, LL ? nrow * L * 8 : 0, 0x00020000);
+    const int trb = 32 * wid + 4 * h;
+    uint32_t od0 = lvalid ? (uint32_t)(trb * L + l) * 4u : 0x80000000u;
+    uint32_t ob0 = r == 0 ? (uint32_t)(trb * nblk + blk) * 8u : 0x80000000u;
+    uint32_t ol0 = lvalid ? (uint32_t)(trb * L + l) * 8u : 0x80000000u;
+    asm volatile("" : "+v"(od0), "+v"(ob0));
+    if constexpr (LL) asm volatile("" : "+v"(ol0));
+    // Two halves of 8 rows: (1) ll in f64 and its f32 block-max key, (2) the 8 half-wave
+    // max reductions interleaved, (3) outputs.  Digit pairs combine exactly in int32 first
+    // (|a0 + 256 a1| <= 127 * 128 * 512 * 257 < 2^31 for Kp <= 512), so q is the same
+    // integer as k_emission_i8's Horner sum.
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      double vv[8];
+      int kk[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = 8 * hf + j;
+        const int lo = acc[0][i] + (acc[1][i] << 8);
+        const int mid = acc[2][i] + (acc[3][i] << 8);
+        const double q = fma(fma((double)acc[4][i], 65536.0, (double)mid), 65536.0, (double)lo);
+        double v = q * kQInv + lc - gcr[i];   // lc = -lamsum: (q/2^32 - lamsum) - gc as k_emission_i8
+        if constexpr (MASK) v = v == INFINITY ? -1e20 : v;   // masked latent (lc = +inf)
+        vv[j] = v;                                            // padding latents: lc = -inf
+        kk[j] = fkey((float)v);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) kk[j] = dpp_imax<0xB1>(kk[j]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) kk[j] = dpp_imax<0x4E>(kk[j]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) kk[j] = dpp_imax<0x141>(kk[j]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) kk[j] = dpp_imax<0x140>(kk[j]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const auto pr = __builtin_amdgcn_permlane16_swap(kk[j], kk[j], false, false);
+        kk[j] = max((int)pr[0], (int)pr[1]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = 8 * hf + j;
+        const int ri = (i & 3) + 8 * (i >> 2);
+        const double v = vv[j];
+        const double mx = (double)__int_as_float(fkey(__int_as_float(kk[j])));
+        const float dv = (float)(v - mx);
+        const uint32_t od = od0 + (uint32_t)(ri * L) * 4u;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dv), rd, od, 0, 0);
+        if constexpr (LL) {
+          const unsigned long long vu = (unsigned long long)__double_as_longlong(v);
+          const uint32_t ol = ol0 + (uint32_t)(ri * L) * 8u;
+          __builtin_amdgcn_raw_buffer_store_b32((uint32_t)vu, rl, ol, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(vu >> 32), rl, ol + 4, 0, 0);
+        }
+        const uint32_t ob = ob0 + (uint32_t)(ri * nblk) * 8u;
+        const unsigned long long mu = (unsigned long long)__double_as_longlong(mx);
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)mu, rr, ob, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(mu >> 32), rr, ob + 4, 0, 0);
+      }
+    }
+  }
+#ifdef PMG_EM_STAMPS
+  __syncthreads();
+  if (stamps && (wid == 0 || wid == 4) && lane == 0)
+    for (int i = 0; i < 256; ++i) stamps[blockIdx.x * 512 + (wid == 4) * 256 + i] = sst[(wid == 4) * 256 + i];
+#endif
+#undef PMG_YR_STAMP
+#undef PMG_YR_ISSUE
+}
+
 // Generic f64 emission: any y, weighted and/or 2-D neuron masks.
 // Block: 256 threads = tile of 16 time bins x 64 latents; thread (ty, tx) owns
 // latent l0+tx and time bins t0+4ty .. +3.
@@ -383,6 +934,7 @@ size_t pmg_emission_workspace_size(int64_t T, int32_t L, int32_t N) {
   c.take<int8_t>(kDig * Lp * Kp);
   c.take<double>(Lp);
   c.take<int>(4);
+  c.take<double>(Lp);
   return c.off + 256;
 }
 
@@ -411,11 +963,139 @@ int pmg_emission_poisson(const int8_t* yq, const double* gconst, const double* t
   int8_t* qd = c.take<int8_t>(kDig * (size_t)Lp * Kp);
   double* lamsum = c.take<double>(Lp);
   int* bad = c.take<int>(4);   // sticky range flag (zero-filled workspace; the caller clears it)
+  double* lconst = c.take<double>(Lp);
   hipLaunchKernelGGL(k_rates_prepare, dim3((Lp + 3) / 4), dim3(256), 0, st, tuning64, L, N,
-                     ma_neuron_1d, dt, Lp, Kp, qd, lamsum, bad);
+                     ma_neuron_1d, dt, Lp, Kp, qd, lamsum, bad, ma_latent, lconst);
   PMG_LAUNCH_CHECK();
-  const int nLT = (Lp + EL - 1) / EL;
   const int64_t Tp = round_up(T, 64);   // rows of yq (pmg_spikes_prepare zero-pads to Tp)
+  // pipelined kernel unless PMG_EMISSION_PIPE=0 (env: tests / A/B timing); its 32-bit
+  // offsets need the digit planes and a 256-row slab of y below 2^31 bytes
+  const char* pipe_s = getenv("PMG_EMISSION_PIPE");
+  // register-resident spikes for Kp <= 512 (PMG_EMISSION_PIPE=1 forces the 256 x 64 ring
+  // kernel, 0 the original k_emission_i8)
+  const bool yreg = !(pipe_s && (pipe_s[0] == '0' || pipe_s[0] == '1')) && Kp <= 512 && Lp <= RLC_MAX &&
+                    (int64_t)kDig * Lp * Kp < (1ll << 31) && T < (1ll << 38);
+  if (yreg) {
+    const int nLT32 = Lp / RLW;
+    const int64_t nitem64 = (T + RT - 1) / RT * nLT32;
+    PMG_REQUIRE(nitem64 < (1ll << 30), "pmg_emission_poisson: too many tiles (%lld)", (long long)nitem64);
+    const int nitem = (int)nitem64;
+    int nwg = device_cu_count();
+    if (nwg > nitem) nwg = nitem;
+    unsigned long long* ystamps = nullptr;
+#ifdef PMG_EM_STAMPS
+    static unsigned long long* ybuf = nullptr;
+    if (!ybuf) PMG_HIP(hipMalloc(&ybuf, (size_t)1024 * 512 * 8));
+    PMG_HIP(hipMemsetAsync(ybuf, 0, (size_t)nwg * 512 * 8, st));
+    ystamps = ybuf;
+#endif
+#define PMG_YR_LAUNCH(CK, KC)                                                                               \
+  {                                                                                                         \
+    auto kern = ll64 ? (ma_latent ? k_emission_yreg<CK, KC, true, true> : k_emission_yreg<CK, KC, true, false>) \
+                     : (ma_latent ? k_emission_yreg<CK, KC, false, true> : k_emission_yreg<CK, KC, false, false>); \
+    hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(512), 0, st, yq, qd, lconst, gconst, T, Tp, L, Lp, nitem, \
+                       delta, rblk, ll64, ystamps);                                                        \
+  }
+    // 256-neuron chunks where they divide Kp (fewer barriers per MFMA), else 128
+    switch (Kp) {
+      case 128: PMG_YR_LAUNCH(128, 1); break;
+      case 256: PMG_YR_LAUNCH(256, 1); break;
+      case 384: PMG_YR_LAUNCH(128, 3); break;
+      default: PMG_YR_LAUNCH(256, 2); break;
+    }
+#undef PMG_YR_LAUNCH
+    PMG_LAUNCH_CHECK();
+#ifdef PMG_EM_STAMPS
+    {
+      // chunk x: [0] top, [1] after wait + barrier, [2] after DMA issue; [3] of an item's
+      // last chunk: MFMAs issued (epilogue starts); next chunk's [0] closes the period
+      std::vector<unsigned long long> hh((size_t)nwg * 512);
+      PMG_HIP(hipStreamSynchronize(st));
+      PMG_HIP(hipMemcpy(hh.data(), ybuf, hh.size() * 8, hipMemcpyDeviceToHost));
+      const int KCh = Kp == 384 ? 3 : (Kp == 512 ? 2 : 1);
+      for (int w = 0; w < 2; ++w) {
+        double vw = 0, wb = 0, is = 0, cp = 0, ep = 0, per = 0, pere = 0;
+        int n = 0, ne = 0;
+        for (int b = 0; b < nwg; ++b)
+          for (int x = 1; x < 47; ++x) {
+            const unsigned long long* q = &hh[(size_t)b * 512 + w * 256 + x * 5];
+            if (!q[0] || !q[5]) continue;
+            vw += q[4] - q[0];
+            wb += q[1] - q[4];
+            is += q[2] - q[1];
+            if ((x % KCh) == KCh - 1 && q[3]) {
+              cp += q[3] - q[2];
+              ep += q[5] - q[3];
+              pere += q[5] - q[0];
+              ++ne;
+            } else {
+              per += q[5] - q[0];
+              ++n;
+            }
+          }
+        fprintf(stderr, "[yr-stamps] wave %d: vmwait %.0f barrier %.0f issue %.0f | inner period %.0f (n=%d) | last chunk: mfma %.0f epilogue %.0f period %.0f (n=%d)\n",
+                w ? 4 : 0, vw / (n + ne), wb / (n + ne), is / (n + ne), n ? per / n : 0.0, n, ne ? cp / ne : 0.0,
+                ne ? ep / ne : 0.0, ne ? pere / ne : 0.0, ne);
+      }
+    }
+#endif
+    return PMG_OK;
+  }
+  const bool pipe = !(pipe_s && pipe_s[0] == '0') && (int64_t)kDig * Lp * Kp < (1ll << 31) &&
+                    (int64_t)PT * Kp < (1ll << 31) && T < (1ll << 38);
+  if (pipe) {
+    const int nLTp = (Lp + PL - 1) / PL;
+    const int64_t ntile64 = (T + PT - 1) / PT * nLTp;
+    PMG_REQUIRE(ntile64 < (1ll << 30), "pmg_emission_poisson: too many tiles (%lld)", (long long)ntile64);
+    const int ntile = (int)ntile64;
+    int nwg = device_cu_count() & ~7;
+    if (nwg < 8) nwg = 8;
+    auto kern = ll64 ? k_emission_pipe<true> : k_emission_pipe<false>;
+    unsigned long long* stamps = nullptr;
+#ifdef PMG_EM_STAMPS
+    static unsigned long long* dst_stamps = nullptr;
+    if (!dst_stamps) PMG_HIP(hipMalloc(&dst_stamps, (size_t)nwg * 512 * 8));
+    PMG_HIP(hipMemsetAsync(dst_stamps, 0, (size_t)nwg * 512 * 8, st));
+    stamps = dst_stamps;
+#endif
+    hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(1024), 0, st, yq, qd, lconst, gconst, T, Tp, L, Lp, Kp,
+                       nLTp, ntile, delta, rblk, ll64, stamps);
+    PMG_LAUNCH_CHECK();
+#ifdef PMG_EM_STAMPS
+    {
+      std::vector<unsigned long long> h((size_t)nwg * 512);
+      PMG_HIP(hipStreamSynchronize(st));
+      PMG_HIP(hipMemcpy(h.data(), dst_stamps, h.size() * 8, hipMemcpyDeviceToHost));
+      const int nchh = Kp / PK;
+      for (int w = 0; w < 2; ++w) {
+        double wb[2] = {0, 0}, is[2] = {0, 0}, cm[2] = {0, 0}, per[2] = {0, 0};
+        int cnt[2] = {0, 0};
+        for (int b = 0; b < nwg; ++b)
+          for (int x = 1; x < 63; ++x) {
+            const unsigned long long* q = &h[(size_t)b * 512 + w * 256 + x * 4];
+            if (!q[0] || !q[3] || !q[4]) continue;
+            const int e = (x % nchh) == nchh - 1;
+            wb[e] += q[1] - q[0];
+            is[e] += q[2] - q[1];
+            cm[e] += q[3] - q[2];
+            per[e] += q[4] - q[0];
+            ++cnt[e];
+          }
+        for (int e = 0; e < 2; ++e)
+          if (cnt[e])
+            fprintf(stderr, "[em-stamps] wave %d %s chunks: n=%d wait+barrier %.0f issue %.0f compute%s %.0f period %.0f (s_memtime ticks)\n",
+                    w ? 7 : 0, e ? "tile-last" : "inner", cnt[e], wb[e] / cnt[e], is[e] / cnt[e], e ? "+epilogue" : "",
+                    cm[e] / cnt[e], per[e] / cnt[e]);
+      }
+      const unsigned long long* q0 = &h[0];
+      fprintf(stderr, "[em-stamps] wg0 wave0 first stamps:");
+      for (int x = 0; x < 12; ++x) fprintf(stderr, " %lld", (long long)(q0[x * 4] - q0[0]));
+      fprintf(stderr, "\n");
+    }
+#endif
+    return PMG_OK;
+  }
+  const int nLT = (Lp + EL - 1) / EL;
   // one time fragment per wave: two workgroups share a CU (one's epilogue beside the
   // other's MFMAs).  MT = 2 (PMG_EMISSION_MT=2, env: tests / A/B timing) halves the
   // digit-plane traffic but holds the CU alone: C3 emission 0.223 -> 0.284 ms, so it is

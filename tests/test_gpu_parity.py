@@ -545,22 +545,36 @@ def test_emission_range_flag_raises():
     eng.emission_status()                       # cleared by the previous check
 
 
-@pytest.mark.parametrize("L,T", [(512, 3000), (100, 1000), (256, 700)])
-def test_emission_time_tile_invariant(L, T, monkeypatch):
-    """The int8-MFMA emission with one or two 32-step time fragments per wave (128- or
-    256-step workgroup tiles, PMG_EMISSION_MT) is the same exact integer contraction:
-    delta, block references and the f64 ll bit-identical, ragged T and L included."""
+@pytest.mark.parametrize("L,T,N", [(512, 3000, 64), (100, 1000, 64), (256, 700, 64), (96, 1300, 300),
+                                   (512, 9000, 512)])
+@pytest.mark.parametrize("with_ll,masked", [(True, False), (False, False), (False, True)])
+def test_emission_time_tile_invariant(L, T, N, with_ll, masked, monkeypatch):
+    """The int8-MFMA emission kernels -- k_emission_i8 with one or two 32-step time
+    fragments per wave (128- or 256-step tiles, PMG_EMISSION_MT), the pipelined
+    k_emission_pipe (256 x 64 tiles, LDS-DMA ring; PMG_EMISSION_PIPE=1) and the default
+    k_emission_yreg (spikes in VGPRs, digit planes through an LDS-DMA ring) -- are the same exact
+    integer contraction: delta, block references and the f64 ll bit-identical, ragged T,
+    L and N, latent masks and the EM form without ll included."""
     import torch
     from poor_man_gplvm_amd.engine import DeviceEM, SpikeData
-    d = make(37, L, T)
+    d = make(N, L, T)
+    ml = None
+    if masked:
+        ml = (np.random.default_rng(5).random(L) > 0.3).astype(np.uint8)
+        ml[:40] = 0                                   # a fully masked 32-block as well
     out = {}
-    for mt in ("1", "2"):
+    for pipe, mt in (("0", "1"), ("0", "2"), ("1", "1"), ("auto", "1")):
         monkeypatch.setenv("PMG_EMISSION_MT", mt)
+        monkeypatch.setenv("PMG_EMISSION_PIPE", pipe)
         eng = DeviceEM(SpikeData(d['y']), L)
-        eng.ll64 = torch.empty((T, L), dtype=torch.float64, device='cuda')
+        eng.set_ma_latent(ml)
+        if with_ll:
+            eng.ll64 = torch.empty((T, L), dtype=torch.float64, device='cuda')
         eng.set_tuning(d['tuning'])
         eng.emission(1.0)
         eng.emission_status()
-        out[mt] = [x.cpu().numpy() for x in (eng.delta, eng.rblk, eng.ll64)]
-    for a, b in zip(out["1"], out["2"]):
-        np.testing.assert_array_equal(a, b)
+        out[pipe + mt] = [x.cpu().numpy() for x in ((eng.delta, eng.rblk, eng.ll64) if with_ll
+                                                    else (eng.delta, eng.rblk))]
+    for key in ("02", "11", "auto1"):
+        for a, b in zip(out["01"], out[key]):
+            np.testing.assert_array_equal(a, b)
