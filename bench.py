@@ -197,7 +197,8 @@ def compute_rooflines(summ, T, L, N, NB, adam_iters, pmc):
         "forward_filter": ("k_forward", "hbm", 12.0 * T * L + 4.0 * T * nblk + 16.0 * T, 1e9, PEAK_HBM_GBS, "GB/s"),
         "backward_smoother": ("k_backward", "hbm", 16.0 * T * L + 4.0 * T * nblk, 1e9, PEAK_HBM_GBS, "GB/s"),
         "suffstats": ("k_ptb3", "mfma", 2.0 * T * L * N, 1e12, PEAK_BF16_MFMA_TFLOPS, "TFLOP/s"),
-        "emission": ("k_emission_i8", "mfma", 2.0 * T * L * N, 1e12, PEAK_I8_MFMA_TOPS, "TOP/s"),
+        "emission": ("k_emission_yreg" if N <= 512 else "k_emission_pipe", "mfma", 2.0 * T * L * N, 1e12,
+                     PEAK_I8_MFMA_TOPS, "TOP/s"),
     }
     rooflines = {}
     for sec, (kname, bound, units_per_launch, scale, peak, unit) in units.items():

@@ -7,7 +7,7 @@ mkdir -p $R/gpurun_out
 export TMPDIR=/tmp
 run() {  # name, counters...
   local name=$1; shift
-  timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex "k_ptb3|k_emission_i8|k_adam<|k_forward<|k_backward<|k_verify|k_forward_relax|k_backward_relax" --output-format csv -d $R/gpurun_out/${TAG}_$name -o run \
+  timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex "k_ptb3|k_emission_i8|k_emission_yreg|k_emission_pipe|k_adam<|k_forward<|k_backward<|k_verify|k_forward_relax|k_backward_relax" --output-format csv -d $R/gpurun_out/${TAG}_$name -o run \
     -- python3 $R/bench.py --config $CFG --steps 3 --warmup 3 --no-cpu-baseline --no-api-fit > $R/gpurun_out/${TAG}_$name.log 2>&1
   local rc=$?; echo "pmc $name rc=$rc"; return $rc
 }

@@ -14,7 +14,8 @@ import sys
 from collections import defaultdict
 
 KEYS = {"k_forward<": "k_forward", "k_backward<": "k_backward", "k_ptb3": "k_ptb3",
-        "k_emission_i8": "k_emission_i8", "k_adam<": "k_adam", "k_verify": "k_verify",
+        "k_emission_i8": "k_emission_i8", "k_emission_yreg": "k_emission_yreg",
+        "k_emission_pipe": "k_emission_pipe", "k_adam<": "k_adam", "k_verify": "k_verify",
         "k_forward_relax<": "k_forward_relax", "k_backward_relax<": "k_backward_relax"}
 
 
