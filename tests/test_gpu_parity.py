@@ -546,13 +546,14 @@ def test_emission_range_flag_raises():
 
 
 @pytest.mark.parametrize("L,T,N", [(512, 3000, 64), (100, 1000, 64), (256, 700, 64), (96, 1300, 300),
-                                   (512, 9000, 512)])
+                                   (512, 9000, 512), (160, 1500, 700)])
 @pytest.mark.parametrize("with_ll,masked", [(True, False), (False, False), (False, True)])
 def test_emission_time_tile_invariant(L, T, N, with_ll, masked, monkeypatch):
     """The int8-MFMA emission kernels -- k_emission_i8 with one or two 32-step time
     fragments per wave (128- or 256-step tiles, PMG_EMISSION_MT), the pipelined
     k_emission_pipe (256 x 64 tiles, LDS-DMA ring; PMG_EMISSION_PIPE=1) and the default
-    k_emission_yreg (spikes in VGPRs, digit planes through an LDS-DMA ring) -- are the same exact
+    k_emission_yreg (spikes in VGPRs, digit planes through an LDS-DMA ring; N > 512: the ring
+    kernel is the default) -- are the same exact
     integer contraction: delta, block references and the f64 ll bit-identical, ragged T,
     L and N, latent masks and the EM form without ll included."""
     import torch
