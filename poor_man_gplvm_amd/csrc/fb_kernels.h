@@ -376,7 +376,7 @@ __device__ __forceinline__ float hilbert_dist(const float* __restrict__ x, const
   for (int q = 0; q < 4 * kQ; ++q) {
     const float a = xv[q] * ix, b = yv[q] * iy;
     if (a > lo_thr && b > lo_thr) {
-      const float r = __logf(a) - __logf(b);
+      const float r = __logf(a * __builtin_amdgcn_rcpf(b));  // log of the ratio: see hilbert_reg
       lo = fminf(lo, r);
       hi = fmaxf(hi, r);
     } else if (fmaxf(a, b) > hi_thr) {
@@ -421,7 +421,10 @@ __device__ __forceinline__ float hilbert_reg(const float x0[J], const float x1[J
   for (int j = 0; j < 2 * J; ++j) {
     const float u = a[j] * ix, v = b[j] * iy;
     if (u > lo_thr && v > lo_thr) {
-      const float r = __logf(u) - __logf(v);
+      // log of the ratio, not a difference of logs: for components near 1e-20 the log is
+      // ~46, whose f32 ulp (3.8e-6) exceeds the tolerance, so two states 1 ulp apart
+      // (the unnormalised scans store q * iS) would never read as converged
+      const float r = __logf(u * __builtin_amdgcn_rcpf(v));
       lo = fminf(lo, r);
       hi = fmaxf(hi, r);
     } else if (fmaxf(u, v) > hi_thr) {
