@@ -57,8 +57,11 @@ class ScanConfig:
                                  # In slowly mixing regimes (the flat tuning of the first EM
                                  # iterations) two f32 chains of one filter settle 1.4e-6
                                  # (median) to 7.6e-6 (q99) apart and never coalesce bitwise
-                                 # (profiles/r02_diag_cascade_c3.log); boundaries that fail on
-                                 # that noise alone cost a short relaxation, not a rescan of T
+                                 # (profiles/r02_diag_cascade_c3.log, measured with a difference
+                                 # of f32 logs, which overstates distances between tiny
+                                 # components; the kernels now take the log of the ratio);
+                                 # boundaries that fail on that noise alone cost a short
+                                 # relaxation, not a rescan of T
     adaptive: bool = False       # per pass: double the warm-up when >1% of chunks needed
                                  # repair, halve it after two E-steps with <=0.1%.  Off by
                                  # default: the relaxation kernel absorbs the cascades of the
