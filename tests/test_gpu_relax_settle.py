@@ -1,0 +1,49 @@
+"""Relaxations settle once the chain has forgotten a bad start (fb_kernels.h hilbert_reg /
+hilbert_dist).  Regression for the boundary metric: a difference of f32 logs cannot
+resolve the 3e-6 tolerance on components near 1e-20 (their log's ulp is 3.8e-6), so a
+recomputed chunk whose end state matches the stored one to rounding read as unconverged
+and every repair ran to the end of its segment (C5: 0.90 ms of forward repair per
+iteration instead of 0.12).  At C3, iteration 3 of a fresh fit repairs 3 + 1 chunks in
+one round with the log-of-ratio metric (profiles/r03u_c3_first_iterations.jsonl)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+@pytest.mark.gpu
+def test_c3_third_iteration_repairs_settle():
+    import torch
+    import bench
+    from poor_man_gplvm_amd.engine import SpikeData, DeviceEM, AdamConfig, ScanConfig
+    from poor_man_gplvm_amd.gp_kernel import banded_transition
+    N, T, L = bench.CONFIGS["c3"]
+    y, B, W0, lp0 = bench.synth(N, T, L, rank=0)
+    dev = torch.device("cuda", 0)
+    eng = DeviceEM(SpikeData(y), L, basis=B, scan=ScanConfig(warmup=48))
+    eng.adaptive = True
+    eng.set_transition(banded_transition(L, 1.0, 0.01, 0.01))
+    eng.set_log_posterior(lp0)
+    eng.reset_adaptive()
+    adam = AdamConfig(lr=0.01, maxiter=1000, tol=1e-6, prior_std=1.0)
+    W = torch.as_tensor(W0.astype(np.float64), device=dev).contiguous()
+    mu, nu = torch.zeros_like(W), torch.zeros_like(W)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    stats = torch.zeros(4, dtype=torch.float64, device=dev)
+    lh = torch.zeros(adam.maxiter, dtype=torch.float64, device=dev)
+    eh = torch.zeros_like(lh)
+    logz = torch.zeros(1, dtype=torch.float64, device=dev)
+    reps = []
+    for _ in range(3):
+        eng.m_step(W, mu, nu, cnt, adam, stats, lh, eh)
+        eng.compute_tuning(W)
+        eng.e_step(1.0, logz)
+        reps.append((eng.repairs(), eng.relax_rounds()))
+    (f1, b1), _ = reps[0]
+    assert f1 > 1000 and b1 > 1000, reps   # iteration 1: the unmixed chain fails everywhere
+    (f3, b3), (rf3, rb3) = reps[2]
+    assert f3 + b3 <= 64 and rf3 <= 2 and rb3 <= 2, reps
