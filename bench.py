@@ -355,6 +355,8 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-api-fit", action="store_true", help="skip the public-API fit_em(n_iter=20) timing")
+    ap.add_argument("--decode", action="store_true",
+                    help="also time decode_latent at this config (exact dense and banded paths)")
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--chunk-bwd", type=int, default=0, help="backward chunk (0: ScanConfig default, 2x forward)")
     ap.add_argument("--warm-steps", type=int, default=48)
@@ -525,6 +527,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_api_fit:
         out["fit_em_api"] = api_fit_wall(y, B, W0, lp0, L)
+    if rank == 0 and world == 1 and args.decode:
+        out["decode_latent"] = decode_leg(y, eng.tuning64.cpu().numpy(), L)
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(N, T, L, adam_iters)
     if rank == 0:
@@ -733,6 +737,52 @@ def launcher_selftest(args):
                           "ranks_max_s": float(te[0])}), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def decode_leg(y, tuning, L, reps=2):
+    """decode_latent (core.py:454-497) at the bench shape with the fitted tuning: wall time
+    of the public call (spikes uploaded, smoother, pairwise joint, every returned array
+    copied to numpy; the first call loads code objects and is not counted), then the
+    device sections of one decode under HIP events.  Default exact path (dense
+    log-domain scans, f64 log-domain joint) and the banded path (decode_exact=False)."""
+    import torch
+    from poor_man_gplvm_amd import PoissonGPLVMJump1D, ScanConfig
+    from poor_man_gplvm_amd.engine import KernelTimer
+    out = {}
+    for name, exact in (("exact", True), ("banded", False)):
+        m = PoissonGPLVMJump1D(y.shape[1], n_latent_bin=L, tuning_lengthscale=10.0, movement_variance=1.0,
+                               scan_config=ScanConfig(decode_exact=exact))
+        m.decode_latent(y, tuning=tuning)
+        walls = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            r = m.decode_latent(y, tuning=tuning)
+            walls.append(time.perf_counter() - t0)
+        eng = m._decode_engine(y, tuning, {}, None, None)
+        eng.timer = KernelTimer()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        m._decode_on(eng, {}, None, 1.0)
+        torch.cuda.synchronize()
+        dev_wall = time.perf_counter() - t0
+        summ = eng.timer.summary()
+        eng.timer = None
+        sec = {k: round(v[0] * v[1], 3) for k, v in summ.items()}
+        out[name] = {"wall_s": min(walls), "smoother_joint_call_s": dev_wall,
+                     "device_ms": round(sum(sec.values()), 3), "sections_ms": sec,
+                     "log_marginal_final": float(r["log_marginal_final"])}
+        del m, eng, r
+        torch.cuda.empty_cache()
+    T = y.shape[0]
+    jl = out["exact"]["sections_ms"].get("joint_log", 0.0)
+    if jl > 0:
+        terms = 4.0 * L * L * (T - 1)
+        out["exact"]["joint_log_terms_per_s"] = terms / (jl * 1e-3)
+    out["note"] = ("wall_s: public decode_latent, best of %d after one untimed call (upload of y, prepare, "
+                   "scans, joint, host copies); sections_ms: HIP events of the smoother + joint of one decode; "
+                   "joint_log_terms_per_s: 4 L^2 (T-1) log-domain terms / k_joint_log time" % reps)
+    return out
 
 
 def api_fit_wall(y, B, W0, lp0, L, n_iter=20):

@@ -402,6 +402,14 @@ int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const floa
                    const double* yw, const double* tw, int32_t L, int32_t NB, int32_t N,
                    const pmg_adam_cfg* cfg, double* stats, double* loss_hist, double* err_hist,
                    void* workspace, size_t workspace_bytes, void* stream);
+/* Workgroups of the persistent launch wait on one another (the lagged stop      */
+/* decision, the row-block B^T G exchange) in waits bounded by 2 s of the real-    */
+/* time clock.  A wait that gives up sets the sticky int32 word 0 of the workspace */
+/* and the launch's W / mu / nu / stats are then invalid.  No launch clears it:    */
+/* allocate the workspace zeroed and read it with pmg_mstep_adam_status, which      */
+/* syncs the stream, sets *timed_out (0/1) and clears the word (also the batched    */
+/* call's workspace: every restart shares word 0).                                 */
+int pmg_mstep_adam_status(void* workspace, int32_t* timed_out, void* stream);
 /* R restarts' M-steps (batched restarts): W, mu, nu (R,NB,N),  */
 /* count (R), yw (R*L, N) and tw (R*L) (the stacked suff-stats), stats (R,4), */
 /* loss_hist / err_hist (R, max(maxiter,1)).  Each restart runs its own loop */

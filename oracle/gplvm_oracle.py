@@ -403,9 +403,19 @@ def adam_run(W, state, param_prior_std, basis, yw, tw, lr=0.01, maxiter=1000, to
             'final_error': err, 'loss_history': lh, 'error_history': eh}
 
 
-def m_step(W, y, log_posterior_curr, basis, param_prior_std, opt_state, lr=0.01, maxiter=1000, tol=1e-6):
-    """core.py:802-827: suff-stats -> Adam -> trimmed histories."""
+def m_step(W, y, log_posterior_curr, basis, param_prior_std, opt_state, lr=0.01, maxiter=1000, tol=1e-6,
+           stats_perturb=None):
+    """core.py:802-827: suff-stats -> Adam -> trimmed histories.
+
+    stats_perturb = (rng, eps) multiplies y_w and t_w by (1 + eps * N(0, 1)) elementwise
+    before the Adam loop.  Not part of the reference: the golden generator uses it to run
+    an ensemble of f64 fits whose statistics differ at the level of summation-order
+    rounding (eps = 1e-15), which measures how far rounding alone moves a long M-step."""
     yw, tw = get_statistics(log_posterior_curr, y)
+    if stats_perturb is not None:
+        rng, eps = stats_perturb
+        yw = yw * (1.0 + eps * rng.standard_normal(yw.shape))
+        tw = tw * (1.0 + eps * rng.standard_normal(tw.shape))
     res = adam_run(W, opt_state, param_prior_std, basis, yw, tw, lr, maxiter, tol)
     n = res['n_iter']
     return {'params': res['params'], 'opt_state': res['opt_state'], 'n_iter': n,
@@ -419,9 +429,11 @@ def m_step(W, y, log_posterior_curr, basis, param_prior_std, opt_state, lr=0.01,
 def fit_em(y, params, basis, log_posterior_init, n_iter=20, movement_variance=1.0,
            p_move_to_jump=0.01, p_jump_to_move=0.01, param_prior_std=1.0, ma_neuron=None,
            ma_latent=None, n_time_per_chunk=10000, likelihood_scale=1.0, save_every=None,
-           m_step_step_size=0.01, m_step_maxiter=1000, m_step_tol=1e-6, custom_kernel=None):
+           m_step_step_size=0.01, m_step_maxiter=1000, m_step_tol=1e-6, custom_kernel=None,
+           stats_perturb=None):
     """core.py:829-849 + core.py:592-713 with injected params / basis /
-    log_posterior_init (JAX PRNG is not reproducible without JAX)."""
+    log_posterior_init (JAX PRNG is not reproducible without JAX).  stats_perturb: see
+    m_step (ensemble runs of the golden generator only)."""
     y = np.asarray(y, _F)
     L = basis.shape[0]
     if save_every is None:
@@ -437,7 +449,7 @@ def fit_em(y, params, basis, log_posterior_init, n_iter=20, movement_variance=1.
     m_step_res_l = {}
     for i in range(n_iter):
         m_res = m_step(W, y, logpost, basis, param_prior_std, opt_state, m_step_step_size,
-                       m_step_maxiter, m_step_tol)
+                       m_step_maxiter, m_step_tol, stats_perturb)
         if i == 0:
             m_step_res_l = {k: [] for k in m_res.keys()}                   # core.py:655
         for k in m_res:

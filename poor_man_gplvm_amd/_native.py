@@ -59,7 +59,7 @@ EXPORTED_SYMBOLS = (
     "pmg_tuning_softplus_batched", "pmg_emission_rowref_batched", "pmg_fwdbwd_batched_workspace_size",
     "pmg_forward_filter_batched", "pmg_backward_smoother_batched",
     "pmg_mstep_batched_workspace_size", "pmg_mstep_adam_batched_supported", "pmg_mstep_adam_batched",
-    "pmg_emission_range_flag",
+    "pmg_emission_range_flag", "pmg_mstep_adam_status",
 )
 
 
@@ -132,6 +132,7 @@ _SIGS = {
     "pmg_mstep_adam_supported": ([_I32, _I32, _I32], ctypes.c_int),
     "pmg_mstep_adam": ([_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, ctypes.POINTER(AdamCfg),
                         _P, _P, _P, _P, _SZ, _P], _I32),
+    "pmg_mstep_adam_status": ([_P, ctypes.POINTER(_I32), _P], _I32),
     "pmg_mstep_tiled_workspace_size": ([_I32, _I32, _I32], _SZ),
     "pmg_mstep_adam_tiled": ([_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, ctypes.POINTER(AdamCfg),
                               _P, _P, _P, _P, _SZ, _P], _I32),

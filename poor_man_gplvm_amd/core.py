@@ -745,6 +745,7 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
         res['m_step_res_l'] = {'params': [], 'opt_state': []}      # core.py:655-658 with m_step core.py:898-904
     else:
         eng.emission_status()
+        eng.adam_status()
     info = {'opt_state': {'mu': _np(mu), 'nu': _np(nu), 'count': int(_np(cnt)[0])},
             'params64': _np(W), 'repairs': eng.repairs(), 'chunk': eng.C}
     return res, info
@@ -813,6 +814,7 @@ def run_em_restarts(y, params, basis, log_posterior_inits, n_iter, transition, m
     st, lhn, ehn = _np(stats), _np(lh), _np(eh)
     repairs = eng.repairs()
     eng.emission_status()
+    eng.ws_ad.status()
     out = []
     for r in range(R):
         posterior = _np(gamma[r])

@@ -41,6 +41,7 @@ constexpr int kThreads = 512;           // L <= 512
 constexpr int kPartPerLane = 4;         // G <= 256 workgroups -> 4 partials per lane
 constexpr int kBiasLds = 1024;          // bias corrections held in LDS (bodies)
 constexpr int kXSlots = 512;            // exchange slots per workgroup (NB S <= 512 elements)
+constexpr uint64_t kAdamSpinTicks = 200000000ull;   // 2 s of the 100 MHz real-time clock
 
 struct AdamParams {
   double* W;
@@ -59,7 +60,10 @@ struct AdamParams {
   const double* bias;         // [2][maxiter] 1/(1 - b1^(count0+k+1)), 1/(1 - b2^(count0+k+1))
   unsigned long long* lpart;  // [maxiter + kLag + 2][G] f64 bits, pre-filled with kSentinel
   unsigned long long* gpart;  // [..][G]
-  int* timeout;
+  int* timeout;               // sticky: word 0 of the workspace, shared by all restarts,
+                              // set by a bounded wait that gave up; read and cleared only
+                              // by pmg_mstep_adam_status (never by a launch)
+  uint64_t spin;              // bound of those waits (real-time clock ticks, spin_ticks)
   // row blocks (L > 512): workgroup g = rb Gg + gg owns rows [rb 32 A, (rb + 1) 32 A) of
   // neuron group gg; the RB row blocks of a group swap their B^T G partials every body
   int RB, Gg;
@@ -93,7 +97,6 @@ __device__ __forceinline__ AdamParams adam_view(const AdamParams& p0) {
   p.bias = reinterpret_cast<const double*>(reinterpret_cast<const char*>(p.bias) + o);
   p.lpart = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(p.lpart) + o);
   p.gpart = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(p.gpart) + o);
-  p.timeout = reinterpret_cast<int*>(reinterpret_cast<char*>(p.timeout) + o);
   p.prof = nullptr;
   return p;
 }
@@ -137,7 +140,7 @@ __global__ void k_fill_u64(unsigned long long* __restrict__ x, size_t n, unsigne
 }
 
 // Launch prologue: sentinel-fill both partial arrays, zero the outputs the loop fills
-// sparsely (histories, stats, the timeout word: no host memsets), and tabulate the bias
+// sparsely (histories, stats: no host memsets), and tabulate the bias
 // corrections of every body from the Adam step count, c_k = 1 / (1 - b^(count0 + k + 1)).
 // A closed form per body (not a running product) gives the same bits however the loop
 // is split into launches (the speculative batches of the neuron-sharded M-step).
@@ -152,7 +155,6 @@ __global__ void k_adam_prologue(AdamParams p_arg, size_t n) {
   double* __restrict__ loss_hist = p.loss_hist;
   double* __restrict__ err_hist = p.err_hist;
   double* __restrict__ stats = p.stats;
-  int* __restrict__ timeout = p.timeout;
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t q = i; q < n; q += stride) {
@@ -167,7 +169,6 @@ __global__ void k_adam_prologue(AdamParams p_arg, size_t n) {
     err_hist[k] = 0.0;
   }
   if (i < 4) stats[i] = 0.0;
-  if (i == 0) timeout[0] = 0;
   if (p.xflag)
     for (size_t q = i; q < (size_t)p.G * 8; q += stride) p.xflag[q] = 0;
 }
@@ -545,11 +546,11 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
       for (int rr = 0; rr < p.RB; ++rr) {
         const int gp = rr * p.Gg + gg;
         if (rr != rb) {
-          unsigned spins = 0;
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
           while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&p.xflag[gp * kNW + wid], __ATOMIC_RELAXED,
                                                                   __HIP_MEMORY_SCOPE_AGENT)) < k + 1) {
             __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1u << 24)) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > p.spin) {
               if (lane == 0) {
                 atomicOr(p.timeout, 1);
                 sCtl[2] = 1;
@@ -624,7 +625,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
         ok = __all(ok);
         if (p.prof && g == 0 && lane == 0 && k < 64 && rep == 0) p.prof[k * 16 + 8] = __builtin_amdgcn_s_memtime();
         if (!ok && must) {  // blocking re-poll of body dj
-          unsigned spins = 0;
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
           while (!ok) {
             __builtin_amdgcn_s_sleep(1);
             load_parts(p, dj, lane, lv0);
@@ -633,7 +634,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
             for (int q = 0; q < kPartPerLane; ++q) ok &= (lv0[q] != kSentinel);
             ok = __all(ok);
             if (p.prof && g == 0 && lane == 0 && k < 64) p.prof[k * 16 + 7] += 1;
-            if (++spins > (1u << 24)) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > p.spin) {
               if (lane == 0) {
                 atomicOr(p.timeout, 1);
                 sCtl[2] = 1;
@@ -946,6 +947,7 @@ static int adam_run(double* W, double* mu, double* nu, int64_t* count, const flo
   p.lpart = w.lpart;
   p.gpart = w.gpart;
   p.timeout = w.timeout;
+  p.spin = spin_ticks(kAdamSpinTicks);
   p.bias = w.bias;
   p.rs_W = (int64_t)NB * N;
   p.rs_yw = (int64_t)L * N;
@@ -982,7 +984,6 @@ static int adam_run(double* W, double* mu, double* nu, int64_t* count, const flo
     q.bias = reinterpret_cast<const double*>(reinterpret_cast<char*>(w.bias) + o);
     q.lpart = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(w.lpart) + o);
     q.gpart = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(w.gpart) + o);
-    q.timeout = reinterpret_cast<int*>(reinterpret_cast<char*>(w.timeout) + o);
     hipLaunchKernelGGL(k_adam_prologue, dim3(256, rg), dim3(256), 0, st, q, n);
     PMG_LAUNCH_CHECK();
     // rg x G workgroups, at most one per CU (adam_batch_geometry): all co-resident
@@ -1027,6 +1028,17 @@ int pmg_mstep_adam(double* W, double* mu, double* nu, int64_t* count, const floa
                    void* workspace, size_t workspace_bytes, void* stream) {
   return adam_run(W, mu, nu, count, basis, yw, tw, L, NB, N, 1, cfg, stats, loss_hist, err_hist, workspace,
                   workspace_bytes, as_stream(stream));
+}
+
+int pmg_mstep_adam_status(void* workspace, int32_t* timed_out, void* stream) {
+  PMG_REQUIRE(workspace && timed_out, "pmg_mstep_adam_status: null argument");
+  hipStream_t st = as_stream(stream);
+  int32_t h = 0;
+  PMG_HIP(hipMemcpyAsync(&h, workspace, sizeof(h), hipMemcpyDeviceToHost, st));
+  PMG_HIP(hipStreamSynchronize(st));
+  if (h != 0) PMG_HIP(hipMemsetAsync(workspace, 0, sizeof(h), st));
+  *timed_out = h != 0;
+  return PMG_OK;
 }
 
 size_t pmg_mstep_batched_workspace_size(int32_t L, int32_t NB, int32_t N, int32_t R, int32_t maxiter) {

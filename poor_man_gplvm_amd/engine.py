@@ -274,7 +274,7 @@ class DeviceEM:
         self.ws_ss = torch.empty(int(ss_bytes), dtype=torch.uint8, device=dev)
         if self.ws_fb.numel() == 0:
             raise nat.NativeError(f"n_latent_bin={L} unsupported by the scan kernels (max 1024)")
-        self.ws_ad = None
+        self.ws_ad = AdamWorkspace(self.lib, self.dev)
         self.warm = [int(self.scan.warmup), int(self.scan.warmup)]   # forward, backward
         self._clean = [0, 0]
         self._rep_host = torch.zeros(nat.CTL_WORDS, dtype=torch.int32).pin_memory()
@@ -442,16 +442,15 @@ class DeviceEM:
                  or not self.lib.pmg_mstep_adam_supported(self.L, self.NB, n))
         need = int(self.lib.pmg_mstep_tiled_workspace_size(self.L, self.NB, n) if tiled
                    else self.lib.pmg_mstep_workspace_size(n, int(cfg.maxiter)))
-        if self.ws_ad is None or self.ws_ad.numel() < need:
-            self.ws_ad = torch.empty(need, dtype=torch.uint8, device=self.dev)
+        ws = self.ws_ad.get(need, tiled)
         c = cfg.to_c()
         fn = self.lib.pmg_mstep_adam_tiled if tiled else self.lib.pmg_mstep_adam
         with self._t('mstep_adam'):
           nat.check(fn(nat.ptr(W), nat.ptr(mu), nat.ptr(nu), nat.ptr(count),
                        nat.ptr(self.basis), nat.ptr(yw), nat.ptr(self.tw),
                        self.L, self.NB, n, ctypes.byref(c), nat.ptr(stats_out),
-                       nat.ptr(lh_out), nat.ptr(eh_out), nat.ptr(self.ws_ad),
-                       self.ws_ad.numel(), nat.stream_handle()),
+                       nat.ptr(lh_out), nat.ptr(eh_out), nat.ptr(ws),
+                       ws.numel(), nat.stream_handle()),
                     "pmg_mstep_adam_tiled" if tiled else "pmg_mstep_adam")
 
     def compute_tuning(self, W):
@@ -713,10 +712,17 @@ class DeviceEM:
         w = self.ctl_words()
         _raise_on_timeout(w, w.cpu().numpy(), "scan relaxation")
 
+    def adam_status(self):
+        """Raise if a persistent Adam launch since the last check timed out in a
+        cross-workgroup wait (sticky word, cleared here; syncs)."""
+        self.ws_ad.status()
+
     def check_status(self):
-        """Every sticky device error of the calls since the last check: the scans'
-        timeout words and (integer-path Poisson emission) the digit-range flag."""
+        """Every sticky device error of the calls since the last check: the scans' and
+        the Adam loop's timeout words and (integer-path Poisson emission) the digit-range
+        flag."""
         self.scan_status()
+        self.adam_status()
         if self.noise_std is None:
             self.emission_status()
 
@@ -734,17 +740,19 @@ class DeviceEM:
     def joint_log(self, log_rho):
         """Dense scans: log S[x,x'] = LSE_t log alpha_t[x] + log rho_{t+1}[x'] (2L x 2L, f64)."""
         S = torch.empty((2 * self.L, 2 * self.L), dtype=torch.float64, device=self.dev)
-        nat.check(self.lib.pmg_joint_log_accumulate(nat.ptr(self.log_alpha), nat.ptr(log_rho), self.T, self.L,
-                                                    nat.ptr(S), nat.stream_handle()), "pmg_joint_log_accumulate")
+        with self._t('joint_log'):
+            nat.check(self.lib.pmg_joint_log_accumulate(nat.ptr(self.log_alpha), nat.ptr(log_rho), self.T, self.L,
+                                                        nat.ptr(S), nat.stream_handle()), "pmg_joint_log_accumulate")
         return S
 
     def joint(self, rho):
         """S[x,x'] = sum_t alpha_t[x] rho_{t+1}[x'] (2L x 2L, f64)."""
         ws = torch.empty(int(self.lib.pmg_joint_workspace_size(self.T, self.L)), dtype=torch.uint8, device=self.dev)
         S = torch.empty((2 * self.L, 2 * self.L), dtype=torch.float64, device=self.dev)
-        nat.check(self.lib.pmg_joint_accumulate(nat.ptr(self.alpha), nat.ptr(rho), self.T, self.L, nat.ptr(S),
-                                                nat.ptr(ws), ws.numel(), nat.stream_handle()),
-                  "pmg_joint_accumulate")
+        with self._t('joint'):
+            nat.check(self.lib.pmg_joint_accumulate(nat.ptr(self.alpha), nat.ptr(rho), self.T, self.L, nat.ptr(S),
+                                                    nat.ptr(ws), ws.numel(), nat.stream_handle()),
+                      "pmg_joint_accumulate")
         return S
 
 
@@ -757,6 +765,39 @@ def _raise_on_timeout(words, host, what):
             words[d + nat.CTL_ERR] = 0
         raise nat.NativeError(f"{what}: grid barrier timed out (results of the calls since the last check are "
                               "invalid)")
+
+
+class AdamWorkspace:
+    """Workspaces of the Adam M-step.  The persistent kernels' (pmg_mstep_adam,
+    _batched) starts with the sticky timeout word of their bounded cross-workgroup waits,
+    so it is allocated zeroed and its word is read (and cleared) by status(); it is
+    checked before a larger one replaces it.  The tiled kernels get their own buffer."""
+
+    def __init__(self, lib, dev):
+        self.lib, self.dev = lib, dev
+        self.persistent = None
+        self.tiled = None
+
+    def get(self, need, tiled):
+        if tiled:
+            if self.tiled is None or self.tiled.numel() < need:
+                self.tiled = torch.empty(need, dtype=torch.uint8, device=self.dev)
+            return self.tiled
+        if self.persistent is None or self.persistent.numel() < need:
+            self.status()
+            self.persistent = torch.zeros(max(need, 256), dtype=torch.uint8, device=self.dev)
+        return self.persistent
+
+    def status(self):
+        """Raise if a persistent Adam launch since the last check gave up a bounded wait
+        on another workgroup (its W / mu / nu are then invalid).  Syncs the stream."""
+        if self.persistent is None:
+            return
+        flag = ctypes.c_int32(0)
+        nat.check(self.lib.pmg_mstep_adam_status(nat.ptr(self.persistent), ctypes.byref(flag),
+                                                 nat.stream_handle()), "pmg_mstep_adam_status")
+        if flag.value:
+            raise nat.NativeError("pmg_mstep_adam: a cross-workgroup wait timed out; the M-step result is invalid")
 
 
 def _flag_view(lib, ws, T, L, N):
@@ -845,7 +886,7 @@ class RestartBatchEM:
         ss_bytes = (self.lib.pmg_suffstats_bf16_workspace_size(T, LA, N) if spikes.ybt is not None
                     else self.lib.pmg_suffstats_workspace_size(T, LA, spikes.Np))
         self.ws_ss = torch.empty(int(ss_bytes), dtype=torch.uint8, device=dev)
-        self.ws_ad = None
+        self.ws_ad = AdamWorkspace(self.lib, self.dev)
         self.warm = [int(self.scan.warmup), int(self.scan.warmup)]
         self.timer = None
         self._tr_c = None
@@ -903,15 +944,14 @@ class RestartBatchEM:
         else:
             need = int(self.lib.pmg_mstep_tiled_workspace_size(L, NB, N) if tiled
                        else self.lib.pmg_mstep_workspace_size(N, int(cfg.maxiter)))
-        if self.ws_ad is None or self.ws_ad.numel() < need:
-            self.ws_ad = torch.empty(need, dtype=torch.uint8, device=self.dev)
+        ws = self.ws_ad.get(need, tiled)
         c = cfg.to_c()
         if batched:     # several restarts per persistent launch, each its own loop and stop rule
             with self._t('mstep_adam'):
                 nat.check(self.lib.pmg_mstep_adam_batched(
                     nat.ptr(W), nat.ptr(mu), nat.ptr(nu), nat.ptr(count), nat.ptr(self.basis), nat.ptr(self.yw),
                     nat.ptr(self.tw), L, NB, N, R, ctypes.byref(c), nat.ptr(stats_out), nat.ptr(lh_out),
-                    nat.ptr(eh_out), nat.ptr(self.ws_ad), self.ws_ad.numel(), sh), "pmg_mstep_adam_batched")
+                    nat.ptr(eh_out), nat.ptr(ws), ws.numel(), sh), "pmg_mstep_adam_batched")
             return
         fn = self.lib.pmg_mstep_adam_tiled if tiled else self.lib.pmg_mstep_adam
         with self._t('mstep_adam'):
@@ -920,7 +960,7 @@ class RestartBatchEM:
                              nat.ptr(self.basis), nat.ptr(self.yw[r * L:(r + 1) * L]),
                              nat.ptr(self.tw[r * L:(r + 1) * L]), L, NB, N, ctypes.byref(c),
                              nat.ptr(stats_out[r]), nat.ptr(lh_out[r]), nat.ptr(eh_out[r]),
-                             nat.ptr(self.ws_ad), self.ws_ad.numel(), sh),
+                             nat.ptr(ws), ws.numel(), sh),
                           "pmg_mstep_adam_tiled" if tiled else "pmg_mstep_adam")
 
     def compute_tuning(self, W):

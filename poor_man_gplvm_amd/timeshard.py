@@ -607,6 +607,7 @@ def run_em_timesharded(y, params, basis, log_posterior_init, n_iter, transition,
     lhn, ehn, lz = lh.cpu().numpy(), eh.cpu().numpy(), logz.cpu().numpy()
     for s in eng.shards:            # sticky device errors of every shard's calls
         s.emission_status()
+        s.adam_status()
     info = {'layouts': lays, 'carry_rounds': rounds, 'params64': Ws[0].cpu().numpy(),
             'repairs': [s.repairs() for s in eng.shards], 'chunk': lays[0].chunk,
             'warmup': [list(s.warm) for s in eng.shards]}

@@ -124,3 +124,46 @@ def test_emission_range_flag_other_paths(path):
         m.decode_latent_naive_bayes(d['y'], tuning=d['tuning'])
     else:
         m.log_marginal_masked(d['y'], np.ones((2, L)), tuning=d['tuning'])
+
+
+def test_adam_timeout_raises_and_clears():
+    """The persistent Adam kernel's cross-workgroup waits (row-block B^T G exchange at
+    L > 512, the lagged stop decision) are bounded by spin_ticks(): PMG_DEBUG_SPIN_TICKS=0
+    makes the first wait give up.  The sticky word in the workspace survives later
+    launches, adam_status() raises once and clears it, and a normal launch is exact again."""
+    from oracle import gplvm_oracle as O
+    from poor_man_gplvm_amd import _native as nat
+    from poor_man_gplvm_amd.engine import AdamConfig
+    N, L = 64, 1024
+    d = make(N, L, 300)
+    sp, eng = _engine(d, L)
+    assert eng.lib.pmg_mstep_adam_supported(eng.L, eng.NB, N) == 1
+    yw, tw = O.get_statistics(d['lp0'].astype(np.float64), d['y'])
+    eng.yw.copy_(torch.as_tensor(yw, device='cuda'))
+    eng.tw.copy_(torch.as_tensor(tw, device='cuda'))
+
+    def run():
+        W = torch.as_tensor(d['W0'].astype(np.float64), device='cuda').contiguous()
+        mu, nu = torch.zeros_like(W), torch.zeros_like(W)
+        cnt = torch.zeros(1, dtype=torch.int64, device='cuda')
+        stats = torch.zeros(4, dtype=torch.float64, device='cuda')
+        lh = torch.zeros(200, dtype=torch.float64, device='cuda')
+        eng.adam(W, mu, nu, cnt, AdamConfig(maxiter=200, tol=0.0), stats, lh, torch.zeros_like(lh))
+        return W, stats
+    os.environ["PMG_DEBUG_SPIN_TICKS"] = "0"
+    try:
+        run()
+        torch.cuda.synchronize()
+    finally:
+        os.environ.pop("PMG_DEBUG_SPIN_TICKS", None)
+    run()                                       # a later launch does not clear the word
+    with pytest.raises(nat.NativeError, match="timed out"):
+        eng.adam_status()
+    eng.adam_status()                           # cleared by the check
+    W, stats = run()
+    eng.check_status()
+    ref = O.adam_run(d['W0'].astype(np.float64), O.adam_init(d['W0']), 1.0, d['B'].astype(np.float64), yw, tw,
+                     maxiter=200, tol=0.0)
+    assert int(stats[0].item()) == ref['n_iter']
+    B = d['B'].astype(np.float64)
+    np.testing.assert_allclose(np.logaddexp(B @ W.cpu().numpy(), 0), np.logaddexp(B @ ref['params'], 0), rtol=1e-5)
