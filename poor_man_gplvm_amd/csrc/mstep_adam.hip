@@ -30,8 +30,8 @@ namespace pmg {
 // would drain vmcnt, cdna_hip_programming.md "Pipelining across barriers").
 #define PMG_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
-#ifndef PMG_ADAM_FASTSP
-#define PMG_ADAM_FASTSP 0
+#ifndef PMG_ADAM_SP_OCML
+#define PMG_ADAM_SP_OCML 0
 #endif
 
 constexpr int kLag = 4;                 // bodies a workgroup runs ahead of the decision
@@ -232,6 +232,33 @@ __device__ __forceinline__ double rcp_nr(double x) {
   r = fma(r, fma(-x, r, 1.0), r);
   return r;
 }
+// softplus(x) = max(x, 0) + log1p(e) and sigmoid(x), e = exp(-|x|), in f32 from three
+// hardware transcendentals (exp2, log2, rcp; ~25 VALU instead of the ~300 of OCML's
+// compensated log1pf + two expf + an IEEE division):
+//   e      exp_acc (the f32 product's rounding error restored);
+//   log1p  e >= 2^-7: Goldberg's log(u) e / (u - 1), u = f32(1 + e), which cancels the
+//          rounding of u; e < 2^-7: e (1 - e (1/2 - e (1/3 - e / 4))) (truncation < e^4 / 5);
+//   sigmoid (x >= 0 ? 1 : e) / u.
+// Each is within a few f32 ulps; the caller corrects f to first order in the f64 residual
+// of x and evaluates the gradient factor and the loss in f64.
+struct SoftplusF32 {
+  float f, sg;
+};
+__device__ __forceinline__ float log_f32(float x) {   // natural log from v_log_f32 (x > 0, normal)
+  return __builtin_amdgcn_logf(x) * 0.693147180559945309f;
+}
+__device__ __forceinline__ SoftplusF32 softplus_sigmoid(float x) {
+  const float e = exp_acc(-fabsf(x));
+  const float u = 1.f + e;
+  const float ru = __builtin_amdgcn_rcpf(u);
+  const float lg = log_f32(u) * (e * __builtin_amdgcn_rcpf(u - 1.f));   // u > 1 on this branch
+  const float ps = e * fmaf(-e, fmaf(-e, fmaf(-e, 0.25f, 0.333333343f), 0.5f), 1.f);
+  SoftplusF32 o;
+  o.f = fmaxf(x, 0.f) + (e < 0.0078125f ? ps : lg);
+  o.sg = (x >= 0.f ? 1.f : e) * ru;
+  return o;
+}
+
 template <int CTRL, typename T>
 __device__ __forceinline__ T dpp_t(T v) {
   if constexpr (sizeof(T) == 8) return dpp_d<CTRL>(v);
@@ -437,24 +464,24 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
       const float Fh = (float)F;
       const double r = F - (double)Fh;
       const bool live = is_row && s < S;
-#if PMG_ADAM_FASTSP
-      // one exp for softplus and sigmoid, one reciprocal of f for G and the loss's
-      // first-order correction
-      const float ex = expf(-fabsf(Fh));
-      const float f32 = fmaxf(Fh, 0.f) + log1pf(ex);
-      const float sg = (Fh >= 0.f ? 1.f : ex) / (1.f + ex);
-      const double fd = (double)f32 + (double)sg * r;
-      const double ifd = rcp_nr(fd + 1e-20);
-      const float gv = live ? (float)((ywd * ifd - twd) * (double)sg) : 0.f;
-      if (owner) sG[(lb * A + slot) * SP + s] = gv;
-      const double xl = (ywd != 0.0) ? ywd * ((double)logf(f32 + 1e-20f) + (double)sg * r * ifd) : 0.0;
-#else
+#if PMG_ADAM_SP_OCML
+      // round-3 form (A/B builds only): OCML log1pf / expf and a second f64 reciprocal
       const float f32 = fmaxf(Fh, 0.f) + log1pf(expf(-fabsf(Fh)));
       const float sg = 1.f / (1.f + expf(-Fh));
       const double fd = (double)f32 + (double)sg * r;
       const float gv = live ? (float)((ywd * rcp_nr(fd + 1e-20) - twd) * (double)sg) : 0.f;
       if (owner) sG[(lb * A + slot) * SP + s] = gv;
       const double xl = (ywd != 0.0) ? ywd * ((double)logf(f32 + 1e-20f) + (double)sg * r * rcp_nr((double)f32)) : 0.0;
+#else
+      const SoftplusF32 sp = softplus_sigmoid(Fh);
+      const float f32 = sp.f, sg = sp.sg;
+      const double fd = (double)f32 + (double)sg * r;
+      const double ifd = rcp_nr(fd + 1e-20);
+      const float gv = live ? (float)((ywd * ifd - twd) * (double)sg) : 0.f;
+      if (owner) sG[(lb * A + slot) * SP + s] = gv;
+      // log f = log f32 + sigmoid r / f to first order (the f64 reciprocal of fd: the
+      // difference from 1 / f32 is second order in r)
+      const double xl = (ywd != 0.0) ? ywd * ((double)log_f32(f32 + 1e-20f) + (double)sg * r * ifd) : 0.0;
 #endif
       lpart -= live ? xl - fd * twd : 0.0;
       __builtin_amdgcn_sched_barrier(0);

@@ -134,41 +134,46 @@ def test_c3_decode_vs_oracle(c3):
 
 def test_c3_one_em_iteration_vs_oracle(c3):
     """One EM iteration at the headline shape from (W0, lp0) under the reference's stop
-    rule (maxiter 1000, tol 1e-6): identical Adam iteration count, tuning rel 1e-5, log
-    marginal rel 1e-7, posterior within 1e-5 and 10 % of the fp32 reference-mimic's own
-    deviation (the bar of test_fit_em_fixed_iterations_golden), argmax exact."""
+    rule (maxiter 1000, tol 1e-6): identical Adam iteration count, final loss rel 1e-6, log
+    marginal rel 1e-7.  Tuning and posterior against a MEASURED floor, not a picked
+    constant: the 864-body Adam loop is chaotic at the f64 ulp, so 16 f64 oracle fits
+    whose y_w / t_w differ by 1e-15 relative (the scale of a different summation order;
+    tests/golden/make_ensemble.py -> c3_em_ensemble.npz) spread around the golden run by
+    up to 7.4e-5 in tuning, 8.6e-5 on the sampled posterior rows, 1.3e-4 in per-bin
+    occupancy and 1..8 argmax rows of 5000.  Ours must sit within 1.5x the ensemble's
+    largest deviation on each, argmax exact on the sampled rows wherever the top-2 gap
+    exceeds twice the posterior bar, and no more argmax flips over all rows than 1.5x the
+    ensemble's worst (the fp32 reference-mimic is 4.1e-2 off in tuning)."""
     import poor_man_gplvm_amd as P
     f, d = c3
+    e = np.load(os.path.join(HERE, 'golden', 'c3_em_ensemble.npz'))
     L = int(f['L'])
     m = P.PoissonGPLVMJump1D(int(f['N']), n_latent_bin=L, tuning_lengthscale=10.)
     m.params = d['W0'].astype(np.float32)
     res = m.fit_em(d['y'], n_iter=1, log_posterior_init=d['lp0'])
     rows = f['rows']
     assert res['m_step_res_l']['n_iter'] == list(f['em_m_n_iter'])
+    assert set(e['ens_n_iter'].tolist()) == {int(f['em_m_n_iter'][0])}
     np.testing.assert_allclose(res['m_step_res_l']['final_loss'], f['em_m_final_loss'], rtol=1e-6)
     np.testing.assert_allclose(res['log_marginal_l'], f['em_log_marginal_l'], rtol=1e-7)
-    # Tuning: at this shape the 864-body Adam loop is chaotic at the f64 ulp: perturbing
-    # y_w by 1e-15 relative moves the f64 oracle's own tuning by 1.8e-5 (1e-13: 9e-6,
-    # 1e-9: 2.7e-5; tools/diag_mstep_conditioning.py, profiles/r03_mstep_conditioning.txt)
-    # and the fp32 reference-mimic lands 4.1e-2 away, so no implementation that is not
-    # the oracle's own f64 summation order can meet 1e-5 here (measured: 3.4e-5).  Bar:
-    # 1e-4 (the f64 perturbation floor) and 1 % of the reference-mimic's deviation.
     tun_dev = np.max(np.abs(res['tuning'] / f['em_tuning'] - 1))
-    mimic_dev = np.max(np.abs(f['mimic32_tuning'].astype(np.float64) / f['em_tuning'] - 1))
-    assert tun_dev < 1e-4 and tun_dev < 0.01 * mimic_dev, (tun_dev, mimic_dev)
-    # The posterior inherits that tuning spread (measured 6.5e-5 max abs against the
-    # mimic's 2.0e-2); the E-step itself is exact at this shape (test_c3_decode_vs_oracle,
-    # rel 1e-5 with the oracle's tuning).  Bar: 2e-4 and 1 % of the mimic's deviation.
     plm = np.asarray(res['posterior_latent_marg'], np.float64)
     exact = f['em_posterior_latent_rows'].astype(np.float64)
-    ref_noise = np.abs(f['mimic32_posterior_latent_rows'].astype(np.float64) - exact).max()
     dev = np.abs(plm[rows] - exact).max()
-    assert dev < 2e-4 and dev < 0.01 * ref_noise, (dev, ref_noise)
+    tw_dev = np.abs(plm.sum(0) - f['em_tw']).sum() / plm.shape[0]
+    flips = int((np.argmax(plm, 1) != f['em_argmax']).sum())
+    bars = {k: 1.5 * float(np.max(e[k])) for k in ('ens_tuning_dev', 'ens_posterior_dev', 'ens_tw_dev',
+                                                      'ens_argmax_flips')}
+    print(f"C3 one EM iteration: tuning {tun_dev:.3e} (bar {bars['ens_tuning_dev']:.3e}), posterior rows {dev:.3e} "
+          f"(bar {bars['ens_posterior_dev']:.3e}), tw {tw_dev:.3e} (bar {bars['ens_tw_dev']:.3e}), argmax flips "
+          f"{flips} (bar {bars['ens_argmax_flips']:.1f})")
+    assert tun_dev <= bars['ens_tuning_dev']
+    assert dev <= bars['ens_posterior_dev']
+    assert tw_dev <= bars['ens_tw_dev']
+    assert flips <= bars['ens_argmax_flips']
     srt = np.sort(exact, axis=1)
-    clear = (srt[:, -1] - srt[:, -2]) > 1e-3
+    clear = (srt[:, -1] - srt[:, -2]) > 2 * bars['ens_posterior_dev']
     assert np.all(np.argmax(plm[rows], 1)[clear] == np.argmax(exact, 1)[clear])
-    # occupancies t_w = sum_t P: the same spread summed over T (mean per-bin L1 <= 2e-4)
-    assert np.abs(plm.sum(0) - f['em_tw']).sum() / plm.shape[0] < 2e-4
 
 
 def test_c4_time_sharded_vs_single():
