@@ -388,6 +388,9 @@ int pmg_roll_columns(const float* y, int64_t T, int32_t N, const int64_t* shift,
 /*   W, mu, nu (NB,N) f64 in/out; count (1) int64 in/out (optax count).  */
 /*   stats (4) f64 out: n_iter, final_loss, final_error, unused.          */
 /*   loss_hist, err_hist (maxiter) f64 out (zeros past n_iter).           */
+/*   tol < 0: the loop never stops before maxiter (not even on a NaN loss,  */
+/*   whose relative change compares false): the speculative batches of the */
+/*   neuron-sharded M-step apply the stop rule on the host.                */
 typedef struct pmg_adam_cfg {
   double lr, b1, b2, eps, eps_root;
   double prior_std;

@@ -308,6 +308,30 @@ class PoissonGPLVMJump1D:
         model's own transition for these hyper-parameters."""
         return dict(hyperparam), None, None
 
+    def decode_marginals(self, y, tuning=None, hyperparam={}, ma_neuron=None, ma_latent=None,
+                         likelihood_scale=1.):
+        """The part of decode_latent that model evaluation reads (model_selection_helper.py:
+        89-97): log_marginal_final, log_one_step_predictive_marginals_all and
+        posterior_dynamics_marg, from the banded linear-space scans without the pairwise
+        joint (the dense log-domain scans of ScanConfig.decode_exact only matter for the
+        transition rows of latents the posterior never visits).  The same values as
+        decode_latent's within the scans' 1e-5 parity bar; not part of the reference API."""
+        if _is_tsd(y):
+            y = y.d
+        tuning = self.tuning if tuning is None else tuning
+        ma_neuron = self.ma_neuron_default if ma_neuron is None else ma_neuron
+        ma_latent = self.ma_latent_default if ma_latent is None else ma_latent
+        hp, logK, logA = self._dynamics_decode_args(hyperparam)
+        eng = self._decode_engine(y, tuning, hp, ma_neuron, ma_latent, logK, logA, exact=False)
+        logz = torch.zeros(1, dtype=torch.float64, device=eng.dev)
+        gamma = torch.empty((eng.T, 2, self.n_latent_bin), dtype=torch.float32, device=eng.dev)
+        lgam = torch.empty_like(gamma) if eng.dense else None
+        eng.e_step(likelihood_scale, logz, gamma=gamma, log_gamma=lgam)
+        eng.check_status()
+        return {'log_marginal_final': float(_np(logz)[0]),
+                'log_one_step_predictive_marginals_all': _np(eng.logc).astype(np.float32),
+                'posterior_dynamics_marg': _np(gamma.sum(dim=2))}
+
     def _decode_result(self, r, t_l=None):
         """decode_latent's returned dict from a _decode_on result (core.py:477-497)."""
         posterior_all = r['posterior_all']
@@ -447,7 +471,7 @@ class PoissonGPLVMJump1D:
         delta0, rblk0 = eng.emission_unmasked()
         mu8 = torch.as_tensor((masks != 0).astype(np.uint8), device=eng.dev)
         R = len(masks)
-        if not eng.dense and self.n_latent_bin % 32 == 0 and R > 1:
+        if not eng.dense and self.n_latent_bin % 32 == 0:
             # batched: Rg masks per pass (stacked masked emissions, one forward launch)
             Rg = eng.mask_batch_size(R)
             for r0 in range(0, R, Rg):

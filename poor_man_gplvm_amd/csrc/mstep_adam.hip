@@ -687,7 +687,9 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
           cont = false;
         } else {
           const double rel = fabs(loss - loss_prev) / fmax(fabs(loss), 1e-8);
-          cont = (j + 1 < maxiter - 1) && ((j + 1 < 5) || (rel > p.tol));
+          // tol < 0: no early stop (the speculative batches of the neuron-sharded M-step),
+          // also not on a NaN loss, whose rel compares false
+          cont = (j + 1 < maxiter - 1) && ((j + 1 < 5) || p.tol < 0.0 || (rel > p.tol));
         }
         loss_prev = loss;
         ++dj;

@@ -249,7 +249,8 @@ __global__ void __launch_bounds__(256) k_at_ctrl(AtParams p, int mode) {
     *p.count += 1;
   }
   const double L0 = c->loss, Lp = c->loss_prev;
-  const bool go = (i < p.maxiter - 1) && (i < 5 || fabs(L0 - Lp) / fmax(fabs(L0), 1e-8) > p.tol);
+  // tol < 0: no early stop (speculative batches), also not on a NaN loss
+  const bool go = (i < p.maxiter - 1) && (i < 5 || p.tol < 0.0 || fabs(L0 - Lp) / fmax(fabs(L0), 1e-8) > p.tol);
   p.stats[0] = (double)(i + 1);
   p.stats[1] = L0;
   p.stats[2] = c->err;

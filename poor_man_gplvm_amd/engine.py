@@ -497,6 +497,9 @@ class DeviceEM:
         device tensor; pmg_emission_latent_mask), then the row reference."""
         if tuple(ma_latent_u8.shape) != (self.L,) or ma_latent_u8.dtype != torch.uint8:
             raise ValueError(f"ma_latent_u8 must be a ({self.L},) uint8 tensor")
+        # the f64 ll the dense scans prefer when present is the UNMASKED one
+        # (emission_unmasked): drop it, so the masked (delta, rblk) are what the scans read
+        self.ll64 = None
         sh = nat.stream_handle()
         with self._t('emission_mask'):
             nat.check(self.lib.pmg_emission_latent_mask(nat.ptr(delta0), nat.ptr(rblk0), self.T, self.L,
@@ -514,6 +517,18 @@ class DeviceEM:
         per = 13 * self.T * self.L
         return int(max(1, min(R, self.MASK_BATCH_MAX, self.MASK_BATCH_BYTES // max(per, 1))))
 
+    def masked_chunk(self):
+        """Forward chunk of the log-marginal mask passes (independent of the batch size)."""
+        return max(32, int(math.ceil(self.MASK_BATCH_MAX * self.T / 2048)))
+
+    def masked_segments(self):
+        """Relaxation segments per mask of the log-marginal passes (independent of the batch
+        size; all MASK_BATCH_MAX masks' segments are co-resident)."""
+        if self.scan.relax_segments:
+            return int(self.scan.relax_segments)
+        cus = torch.cuda.get_device_properties(self.dev).multi_processor_count
+        return max(1, cus // self.MASK_BATCH_MAX)
+
     def masked_logz_batched(self, delta0, rblk0, masks_u8, likelihood_scale, logz_out):
         """log_marginal_final of the forward filter under each of R latent masks
         (masks_u8 (R, L) uint8 device tensor) in ONE pass per stage: the R masked
@@ -521,9 +536,11 @@ class DeviceEM:
         (pmg_emission_latent_mask_batched), one row reference per mask
         (pmg_emission_rowref_batched) and one chunk-parallel forward launch covers every
         mask (pmg_forward_filter_batched, blockIdx.y = mask, no alpha written:
-        PMG_PHASE_NO_ALPHA).  Chunks are sized so the R chains together number ~2048.
-        Mask r's logZ equals a single-mask forward on the same chunk and relaxation
-        segment grid (ScanConfig(chunk=C, relax_segments=#CUs / R)) bit for bit.
+        PMG_PHASE_NO_ALPHA).  The chunk and the relaxation segment grid are pinned to
+        the largest batch (MASK_BATCH_MAX masks: chunk ceil(16 T / 2048), #CUs / 16
+        segments per mask), so a mask's logZ does not depend on how many masks share
+        its batch, on the rank count that dealt them, or on the memory budget; it equals
+        a single-mask forward on that chunk and segment grid bit for bit.
         Banded transitions, L % 32 == 0."""
         R = int(masks_u8.shape[0])
         T, L, dev = self.T, self.L, self.dev
@@ -531,7 +548,7 @@ class DeviceEM:
             raise nat.NativeError("batched masks need the banded scans and n_latent_bin % 32 == 0")
         nb = self.nblk
         sc = self.scan
-        C = int(sc.chunk) if sc.chunk else max(32, int(math.ceil(R * T / 2048)))
+        C = int(sc.chunk) if sc.chunk else self.masked_chunk()
         key = (R, C)
         if getattr(self, '_mb_key', None) != key:
             f32, f64 = torch.float32, torch.float64
@@ -561,8 +578,9 @@ class DeviceEM:
         with self._t('forward_filter'):
             nat.check(self.lib.pmg_forward_filter_batched(*args, 1 | nat.PHASE_NO_ALPHA), "pmg_forward_filter_batched")
         with self._t('forward_repair'):
-            nat.check(self.lib.pmg_forward_filter_batched(*args, 2 | nat.PHASE_NO_ALPHA | self._seg_bits()),
-                      "pmg_forward_filter_batched")
+            nat.check(self.lib.pmg_forward_filter_batched(
+                *args, 2 | nat.PHASE_NO_ALPHA | nat.phase_segments(self.masked_segments())),
+                "pmg_forward_filter_batched")
         w = b['ws']
         slab = (w.numel() // R) & ~255 if R > 1 else w.numel()
         views = [w[r * slab:r * slab + 4 * nat.CTL_WORDS].view(torch.int32) for r in range(R)]

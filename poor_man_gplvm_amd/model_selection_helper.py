@@ -200,7 +200,10 @@ def evaluate_model_one_config(model_fit_l, y_test, key=1, n_time_per_chunk=10000
     for k in range(rank, len(model_fit_l), world):
         with _local_only():          # the fits are the shard axis here
             m = model_fit_l[k]
-            dec = m.decode_latent(y_test, n_time_per_chunk=n_time_per_chunk)
+            # only the log marginals and the dynamics marginal are read: no pairwise joint
+            # (jump models; the latent-only models decode through decode_latent)
+            dm = None if isinstance(m, PoissonGPLVM1D) else getattr(m, 'decode_marginals', None)
+            dec = dm(y_test) if dm is not None else m.decode_latent(y_test, n_time_per_chunk=n_time_per_chunk)
             v = {'lml': dec['log_marginal_final'],
                  'os': np.asarray(dec['log_one_step_predictive_marginals_all']).sum()}
             if want_ds:

@@ -166,8 +166,10 @@ def test_latent_mask_apply_matches_masked_emission(path):
 def test_masked_logz_batched_bit_identical(R, chunk):
     """DeviceEM.masked_logz_batched (R masks: one stacked mask launch, one row-reference
     launch, one forward launch, no alpha) == R single-mask forward filters on the same
-    chunk grid and relaxation segments (ScanConfig(chunk=C, relax_segments=#CUs / R)),
-    bit for bit; and == the f64 oracle's masked log marginals at rel 1e-7."""
+    chunk grid and relaxation segments (pinned: ScanConfig(chunk=C, relax_segments=#CUs /
+    MASK_BATCH_MAX)), bit for bit; a mask's logZ does not depend on how many masks share
+    its batch (the first two masks alone give the same bits); and == the f64 oracle's
+    masked log marginals at rel 1e-7."""
     import math
     import torch
     from poor_man_gplvm_amd import model_selection_helper as MS
@@ -176,7 +178,7 @@ def test_masked_logz_batched_bit_identical(R, chunk):
     N, L, T = 40, 128, 3000
     d = make(N, L, T)
     masks = MS.downsample_latent_masks(L, 0.3, R, key=5)
-    C = chunk or max(32, int(math.ceil(R * T / 2048)))
+    C = chunk or max(32, int(math.ceil(DeviceEM.MASK_BATCH_MAX * T / 2048)))
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     tr = banded_transition(L, 1.0, 0.01, 0.01)
 
@@ -191,7 +193,11 @@ def test_masked_logz_batched_bit_identical(R, chunk):
     lz = torch.zeros(R, dtype=torch.float64, device='cuda')
     eng.masked_logz_batched(delta0, rblk0, mu8, 1.0, lz)
     got = lz.cpu().numpy()
-    one = engine(ScanConfig(chunk=C, relax_segments=max(1, cus // R)))
+    assert eng.masked_segments() == max(1, cus // DeviceEM.MASK_BATCH_MAX)
+    lz2 = torch.zeros(2, dtype=torch.float64, device='cuda')
+    eng.masked_logz_batched(delta0, rblk0, mu8[:2].contiguous(), 1.0, lz2)
+    np.testing.assert_array_equal(lz2.cpu().numpy(), got[:2])
+    one = engine(ScanConfig(chunk=C, relax_segments=max(1, cus // DeviceEM.MASK_BATCH_MAX)))
     d1, r1 = one.emission_unmasked()
     seq = np.empty(R)
     for r in range(R):
@@ -203,3 +209,23 @@ def test_masked_logz_batched_bit_identical(R, chunk):
     np.testing.assert_array_equal(got, seq)
     ref = O.downsampled_lml(d['y'], d['tuning'], masks)[0]
     np.testing.assert_allclose(got, ref, rtol=1e-7)
+
+
+def test_decode_marginals_match_decode_latent():
+    """decode_marginals (banded scans, no pairwise joint: what evaluate_model_one_config
+    reads) against decode_latent (dense exact scans + joint) and the f64 oracle: log
+    marginal rel 1e-7, one-step marginals rel 1e-5 (atol 1e-5), dynamics marginal at the
+    posterior bar (rel 1e-5, atol 1e-12)."""
+    import poor_man_gplvm_amd as P
+    from tests.test_gpu_parity import close_prob
+    N, L, T = 40, 128, 2000
+    d = make(N, L, T)
+    m = P.PoissonGPLVMJump1D(N, n_latent_bin=L, tuning_lengthscale=10.)
+    a = m.decode_marginals(d['y'], tuning=d['tuning'])
+    b = m.decode_latent(d['y'], tuning=d['tuning'])
+    ref = O.decode_latent(d['y'], d['tuning'])
+    for r in (a, b):
+        np.testing.assert_allclose(r['log_marginal_final'], ref['log_marginal_final'], rtol=1e-7)
+        np.testing.assert_allclose(r['log_one_step_predictive_marginals_all'],
+                                   ref['log_one_step_predictive_marginals_all'], rtol=1e-5, atol=1e-5)
+        close_prob(r['posterior_dynamics_marg'], ref['posterior_dynamics_marg'])
