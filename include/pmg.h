@@ -251,7 +251,14 @@ int pmg_backward_smoother(const float* delta, const float* phi, const float* alp
 /* so two calls agree bit for bit only on the same segment grid: a single fit    */
 /* run with S = #CUs / R reproduces restart r of an R-restart batch.             */
 #define PMG_PHASE_SEGMENTS(S) ((int32_t)((S) & 0xfff) << 16)
-#define PMG_PHASE_FLAG_BITS (7 | PMG_PHASE_ADAPTIVE_WARMUP | PMG_PHASE_NO_ALPHA | (0xfff << 16))
+/* Backward only: OR PMG_PHASE_P_BF16X3 into both phase calls to write P as three */
+/* bf16 planes instead of f32: P then points at uint16 [3][T][ldd] (ldd = L, or  */
+/* R*L batched), plane k at P + k*T*ldd: hi = the top 16 bits of the f32 P value, */
+/* mid / lo those of the successive remainders, so P = (hi + mid) + lo exactly in  */
+/* f32.  They are the exact-product operands of pmg_suffstats_bf16x3 (the split  */
+/* runs once per value here instead of once per neuron tile in the statistics).  */
+#define PMG_PHASE_P_BF16X3 32
+#define PMG_PHASE_FLAG_BITS (7 | PMG_PHASE_ADAPTIVE_WARMUP | PMG_PHASE_NO_ALPHA | PMG_PHASE_P_BF16X3 | (0xfff << 16))
 int pmg_forward_filter_phase(const float* delta, const float* phi, const double* m, int64_t T,
                              const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                              int32_t warmup, double tol, float* alpha, double* logc, double* logz,
@@ -437,6 +444,17 @@ int pmg_mstep_adam_tiled(double* W, double* mu, double* nu, int64_t* count, cons
                          const double* yw, const double* tw, int32_t L, int32_t NB, int32_t N,
                          const pmg_adam_cfg* cfg, double* stats, double* loss_hist, double* err_hist,
                          void* workspace, size_t workspace_bytes, void* stream);
+
+/* Sufficient statistics from P's bf16 planes (PMG_PHASE_P_BF16X3 output):       */
+/* Pq uint16 [3][T][ldp] (ldp >= L, ldp % 8 == 0: the row stride of the planes,    */
+/* R*L for stacked restarts with L = R*L), ybt as pmg_suffstats_bf16.  The same    */
+/* exact-product bf16 MFMA GEMMs as pmg_suffstats_bf16 without the split (which   */
+/* the backward did once per value); t_w from (hi + mid) + lo.  Replaces           */
+/* fit_tuning_helper.get_statistics (fit_tuning_helper.py:28-42).                  */
+size_t pmg_suffstats_bf16x3_workspace_size(int64_t T, int32_t L, int32_t N);
+int pmg_suffstats_bf16x3(const uint16_t* Pq, int64_t ldp, const uint16_t* ybt, int64_t T, int64_t Tp, int32_t L,
+                         int32_t N, int32_t Np, double* yw, double* tw, void* workspace, size_t workspace_bytes,
+                         void* stream);
 
 /* ------------------------------------------------------------------ */
 /* Pairwise joint (decode only) -- the logaddexp accumulation of         */

@@ -30,6 +30,8 @@ PHASE_NO_JUMP_ROWS = 4
 PHASE_ADAPTIVE_WARMUP = 8
 # forward, both phase calls: no alpha written at all (logc / logZ only; PMG_PHASE_NO_ALPHA)
 PHASE_NO_ALPHA = 16
+# backward, both phase calls: P written as three bf16 planes [3][T][ldd] (PMG_PHASE_P_BF16X3)
+PHASE_P_BF16X3 = 32
 ABI_VERSION = 2
 
 
@@ -60,6 +62,7 @@ EXPORTED_SYMBOLS = (
     "pmg_forward_filter_batched", "pmg_backward_smoother_batched",
     "pmg_mstep_batched_workspace_size", "pmg_mstep_adam_batched_supported", "pmg_mstep_adam_batched",
     "pmg_emission_range_flag", "pmg_mstep_adam_status",
+    "pmg_suffstats_bf16x3_workspace_size", "pmg_suffstats_bf16x3",
 )
 
 
@@ -123,6 +126,8 @@ _SIGS = {
     "pmg_spikes_bf16t": ([_P, _I64, _I32, _P, _I64, _P], _I32),
     "pmg_suffstats_bf16_workspace_size": ([_I64, _I32, _I32], _SZ),
     "pmg_suffstats_bf16": ([_P, _P, _I64, _I64, _I32, _I32, _I32, _P, _P, _P, _SZ, _P], _I32),
+    "pmg_suffstats_bf16x3_workspace_size": ([_I64, _I32, _I32], _SZ),
+    "pmg_suffstats_bf16x3": ([_P, _I64, _P, _I64, _I64, _I32, _I32, _I32, _P, _P, _P, _SZ, _P], _I32),
     "pmg_exp": ([_P, _I64, _P, _P], _I32),
     "pmg_log": ([_P, _I64, _P, _P], _I32),
     "pmg_roll_columns": ([_P, _I64, _I32, _P, _P, _P], _I32),

@@ -366,21 +366,8 @@ __global__ void __launch_bounds__(1024) k_emission_pipe(
     const double* __restrict__ gconst, int64_t T, int64_t Tp, int L, int Lp, int Kp, int nLT,
     int ntile, float* __restrict__ delta, double* __restrict__ rblk, double* __restrict__ ll64,
     unsigned long long* __restrict__ stamps) {
-#ifdef PMG_EM_STAMPS
-  // diagnostic build: s_memtime at 4 points of the first 64 chunks, waves 0 and 7, in the
-  // last 4 KiB of LDS, copied out per workgroup at the end
-  __shared__ __attribute__((aligned(16))) int8_t smem[PLDS + 4096];
-  unsigned long long* sst = reinterpret_cast<unsigned long long*>(smem + PLDS);
-#define PMG_EM_STAMP(x, k)                                                                        \
-  if ((wid == 0 || wid == 7) && lane == 0 && (x) < 64) {                                         \
-    sst[(wid == 7) * 256 + (x) * 4 + (k)] = __builtin_amdgcn_s_memtime();                        \
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                           \
-  }
-#else
   __shared__ __attribute__((aligned(16))) int8_t smem[PLDS];
-#define PMG_EM_STAMP(x, k)
   (void)stamps;
-#endif
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -426,7 +413,6 @@ __global__ void __launch_bounds__(1024) k_emission_pipe(
   v16i acc[kDig];
   int ti = 0, kc = 0;
   for (int x = 0; x < S; ++x) {
-    PMG_EM_STAMP(x, 0)
     {
       // my DMA pieces of chunks x + 1, x + 2 and the stores of epilogues at x - 3 .. x - 1
       // may stay in flight
@@ -437,20 +423,15 @@ __global__ void __launch_bounds__(1024) k_emission_pipe(
       vm_wait_upto(n < 63 ? n : 63);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
-    PMG_EM_STAMP(x, 1)
     if (x + 3 < S) {
       cx.issue(dti, dkc, (x + 3) & (PNS - 1));
       if (++dkc == nch) { dkc = 0; ++dti; }
     }
-    PMG_EM_STAMP(x, 2)
     if (kc == 0) {
 #pragma unroll
       for (int d = 0; d < kDig; ++d) acc[d] = (v16i){0};
     }
     const int sbo = (x & (PNS - 1)) * PSTAGE;
-#ifdef PMG_EM_NOCOMPUTE
-    if (lane == 64) // never: keeps the loop's shape without the MFMAs (diagnostic build)
-#endif
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int8_t* sa = smem + sbo + (aoff ^ (32 * ks));
@@ -464,17 +445,10 @@ __global__ void __launch_bounds__(1024) k_emission_pipe(
     }
     const int cur = ti;
     if (++kc < nch) {
-      PMG_EM_STAMP(x, 3)
       continue;
     }
     kc = 0;
     ++ti;
-#if defined(PMG_EM_NOCOMPUTE) || defined(PMG_EM_NOEPI)
-    if (lane < 64) {   // diagnostic builds: no epilogue
-      PMG_EM_STAMP(x, 3)
-      continue;
-    }
-#endif
 
     // epilogue of tile cur (k_emission_i8's arithmetic, constants from the LDS slot)
     int64_t t0;
@@ -528,14 +502,7 @@ __global__ void __launch_bounds__(1024) k_emission_pipe(
       __builtin_amdgcn_raw_buffer_store_b32((uint32_t)mu, rr, ob, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(mu >> 32), rr, ob + 4, 0, 0);
     }
-    PMG_EM_STAMP(x, 3)
   }
-#ifdef PMG_EM_STAMPS
-  __syncthreads();
-  if (stamps && (wid == 0 || wid == 7) && lane == 0)
-    for (int i = 0; i < 256; ++i) stamps[blockIdx.x * 512 + (wid == 7) * 256 + i] = sst[(wid == 7) * 256 + i];
-#endif
-#undef PMG_EM_STAMP
 }
 
 // ---------------------------------------------------------------------------------
@@ -587,19 +554,8 @@ __global__ void __launch_bounds__(512) k_emission_yreg(
   constexpr int Kp = KC * CK;
   constexpr int RNS = YRing<CK>::NS, RSTAGE = YRing<CK>::STAGE, RPIECES = YRing<CK>::PIECES;
   constexpr int RPP = YRing<CK>::RPP, NSEG = YRing<CK>::NSEG;
-#ifdef PMG_EM_STAMPS
-  __shared__ __attribute__((aligned(16))) int8_t smem[RNS * RSTAGE + RLC_MAX * 8 + 4096];
-  unsigned long long* sst = reinterpret_cast<unsigned long long*>(smem + RNS * RSTAGE + RLC_MAX * 8);
-#define PMG_YR_STAMP(x, k)                                                                        \
-  if ((wid == 0 || wid == 4) && lane == 0 && (x) < 48) {                                         \
-    sst[(wid == 4) * 256 + (x) * 5 + (k)] = __builtin_amdgcn_s_memtime();                        \
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                           \
-  }
-#else
   __shared__ __attribute__((aligned(16))) int8_t smem[RNS * RSTAGE + RLC_MAX * 8];
-#define PMG_YR_STAMP(x, k)
   (void)stamps;
-#endif
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -684,7 +640,6 @@ __global__ void __launch_bounds__(512) k_emission_yreg(
 #pragma unroll
     for (int c = 0; c < KC; ++c) {
       const int x = xi * KC + c;
-      PMG_YR_STAMP(x, 0)
       {
         // my DMA pieces of chunks x + 1 .. x + RNS - 2 and the stores of the epilogues at
         // chunks x - RNS + 1 .. x - 1 (younger than piece x) may stay in flight
@@ -694,10 +649,8 @@ __global__ void __launch_bounds__(512) k_emission_yreg(
 #pragma unroll
         for (int j = 1; j <= RNS - 1; ++j) n += (x - j >= 0 && ((x - j) % KC) == KC - 1) ? NST : 0;
         vm_wait_upto(n < 63 ? n : 63);
-        PMG_YR_STAMP(x, 4)
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       }
-      PMG_YR_STAMP(x, 1)
       const int8_t* sq = smem + (x % RNS) * RSTAGE;
 #pragma unroll
       for (int ks = 0; ks < CK / 32; ++ks) {
@@ -711,13 +664,11 @@ __global__ void __launch_bounds__(512) k_emission_yreg(
           // the next DMA behind the first k-step's MFMAs (their issue hides its SALU work)
           __builtin_amdgcn_sched_barrier(0);
           if (x + RNS - 1 < S) PMG_YR_ISSUE(x + RNS - 1)
-          PMG_YR_STAMP(x, 2)
           __builtin_amdgcn_sched_barrier(0);
         }
       }
     }
 
-    PMG_YR_STAMP(xi * KC + KC - 1, 3)
     // epilogue (k_emission_i8's arithmetic)
     const int nblk = Lp >> 5;
     const int blk = l0 >> 5;
@@ -792,12 +743,6 @@ __global__ void __launch_bounds__(512) k_emission_yreg(
       }
     }
   }
-#ifdef PMG_EM_STAMPS
-  __syncthreads();
-  if (stamps && (wid == 0 || wid == 4) && lane == 0)
-    for (int i = 0; i < 256; ++i) stamps[blockIdx.x * 512 + (wid == 4) * 256 + i] = sst[(wid == 4) * 256 + i];
-#endif
-#undef PMG_YR_STAMP
 #undef PMG_YR_ISSUE
 }
 
@@ -983,12 +928,6 @@ int pmg_emission_poisson(const int8_t* yq, const double* gconst, const double* t
     int nwg = device_cu_count();
     if (nwg > nitem) nwg = nitem;
     unsigned long long* ystamps = nullptr;
-#ifdef PMG_EM_STAMPS
-    static unsigned long long* ybuf = nullptr;
-    if (!ybuf) PMG_HIP(hipMalloc(&ybuf, (size_t)1024 * 512 * 8));
-    PMG_HIP(hipMemsetAsync(ybuf, 0, (size_t)nwg * 512 * 8, st));
-    ystamps = ybuf;
-#endif
 #define PMG_YR_LAUNCH(CK, KC)                                                                               \
   {                                                                                                         \
     auto kern = ll64 ? (ma_latent ? k_emission_yreg<CK, KC, true, true> : k_emission_yreg<CK, KC, true, false>) \
@@ -1005,40 +944,6 @@ int pmg_emission_poisson(const int8_t* yq, const double* gconst, const double* t
     }
 #undef PMG_YR_LAUNCH
     PMG_LAUNCH_CHECK();
-#ifdef PMG_EM_STAMPS
-    {
-      // chunk x: [0] top, [1] after wait + barrier, [2] after DMA issue; [3] of an item's
-      // last chunk: MFMAs issued (epilogue starts); next chunk's [0] closes the period
-      std::vector<unsigned long long> hh((size_t)nwg * 512);
-      PMG_HIP(hipStreamSynchronize(st));
-      PMG_HIP(hipMemcpy(hh.data(), ybuf, hh.size() * 8, hipMemcpyDeviceToHost));
-      const int KCh = Kp == 384 ? 3 : (Kp == 512 ? 2 : 1);
-      for (int w = 0; w < 2; ++w) {
-        double vw = 0, wb = 0, is = 0, cp = 0, ep = 0, per = 0, pere = 0;
-        int n = 0, ne = 0;
-        for (int b = 0; b < nwg; ++b)
-          for (int x = 1; x < 47; ++x) {
-            const unsigned long long* q = &hh[(size_t)b * 512 + w * 256 + x * 5];
-            if (!q[0] || !q[5]) continue;
-            vw += q[4] - q[0];
-            wb += q[1] - q[4];
-            is += q[2] - q[1];
-            if ((x % KCh) == KCh - 1 && q[3]) {
-              cp += q[3] - q[2];
-              ep += q[5] - q[3];
-              pere += q[5] - q[0];
-              ++ne;
-            } else {
-              per += q[5] - q[0];
-              ++n;
-            }
-          }
-        fprintf(stderr, "[yr-stamps] wave %d: vmwait %.0f barrier %.0f issue %.0f | inner period %.0f (n=%d) | last chunk: mfma %.0f epilogue %.0f period %.0f (n=%d)\n",
-                w ? 4 : 0, vw / (n + ne), wb / (n + ne), is / (n + ne), n ? per / n : 0.0, n, ne ? cp / ne : 0.0,
-                ne ? ep / ne : 0.0, ne ? pere / ne : 0.0, ne);
-      }
-    }
-#endif
     return PMG_OK;
   }
   const bool pipe = !(pipe_s && pipe_s[0] == '0') && (int64_t)kDig * Lp * Kp < (1ll << 31) &&
@@ -1052,47 +957,9 @@ int pmg_emission_poisson(const int8_t* yq, const double* gconst, const double* t
     if (nwg < 8) nwg = 8;
     auto kern = ll64 ? k_emission_pipe<true> : k_emission_pipe<false>;
     unsigned long long* stamps = nullptr;
-#ifdef PMG_EM_STAMPS
-    static unsigned long long* dst_stamps = nullptr;
-    if (!dst_stamps) PMG_HIP(hipMalloc(&dst_stamps, (size_t)nwg * 512 * 8));
-    PMG_HIP(hipMemsetAsync(dst_stamps, 0, (size_t)nwg * 512 * 8, st));
-    stamps = dst_stamps;
-#endif
     hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(1024), 0, st, yq, qd, lconst, gconst, T, Tp, L, Lp, Kp,
                        nLTp, ntile, delta, rblk, ll64, stamps);
     PMG_LAUNCH_CHECK();
-#ifdef PMG_EM_STAMPS
-    {
-      std::vector<unsigned long long> h((size_t)nwg * 512);
-      PMG_HIP(hipStreamSynchronize(st));
-      PMG_HIP(hipMemcpy(h.data(), dst_stamps, h.size() * 8, hipMemcpyDeviceToHost));
-      const int nchh = Kp / PK;
-      for (int w = 0; w < 2; ++w) {
-        double wb[2] = {0, 0}, is[2] = {0, 0}, cm[2] = {0, 0}, per[2] = {0, 0};
-        int cnt[2] = {0, 0};
-        for (int b = 0; b < nwg; ++b)
-          for (int x = 1; x < 63; ++x) {
-            const unsigned long long* q = &h[(size_t)b * 512 + w * 256 + x * 4];
-            if (!q[0] || !q[3] || !q[4]) continue;
-            const int e = (x % nchh) == nchh - 1;
-            wb[e] += q[1] - q[0];
-            is[e] += q[2] - q[1];
-            cm[e] += q[3] - q[2];
-            per[e] += q[4] - q[0];
-            ++cnt[e];
-          }
-        for (int e = 0; e < 2; ++e)
-          if (cnt[e])
-            fprintf(stderr, "[em-stamps] wave %d %s chunks: n=%d wait+barrier %.0f issue %.0f compute%s %.0f period %.0f (s_memtime ticks)\n",
-                    w ? 7 : 0, e ? "tile-last" : "inner", cnt[e], wb[e] / cnt[e], is[e] / cnt[e], e ? "+epilogue" : "",
-                    cm[e] / cnt[e], per[e] / cnt[e]);
-      }
-      const unsigned long long* q0 = &h[0];
-      fprintf(stderr, "[em-stamps] wg0 wave0 first stamps:");
-      for (int x = 0; x < 12; ++x) fprintf(stderr, " %lld", (long long)(q0[x * 4] - q0[0]));
-      fprintf(stderr, "\n");
-    }
-#endif
     return PMG_OK;
   }
   const int nLT = (Lp + EL - 1) / EL;

@@ -123,6 +123,8 @@ struct FBParams {
   const float* alpha_in;  // only the d = 0 rows are read
   float* w_first;         // per chunk: alpha at its first step, (2, Lpad) (boundary weights)
   float* P;
+  uint16_t* Pq;         // PMG_PHASE_P_BF16X3: P as bf16 planes hi / mid / lo, plane k at Pq + k pq_stride
+  int64_t pq_stride;    // T ldd
   float* gamma;
   float* rho;
   float* b_in;
@@ -154,6 +156,7 @@ __device__ __forceinline__ FBParams batch_view(const FBParams& p0) {
   const int64_t seq = (int64_t)r * p.T;
   p.delta += (int64_t)r * p.L;
   if (p.P) p.P += (int64_t)r * p.L;
+  if (p.Pq) p.Pq += (int64_t)r * p.L;
   p.phi += (int64_t)r * p.nblk;
   p.m += r;
   if (p.alpha) p.alpha += seq * 2 * p.L;
@@ -529,6 +532,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base, uint
 }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 template <int J, bool VEC>
 __device__ __forceinline__ void bload_row(const float* row, int L, int j0, float v[J]) {
@@ -571,6 +575,43 @@ __device__ __forceinline__ void bstore_row_n(float* row, uint32_t bytes, int j0,
 template <int J, bool VEC>
 __device__ __forceinline__ void bstore_row(float* row, int L, int j0, const float v[J]) {
   bstore_row_n<J, VEC>(row, (uint32_t)L * 4u, j0, v);
+}
+
+// row t of P as three bf16 planes (PMG_PHASE_P_BF16X3): the exact split of each value
+// (split3_pair), the lane's J values as J / 2 dwords per plane
+template <int J, bool VEC>
+__device__ __forceinline__ void bstore_planes(const FBParams& p, int64_t t, int j0, const float v[J]) {
+  const uint32_t bytes = (uint32_t)p.L * 2u;
+  if constexpr (VEC) {   // J % 4 == 0, L % 4 == 0: 8-byte aligned runs
+    uint32_t w[3][J / 2];
+#pragma unroll
+    for (int i = 0; i < J / 2; ++i) split3_pair(v[2 * i], v[2 * i + 1], w[0][i], w[1][i], w[2][i]);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const __amdgpu_buffer_rsrc_t rs = rsrc_of(p.Pq + k * p.pq_stride + t * p.ldd, bytes);
+      if constexpr (J == 4) {
+        const u32x2 q = {w[k][0], w[k][1]};
+        __builtin_amdgcn_raw_buffer_store_b64(q, rs, j0 * 2, 0, 0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < J / 2; i += 4) {
+          const u32x4 q = {w[k][i], w[k][i + 1], w[k][i + 2], w[k][i + 3]};
+          __builtin_amdgcn_raw_buffer_store_b128(q, rs, (j0 + 2 * i) * 2, 0, 0);
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      uint32_t hw, mw, lw;
+      split3_pair(v[j], 0.f, hw, mw, lw);
+      const uint32_t w3[3] = {hw, mw, lw};
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(w3[k] & 0xFFFFu),
+                                             rsrc_of(p.Pq + k * p.pq_stride + t * p.ldd, bytes), (j0 + j) * 2, 0, 0);
+    }
+  }
 }
 
 // two f32 per step (x at 2t, y at 2t + 1) written by lane 0 only
@@ -1100,7 +1141,8 @@ __device__ __forceinline__ void bwd_stream_out(const FBParams& p, Bwd<J, WP>& st
     if constexpr (MODE == 0) {
 #pragma unroll
       for (int j = 0; j < J; ++j) pp[j] *= iG;
-      bstore_row<J, VEC>(p.P + t * p.ldd, p.L, j0, pp);
+      if (p.Pq) bstore_planes<J, VEC>(p, t, j0, pp);
+      else bstore_row<J, VEC>(p.P + t * p.ldd, p.L, j0, pp);
     } else {
 #pragma unroll
       for (int j = 0; j < J; ++j) {
@@ -1109,6 +1151,7 @@ __device__ __forceinline__ void bwd_stream_out(const FBParams& p, Bwd<J, WP>& st
         pp[j] = a0[j] + a1[j];
       }
       if (p.P) bstore_row<J, VEC>(p.P + t * p.ldd, p.L, j0, pp);
+      if (p.Pq) bstore_planes<J, VEC>(p, t, j0, pp);
       if (p.gamma) {
         bstore_row<J, VEC>(p.gamma + t * 2 * L, p.L, j0, a0);
         bstore_row<J, VEC>(p.gamma + t * 2 * L + L, p.L, j0, a1);

@@ -323,8 +323,8 @@ int pmg_forward_filter_phase(const float* delta, const float* phi, const double*
                              const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                              int32_t warmup, double tol, float* alpha, double* logc, double* logz,
                              void* workspace, size_t workspace_bytes, void* stream, int32_t phase) {
-  PMG_REQUIRE((phase & 3) != 0 && (phase & ~PMG_PHASE_FLAG_BITS) == 0, "pmg_forward_filter_phase: phase %d",
-              phase);
+  PMG_REQUIRE((phase & 3) != 0 && (phase & ~(PMG_PHASE_FLAG_BITS & ~PMG_PHASE_P_BF16X3)) == 0,
+              "pmg_forward_filter_phase: phase %d", phase);
   return forward_impl(delta, phi, m, T, tr, likelihood_scale, chunk, warmup, tol, alpha, logc, logz,
                       workspace, workspace_bytes, stream, phase);
 }
@@ -347,7 +347,12 @@ static int backward_impl(const float* delta, const float* phi, const float* alph
   p.alpha_in = alpha;
   p.jsc = w.jsc;
   p.w_first = w.w_first;
-  p.P = P;
+  if (phase & PMG_PHASE_P_BF16X3) {   // P is the bf16 planes [3][T][ldd]
+    p.Pq = reinterpret_cast<uint16_t*>(P);
+    p.P = nullptr;
+  } else {
+    p.P = P;
+  }
   p.gamma = gamma;
   p.rho = rho;
   p.adapt = (phase & PMG_PHASE_ADAPTIVE_WARMUP) ? 1 : 0;
@@ -362,6 +367,7 @@ static int backward_impl(const float* delta, const float* phi, const float* alph
   rc = batch_params(p, R, T, chunk, workspace_bytes, &slab);
   if (rc) return rc;
   requested_segments(p, phase, R);
+  p.pq_stride = T * (int64_t)p.ldd;
   const int J = p.Lpad / 64, WP = pick_WP(tr->band);
   FBKernelSet ks;
   const bool have = fb_set(J, WP, &ks);
@@ -410,7 +416,7 @@ int pmg_forward_filter_batched(const float* delta, const float* phi, const doubl
                                const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                                int32_t warmup, double tol, float* alpha, double* logc, double* logz,
                                void* workspace, size_t workspace_bytes, void* stream, int32_t phase) {
-  PMG_REQUIRE((phase & 3) != 0 && (phase & ~PMG_PHASE_FLAG_BITS) == 0,
+  PMG_REQUIRE((phase & 3) != 0 && (phase & ~(PMG_PHASE_FLAG_BITS & ~PMG_PHASE_P_BF16X3)) == 0,
               "pmg_forward_filter_batched: phase %d", phase);
   return forward_impl(delta, phi, m, T, tr, likelihood_scale, chunk, warmup, tol, alpha, logc, logz,
                       workspace, workspace_bytes, stream, phase, R);

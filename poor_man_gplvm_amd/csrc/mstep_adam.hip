@@ -314,7 +314,9 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
   constexpr int QS = 16 * BCP;                                         // padded columns per neuron
   __shared__ __attribute__((aligned(16))) double sW[kSMax * QS];       // W_k (f64), [s][qb][BCP]
   __shared__ __attribute__((aligned(16))) float sD[kSMax * QS];        // W_k - W_{k-1}
-  __shared__ __attribute__((aligned(16))) float sG[32 * A * SP];       // G of every row, [l][s]
+  // G of every row, row pairs interleaved per neuron: [l/2][s][l&1], so one b64 / b128 read
+  // of a pair is the (even row, odd row) operand of the packed FMAs with no register moves
+  __shared__ __attribute__((aligned(16))) float sG[32 * A * SP];
   __shared__ float sPart[kNW * SP * 16 * BC];                          // per-wave B^T G, [w][s][q]
   __shared__ double sSum[2 * kNW];
   __shared__ int sCtl[4];
@@ -470,7 +472,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
       const float sg = 1.f / (1.f + expf(-Fh));
       const double fd = (double)f32 + (double)sg * r;
       const float gv = live ? (float)((ywd * rcp_nr(fd + 1e-20) - twd) * (double)sg) : 0.f;
-      if (owner) sG[(lb * A + slot) * SP + s] = gv;
+      if (owner) sG[((lb * A + slot) >> 1) * 2 * SP + 2 * s + (slot & 1)] = gv;
       const double xl = (ywd != 0.0) ? ywd * ((double)logf(f32 + 1e-20f) + (double)sg * r * rcp_nr((double)f32)) : 0.0;
 #else
       const SoftplusF32 sp = softplus_sigmoid(Fh);
@@ -478,7 +480,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
       const double fd = (double)f32 + (double)sg * r;
       const double ifd = rcp_nr(fd + 1e-20);
       const float gv = live ? (float)((ywd * ifd - twd) * (double)sg) : 0.f;
-      if (owner) sG[(lb * A + slot) * SP + s] = gv;
+      if (owner) sG[((lb * A + slot) >> 1) * 2 * SP + 2 * s + (slot & 1)] = gv;
       // log f = log f32 + sigmoid r / f to first order (the f64 reciprocal of fd: the
       // difference from 1 / f32 is second order in r)
       const double xl = (ywd != 0.0) ? ywd * ((double)log_f32(f32 + 1e-20f) + (double)sg * r * ifd) : 0.0;
@@ -497,22 +499,9 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
 #pragma unroll
     for (int i = 0; i < A / 2; ++i) {
       f2v gl[SP];                                      // (G[2i][s], G[2i+1][s])
-      const float* src = &sG[(lb * A + 2 * i) * SP];
-      if constexpr (SP == 1) {
-        const float2 v = *reinterpret_cast<const float2*>(src);
-        gl[0] = (f2v){v.x, v.y};
-      } else if constexpr (SP == 2) {
-        const float4 v = *reinterpret_cast<const float4*>(src);
-        gl[0] = (f2v){v.x, v.z};
-        gl[1] = (f2v){v.y, v.w};
-      } else {
-        const float4 v0 = *reinterpret_cast<const float4*>(src);
-        const float4 v1 = *reinterpret_cast<const float4*>(src + 4);
-        gl[0] = (f2v){v0.x, v1.x};
-        gl[1] = (f2v){v0.y, v1.y};
-        gl[2] = (f2v){v0.z, v1.z};
-        gl[3] = (f2v){v0.w, v1.w};
-      }
+      const float* src = &sG[(lb * A / 2 + i) * 2 * SP];
+#pragma unroll
+      for (int s = 0; s < SP; ++s) gl[s] = *reinterpret_cast<const f2v*>(src + 2 * s);
 #pragma unroll
       for (int s = 0; s < SP; ++s)
 #pragma unroll

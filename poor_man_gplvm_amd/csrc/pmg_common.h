@@ -211,6 +211,23 @@ __device__ __forceinline__ float half_max32(float v) {
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
+// Exact 3-way bf16 split of a pair of f32 values, packed two per dword (value a in the
+// low half): hi = the top 16 bits, mid / lo = those of the successive remainders (each
+// remainder is exact in f32).  3 byte-permutes + 8 ALU ops per pair.
+__device__ __forceinline__ void split3_pair(float a, float b, uint32_t& hw, uint32_t& mw, uint32_t& lw) {
+  const uint32_t ua = __float_as_uint(a), ub = __float_as_uint(b);
+  hw = __builtin_amdgcn_perm(ub, ua, 0x07060302u);
+  const float ra = a - __uint_as_float(ua & 0xFFFF0000u), rb = b - __uint_as_float(ub & 0xFFFF0000u);
+  const uint32_t va = __float_as_uint(ra), vb = __float_as_uint(rb);
+  mw = __builtin_amdgcn_perm(vb, va, 0x07060302u);
+  const float sa = ra - __uint_as_float(va & 0xFFFF0000u), sb = rb - __uint_as_float(vb & 0xFFFF0000u);
+  lw = __builtin_amdgcn_perm(__float_as_uint(sb), __float_as_uint(sa), 0x07060302u);
+}
+
+// the f32 value of the bf16 halves of a dword (low half: element 2i, high half: 2i + 1)
+__device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
+
 // f64 DPP: both 32-bit halves moved by the same DPP control
 template <int CTRL, int ROWMASK = 0xf, int BANKMASK = 0xf>
 __device__ __forceinline__ double dppd(double v) {

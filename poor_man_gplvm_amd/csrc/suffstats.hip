@@ -226,18 +226,6 @@ static int atb_run(const float* A, int64_t lda, int Mdim, const float* B, int64_
 typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
 constexpr int KB3 = 64, ROW3 = KB3 + 8;
 
-// Exact 3-way bf16 split of a pair of f32 values, packed two per dword (value a in the
-// low half): hi = the top 16 bits, mid / lo = those of the successive remainders (each
-// remainder is exact in f32).  3 byte-permutes + 8 ALU ops per pair.
-__device__ __forceinline__ void split3_pair(float a, float b, uint32_t& hw, uint32_t& mw, uint32_t& lw) {
-  const uint32_t ua = __float_as_uint(a), ub = __float_as_uint(b);
-  hw = __builtin_amdgcn_perm(ub, ua, 0x07060302u);
-  const float ra = a - __uint_as_float(ua & 0xFFFF0000u), rb = b - __uint_as_float(ub & 0xFFFF0000u);
-  const uint32_t va = __float_as_uint(ra), vb = __float_as_uint(rb);
-  mw = __builtin_amdgcn_perm(vb, va, 0x07060302u);
-  const float sa = ra - __uint_as_float(va & 0xFFFF0000u), sb = rb - __uint_as_float(vb & 0xFFFF0000u);
-  lw = __builtin_amdgcn_perm(__float_as_uint(sb), __float_as_uint(sa), 0x07060302u);
-}
 
 // bijective XCD-grouping of workgroup ids (consecutive logical ids share an XCD)
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
@@ -397,6 +385,192 @@ __global__ void __launch_bounds__(512) k_ptb3(const float* __restrict__ P, int L
 #undef PMG_SS_TILE
 }
 
+// ---------------------------------------------------------------------------------
+// The same statistics from P already split into its three bf16 planes by the backward
+// smoother (PMG_PHASE_P_BF16X3, [3][T][ldp] uint16): no split here, so the kernel is the
+// three exact-product bf16 MFMA GEMMs plus their operand staging.
+//   A planes: each K-tile (64 time rows x 128 latents x 3 planes, 48 KiB) is staged
+//     row-major (one 16-byte chunk = 8 latents of one time row per load / ds_write_b128)
+//     into 256-byte LDS rows with the XOR swizzle ch ^ ((row & 3) << 2 | (row >> 2) & 3)
+//     (cdna_hip_programming.md T10 image (b)), and read back with ds_read_b64_tr_b16, which
+//     hands every lane 4 consecutive TIME steps of one latent: two reads are the 8 time
+//     steps lane (r, h) of the 32x32x16 MFMA A operand holds.
+//   B (spikes): time-contiguous bf16 [Np][Tp] as in k_ptb3.
+//   t_w: the workgroup of neuron tile nt sums P = (hi + mid) + lo (exact in f32) of the
+//     K-tiles with index % nNT == nt, so the four neuron tiles of a latent tile share the
+//     work; f32 within a kFlush segment, then f64.
+// ---------------------------------------------------------------------------------
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t img_off(int row, int ch) {
+  return 256u * row + 16u * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+__global__ void __launch_bounds__(512) k_ptb3q(const uint16_t* __restrict__ Pq, int64_t pq_stride, int ldp,
+                                               int L, const uint16_t* __restrict__ Ybt, int64_t Tp, int Np,
+                                               int64_t K, int64_t KT, int nMT, int nNT, int nKS, int Mp,
+                                               int Npd, double* __restrict__ part, double* __restrict__ twpart) {
+  // 2 x 3 x 64 x 256 B (A planes) + 2 x 128 x 72 x 2 B (B) = 135168 B
+  __shared__ __attribute__((aligned(16))) uint8_t sA[2][3][KB3 * 256];
+  __shared__ __attribute__((aligned(16))) uint16_t sB[2][TN][ROW3];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = lb % nMT;
+  const int nt = (lb / nMT) % nNT;
+  const int ks = lb / (nMT * nNT);
+  const int wm = wid & 3, wn = wid >> 2;       // wave tile: 32 m x 64 n
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t kb = (int64_t)ks * KT;
+  const int64_t ke = kb + KT < K ? kb + KT : K;
+
+  // A staging: chunk ch (latents mt*128 + 8 ch ..) of time rows rw and rw + 32
+  const int ch = tid & 15, rw = tid >> 4;
+  const int col = mt * TM + 8 * ch;
+  const bool col_ok = col + 8 <= ldp;          // chunks past the row feed only dropped outputs
+  const uint32_t voffA = col_ok ? (uint32_t)(rw * ldp + col) * 2u : 0x80000000u;
+  const uint32_t half_off = (uint32_t)(32 * ldp) * 2u;
+  // B staging (as k_ptb3)
+  const int n_l = tid >> 2, hq = tid & 3;
+  const int ng = nt * TN + n_l;
+  const uint16_t* yrow = Ybt + (size_t)(ng < Np ? ng : Np - 1) * Tp + 16 * hq;
+  u32x4 qa[3][2];
+  uint4 rb0, rb1;
+  auto load = [&](int64_t t0) {
+    const int64_t nrow = ke - t0 < 0 ? 0 : (ke - t0 > KB3 ? KB3 : ke - t0);
+    const int64_t tbase = t0 < K ? t0 : 0;
+#pragma unroll
+    for (int sp = 0; sp < 3; ++sp) {
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<uint16_t*>(Pq + sp * pq_stride + tbase * (int64_t)ldp), (short)0, (int)(nrow * ldp * 2),
+          0x00020000);
+      qa[sp][0] = __builtin_amdgcn_raw_buffer_load_b128(rs, voffA, 0, 0);
+      qa[sp][1] = __builtin_amdgcn_raw_buffer_load_b128(rs, voffA, col_ok ? half_off : 0u, 0);
+    }
+    const int64_t tb = t0 < Tp - KB3 ? t0 : Tp - KB3;
+    rb0 = *reinterpret_cast<const uint4*>(yrow + tb);
+    rb1 = *reinterpret_cast<const uint4*>(yrow + tb + 8);
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int sp = 0; sp < 3; ++sp) {
+      *reinterpret_cast<u32x4*>(&sA[buf][sp][img_off(rw, ch)]) = qa[sp][0];
+      *reinterpret_cast<u32x4*>(&sA[buf][sp][img_off(rw + 32, ch)]) = qa[sp][1];
+    }
+    *reinterpret_cast<uint4*>(&sB[buf][n_l][16 * hq]) = rb0;
+    *reinterpret_cast<uint4*>(&sB[buf][n_l][16 * hq + 8]) = rb1;
+  };
+  // t_w of this thread's 8 latents over its two staged rows
+  float tacc[8];
+  double tsum[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) tacc[j] = 0.f, tsum[j] = 0.0;
+  auto tw_add = [&]() {
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t a = qa[0][hh][i], b = qa[1][hh][i], c = qa[2][hh][i];
+        tacc[2 * i] += (bf16_lo(a) + bf16_lo(b)) + bf16_lo(c);
+        tacc[2 * i + 1] += (bf16_hi(a) + bf16_hi(b)) + bf16_hi(c);
+      }
+  };
+  auto tw_flush = [&]() {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      tsum[j] += (double)tacc[j];
+      tacc[j] = 0.f;
+    }
+  };
+
+  double acc64[2][16];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc64[q][i] = 0.0;
+  v16f c0 = {0}, c1 = {0};
+  const int bn0 = wn * 64 + r, bn1 = bn0 + 32;
+  // transposed-read addresses of the A operand: lane 4q + p of 16-lane group g reads row
+  // (kk + 8 (g >> 1) + q [+ 4]), latents wm*32 + 16 (g & 1) + 4p .. + 3
+  const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  const int ach = wm * 4 + 2 * (g & 1) + (pp >> 1);
+  const uint32_t abyte = 8u * (pp & 1);
+  auto mfma_k = [&](int buf, int kk) {
+    const v8bf b0 = *reinterpret_cast<const v8bf*>(&sB[buf][bn0][kk + 8 * h]);
+    const v8bf b1 = *reinterpret_cast<const v8bf*>(&sB[buf][bn1][kk + 8 * h]);
+    const int row0 = kk + 8 * (g >> 1) + qq;
+#pragma unroll
+    for (int sp = 0; sp < 3; ++sp) {
+      const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(&sA[buf][sp][img_off(row0, ach) + abyte]));
+      const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(&sA[buf][sp][img_off(row0 + 4, ach) + abyte]));
+      const v8bf a = __builtin_bit_cast(v8bf, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b0, c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b1, c1, 0, 0, 0);
+    }
+  };
+
+  int64_t tile = kb / KB3;                       // global K-tile index (t_w ownership)
+  if (kb < ke) {
+    load(kb);
+    store(0);
+    if (tile % nNT == nt) tw_add();
+    load(kb + KB3);
+    __syncthreads();
+    int cur = 0;
+    for (int64_t t0 = kb; t0 < ke; t0 += KB3, ++tile) {
+      mfma_k(cur, 0);
+      mfma_k(cur, 16);
+      store(cur ^ 1);                            // tile t0 + KB3 (loaded a tile ago)
+      if (t0 + KB3 < ke && (tile + 1) % nNT == nt) tw_add();
+      load(t0 + 2 * KB3);
+      mfma_k(cur, 32);
+      mfma_k(cur, 48);
+      __syncthreads();
+      cur ^= 1;
+      if (((t0 - kb) / KB3) & 1) {              // every 2 K-tiles: one kFlush segment
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          acc64[0][i] += (double)c0[i];
+          acc64[1][i] += (double)c1[i];
+          c0[i] = c1[i] = 0.f;
+        }
+        tw_flush();
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      acc64[0][i] += (double)c0[i];
+      acc64[1][i] += (double)c1[i];
+    }
+    tw_flush();
+  }
+  double* pq = part + (size_t)ks * Mp * Npd;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int oc = nt * TN + wn * 64 + q * 32 + r;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = mt * TM + wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+      pq[(size_t)row * Npd + oc] = acc64[q][i];
+    }
+  }
+  // t_w: the 32 row-threads of each chunk summed in row order, one partial per (ks, nt);
+  // the A buffers are free (the loop ended on a barrier)
+  double(*sTw)[TM / 8][8] = reinterpret_cast<double(*)[TM / 8][8]>(&sA[0][0][0]);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sTw[rw][ch][j] = tsum[j];
+  __syncthreads();
+  if (tid < TM) {
+    const int c8 = tid >> 3, j = tid & 7;
+    double t = 0.0;
+    for (int q = 0; q < 32; ++q) t += sTw[q][c8][j];
+    twpart[((size_t)ks * nNT + nt) * Mp + mt * TM + tid] = t;
+  }
+}
+
 // t_w[m] = sum over the 4 nKS partial rows, in one fixed order: block = 64 latents x
 // 16 k-groups (group g sums rows k = g, g + 16, ... in k order, coalesced over m), then
 // the 16 group sums in g order through LDS.  (One thread per latent summing every row
@@ -410,6 +584,25 @@ __global__ void __launch_bounds__(kTwM * kTwG) k_tw_reduce(const double* __restr
   double s = 0.0;
   if (m < L)
     for (int k = g; k < 4 * nKS; k += kTwG) s += twpart[(size_t)k * Mp + m];
+  sp[g][mi] = s;
+  __syncthreads();
+  if (g == 0 && m < L) {
+    double t = 0.0;
+#pragma unroll
+    for (int q = 0; q < kTwG; ++q) t += sp[q][mi];
+    tw[m] = t;
+  }
+}
+
+// the same over `rows` partial rows (k_ptb3q: nKS x nNT)
+__global__ void __launch_bounds__(kTwM * kTwG) k_tw_reduce_n(const double* __restrict__ twpart, int rows, int Mp,
+                                                             int L, double* __restrict__ tw) {
+  __shared__ double sp[kTwG][kTwM];
+  const int mi = threadIdx.x % kTwM, g = threadIdx.x / kTwM;
+  const int m = blockIdx.x * kTwM + mi;
+  double s = 0.0;
+  if (m < L)
+    for (int k = g; k < rows; k += kTwG) s += twpart[(size_t)k * Mp + m];
   sp[g][mi] = s;
   __syncthreads();
   if (g == 0 && m < L) {
@@ -530,6 +723,45 @@ int pmg_suffstats_bf16(const float* P, const uint16_t* ybt, int64_t T, int64_t T
   PMG_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_tw_reduce, dim3((unsigned)((L + kTwM - 1) / kTwM)), dim3(kTwM * kTwG), 0, st,
                      (const double*)twpart, nKS, Mp, L, tw);
+  PMG_LAUNCH_CHECK();
+  return PMG_OK;
+}
+
+size_t pmg_suffstats_bf16x3_workspace_size(int64_t T, int32_t L, int32_t N) {
+  int nMT, nNT, nKS, Mp, Npd;
+  int64_t KT;
+  ptb3_geometry(T, L, N, nMT, nNT, nKS, KT, Mp, Npd);
+  return (size_t)nKS * Mp * Npd * sizeof(double) + (size_t)nKS * nNT * Mp * sizeof(double) + 256;
+}
+
+int pmg_suffstats_bf16x3(const uint16_t* Pq, int64_t ldp, const uint16_t* ybt, int64_t T, int64_t Tp, int32_t L,
+                         int32_t N, int32_t Np, double* yw, double* tw, void* workspace, size_t workspace_bytes,
+                         void* stream) {
+  PMG_REQUIRE(T > 0 && L > 0 && N > 0 && Np >= N + 1 && Np % 64 == 0 && Tp == round_up(T, KB3) && ldp >= L &&
+                  ldp % 8 == 0,
+              "pmg_suffstats_bf16x3: bad shape");
+  PMG_REQUIRE(Pq && ybt && yw && tw && workspace, "pmg_suffstats_bf16x3: null");
+  PMG_REQUIRE(workspace_bytes >= pmg_suffstats_bf16x3_workspace_size(T, L, N),
+              "pmg_suffstats_bf16x3: workspace too small");
+  PMG_REQUIRE(T * ldp * 2 < ((int64_t)1 << 31), "pmg_suffstats_bf16x3: planes of %lld elements exceed 2 GiB",
+              (long long)(T * ldp));
+  int nMT, nNT, nKS, Mp, Npd;
+  int64_t KT;
+  ptb3_geometry(T, L, N, nMT, nNT, nKS, KT, Mp, Npd);
+  double* part = reinterpret_cast<double*>(workspace);
+  double* twpart = part + (size_t)nKS * Mp * Npd;
+  hipStream_t st = as_stream(stream);
+  const int64_t wgs = (int64_t)nMT * nNT * nKS;
+  hipLaunchKernelGGL(k_ptb3q, dim3((unsigned)wgs), dim3(512), 0, st, Pq, T * ldp, (int)ldp, L, ybt, Tp, N, T, KT,
+                     nMT, nNT, nKS, Mp, Npd, part, twpart);
+  PMG_LAUNCH_CHECK();
+  const int64_t total = (int64_t)L * Npd;
+  hipLaunchKernelGGL(k_atb_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                     (const double*)part, nKS, Mp, Npd, L, N, N, yw, -1, (double*)nullptr);
+  PMG_LAUNCH_CHECK();
+  // the nKS x nNT partial rows, in the fixed order of k_tw_reduce (its 4 nKS rows: nNT = 4)
+  hipLaunchKernelGGL(k_tw_reduce_n, dim3((unsigned)((L + kTwM - 1) / kTwM)), dim3(kTwM * kTwG), 0, st,
+                     (const double*)twpart, nKS * nNT, Mp, L, tw);
   PMG_LAUNCH_CHECK();
   return PMG_OK;
 }

@@ -258,7 +258,12 @@ class DeviceEM:
         self.mref = torch.empty(T, dtype=f64, device=dev)
         self.alpha = torch.empty((T, 2, L), dtype=f32, device=dev)
         self.logc = torch.empty(T, dtype=f64, device=dev)
-        self.P = torch.empty((T, L), dtype=f32, device=dev)
+        self._P = torch.empty((T, L), dtype=f32, device=dev)
+        # integer spikes: the backward writes P as its three exact bf16 planes, the operands
+        # of the statistics GEMMs (PMG_PHASE_P_BF16X3), instead of f32 P
+        self.use_planes = bool(self.PLANES and spikes.ybt is not None and L % 8 == 0)
+        self.Pq = torch.empty((3, T, L), dtype=torch.int16, device=dev) if self.use_planes else None
+        self._p_fresh = 'f32'       # which of _P / Pq holds the current posterior marginal
         self.tuning64 = torch.empty((L, N), dtype=f64, device=dev)
         self.tuning32 = torch.empty((L, N), dtype=f32, device=dev)
         self.yw = torch.empty((L, N), dtype=f64, device=dev)
@@ -269,7 +274,8 @@ class DeviceEM:
         # zero-filled once (include/pmg.h): the scan kernels keep its control words zero
         self.ws_fb = torch.zeros(int(self.lib.pmg_fwdbwd_workspace_size(T, L, min(self.C, self.Cb))),
                                  dtype=torch.uint8, device=dev)
-        ss_bytes = (self.lib.pmg_suffstats_bf16_workspace_size(T, L, N) if spikes.ybt is not None
+        ss_bytes = (max(self.lib.pmg_suffstats_bf16_workspace_size(T, L, N),
+                        self.lib.pmg_suffstats_bf16x3_workspace_size(T, L, N)) if spikes.ybt is not None
                     else self.lib.pmg_suffstats_workspace_size(T, L, spikes.Np))
         self.ws_ss = torch.empty(int(ss_bytes), dtype=torch.uint8, device=dev)
         if self.ws_fb.numel() == 0:
@@ -298,6 +304,26 @@ class DeviceEM:
         self.gauss_prior_std = 1.0
         self._gstatus = None
         self._ws_gm = None
+
+    PLANES = True       # P as bf16 planes between the backward and the statistics (when possible)
+
+    @property
+    def P(self):
+        """(T, L) f32 posterior marginal sum_d gamma.  When the last backward wrote the bf16
+        planes, they are recombined here, exactly ((hi + mid) + lo in f32).  The buffer is
+        handed out for reading or writing, so the next M-step reads it, not the planes."""
+        if self._p_fresh == 'planes':
+            q = self.Pq.to(torch.int32) << 16
+            f = q.view(torch.float32)
+            torch.add(f[0], f[1], out=self._P)
+            self._P.add_(f[2])
+        self._p_fresh = 'f32'
+        return self._P
+
+    @P.setter
+    def P(self, v):
+        self._P = v
+        self._p_fresh = 'f32'
 
     def _t(self, name):
         return self.timer(name) if self.timer is not None else _NO_TIMER
@@ -377,14 +403,20 @@ class DeviceEM:
         lp = torch.as_tensor(np.ascontiguousarray(log_post, dtype=np.float32), device=self.dev)
         if tuple(lp.shape) != (self.T, self.L):
             raise ValueError(f"log_posterior must be {(self.T, self.L)}")
-        nat.check(self.lib.pmg_exp(nat.ptr(lp), lp.numel(), nat.ptr(self.P), nat.stream_handle()), "pmg_exp")
+        nat.check(self.lib.pmg_exp(nat.ptr(lp), lp.numel(), nat.ptr(self._P), nat.stream_handle()), "pmg_exp")
+        self._p_fresh = 'f32'
 
     # ------------------------------------------------------------------ M-step
     def m_step(self, W, mu, nu, count, cfg: AdamConfig, stats_out, lh_out, eh_out):
         """Sufficient statistics of self.P, then the Adam loop; W/mu/nu/count in place."""
         sh = nat.stream_handle()
         with self._t('suffstats'):
-          if self.sp.ybt is not None:
+          if self._p_fresh == 'planes':
+            nat.check(self.lib.pmg_suffstats_bf16x3(nat.ptr(self.Pq), self.L, nat.ptr(self.sp.ybt), self.T,
+                                                    self.sp.Tp, self.L, self.N, self.sp.Np, nat.ptr(self.yw),
+                                                    nat.ptr(self.tw), nat.ptr(self.ws_ss), self.ws_ss.numel(), sh),
+                      "pmg_suffstats_bf16x3")
+          elif self.sp.ybt is not None:
             nat.check(self.lib.pmg_suffstats_bf16(nat.ptr(self.P), nat.ptr(self.sp.ybt), self.T, self.sp.Tp,
                                                   self.L, self.N, self.sp.Np, nat.ptr(self.yw), nat.ptr(self.tw),
                                                   nat.ptr(self.ws_ss), self.ws_ss.numel(), sh),
@@ -688,17 +720,24 @@ class DeviceEM:
                     nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.ll64), nat.ptr(self.log_alpha), self.T,
                     ctypes.byref(self._tr_d),
                     float(likelihood_scale), self.Cd, int(self.warm[1]), float(self.scan.tol),
-                    nat.ptr(self.P) if P else None, nat.ptr(gamma), nat.ptr(log_gamma), None, nat.ptr(rho),
+                    nat.ptr(self._P) if P else None, nat.ptr(gamma), nat.ptr(log_gamma), None, nat.ptr(rho),
                     nat.ptr(self.ws_dense), self.ws_dense.numel(), nat.stream_handle()), "pmg_dense_backward")
+            if P:
+                self._p_fresh = 'f32'
             return
         if log_gamma is not None:
             raise ValueError("log_gamma is produced by the dense scans only")
         sc = self.scan
+        planes = bool(P) and self.use_planes
+        pout = (nat.ptr(self.Pq) if planes else nat.ptr(self._P)) if P else None
         args = (nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.alpha), self.T, ctypes.byref(self._tr_c),
                 float(likelihood_scale), self.Cb, int(self.warm[1]), float(sc.tol),
-                nat.ptr(self.P) if P else None, nat.ptr(gamma), nat.ptr(rho), nat.ptr(self.ws_fb),
+                pout, nat.ptr(gamma), nat.ptr(rho), nat.ptr(self.ws_fb),
                 self.ws_fb.numel(), nat.stream_handle())
-        ad = nat.PHASE_ADAPTIVE_WARMUP if (sc.device_adaptive and self.adaptive) else 0
+        ad = (nat.PHASE_ADAPTIVE_WARMUP if (sc.device_adaptive and self.adaptive) else 0) | \
+            (nat.PHASE_P_BF16X3 if planes else 0)
+        if P:
+            self._p_fresh = 'planes' if planes else 'f32'
         with self._t('backward_smoother'):       # main chunk-parallel pass (k_backward)
             nat.check(self.lib.pmg_backward_smoother_phase(*args, 1 | ad), "pmg_backward_smoother")
         with self._t('backward_repair'):         # verify / relaxation

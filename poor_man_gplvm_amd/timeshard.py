@@ -336,6 +336,8 @@ class ShardEM(DeviceEM):
     """DeviceEM over one shard's extended range, with own-range statistics and the
     boundary-state views the carry rounds exchange."""
 
+    PLANES = False      # the shard's statistics run over its own rows of the f32 P
+
     def __init__(self, lay: ShardLayout, y, L, basis, scan: ScanConfig, ma_neuron=None, device=None):
         self.lay = lay
         y_ext = np.asarray(y[lay.ext_start:lay.ext_stop])

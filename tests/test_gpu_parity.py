@@ -156,6 +156,45 @@ def test_forward_backward_vs_oracle(case):
         np.testing.assert_allclose(J, np.exp(lj), rtol=1e-5, atol=1e-5 * max(1.0, np.exp(lj).max()))
 
 
+@pytest.mark.parametrize("L,chunk,warm", [(64, None, 64), (128, 16, 0), (256, None, 48), (512, 16, 0),
+                                          (1024, 32, 8), (200, None, 48)])
+def test_backward_planes_bit_identical(L, chunk, warm):
+    """PMG_PHASE_P_BF16X3: the backward's bf16 planes recombine to the f32 P it writes
+    otherwise, bit for bit, for every lane width (J = 1 .. 16 latents per lane; J < 4 takes
+    the per-element stores) and through the relaxation (chunk 16, no warm-up: every
+    boundary repaired, MODE 1 writes the planes); and the statistics on them equal the
+    statistics on f32 P (y_w bit for bit)."""
+    N, T = 48, 2500
+    d = make(N, L, T)
+    sp, eng = _engine(d, L, chunk=chunk, warmup=warm)
+    assert eng.use_planes == (L % 8 == 0)
+    eng.set_tuning(d['tuning'])
+    logz = torch.zeros(1, dtype=torch.float64, device='cuda')
+    eng.e_step(1.0, logz)
+    fresh = eng._p_fresh
+    eng.emission_status()
+    from poor_man_gplvm_amd.engine import AdamConfig
+    stats = torch.zeros(4, dtype=torch.float64, device='cuda')
+    W = torch.zeros((eng.NB, N), dtype=torch.float64, device='cuda')
+    lh = torch.zeros(1, dtype=torch.float64, device='cuda')
+    eng.m_step(W, W.clone(), W.clone(), torch.zeros(1, dtype=torch.int64, device='cuda'), AdamConfig(maxiter=1),
+               stats, lh, lh.clone())
+    yw_a, tw_a = eng.yw.cpu().numpy().copy(), eng.tw.cpu().numpy().copy()
+    Pa = eng.P.cpu().numpy().copy()
+    eng.use_planes = False
+    eng.e_step(1.0, logz)
+    Pb = eng.P.cpu().numpy()
+    if L % 8 == 0:
+        assert fresh == 'planes'
+        f, b = eng.repairs()
+        assert chunk != 16 or (f > 0 and b > 0)
+    np.testing.assert_array_equal(Pa, Pb)
+    eng.m_step(W, W.clone(), W.clone(), torch.zeros(1, dtype=torch.int64, device='cuda'), AdamConfig(maxiter=1),
+               stats, lh, lh.clone())
+    np.testing.assert_array_equal(eng.yw.cpu().numpy(), yw_a)
+    np.testing.assert_allclose(eng.tw.cpu().numpy(), tw_a, rtol=1e-12)
+
+
 def test_flat_tuning_cascade():
     """Nearly flat tuning (the first EM iteration after a random init): the chain
     forgets slowly, every chunk boundary fails and the relaxation kernel recomputes
@@ -253,11 +292,30 @@ def test_masked_latents_scan():
 
 
 # ----------------------------------------------------------------------------- M-step
-@pytest.mark.parametrize("path", ["f32", "bf16x3"])
-@pytest.mark.parametrize("N,L,T", [(70, 100, 3000), (5, 37, 65), (130, 300, 1), (512, 512, 20000)])
+def split_planes(P):
+    """The exact bf16 split of f32 P the backward writes (PMG_PHASE_P_BF16X3): hi = the top
+    16 bits, mid / lo those of the successive f32 remainders; (3, T, L) int16."""
+    P = np.ascontiguousarray(P, np.float32)
+    out = []
+    r = P
+    for _ in range(3):
+        u = r.view(np.uint32)
+        out.append((u >> 16).astype(np.uint16))
+        r = (r - (u & np.uint32(0xFFFF0000)).view(np.float32)).astype(np.float32)
+    assert np.all(r == 0)
+    return np.stack(out).view(np.int16)
+
+
+@pytest.mark.parametrize("path", ["f32", "bf16x3", "planes"])
+@pytest.mark.parametrize("N,L,T", [(70, 100, 3000), (5, 37, 65), (130, 300, 1), (512, 512, 20000),
+                                   (64, 256, 5000), (200, 1024, 3001)])
 def test_suffstats_vs_numpy(path, N, L, T):
-    """y_w = P^T y, t_w = sum_t P (fit_tuning_helper.py:28-42) on both device paths:
-    the f32 MFMA kernel and the exact-product bf16 split (integer spikes)."""
+    """y_w = P^T y, t_w = sum_t P (fit_tuning_helper.py:28-42) on the three device paths:
+    the f32 MFMA kernel, the exact-product bf16 split of f32 P (k_ptb3), and the same
+    GEMMs on P's pre-split bf16 planes (k_ptb3q, PMG_PHASE_P_BF16X3; L % 8 == 0), whose
+    y_w must equal k_ptb3's bit for bit (the same products in the same order)."""
+    if path == "planes" and L % 8:
+        pytest.skip("planes need L % 8 == 0")
     d = make(N, L, T)
     sp, eng = _engine(d, L)
     assert sp.ybt is not None
@@ -273,6 +331,17 @@ def test_suffstats_vs_numpy(path, N, L, T):
         rc = eng.lib.pmg_suffstats_bf16(nat.ptr(eng.P), nat.ptr(sp.ybt), T, sp.Tp, L, N, sp.Np, nat.ptr(eng.yw),
                                         nat.ptr(eng.tw), nat.ptr(ws), ws.numel(), nat.stream_handle())
     nat.check(rc, "suffstats")
+    if path == "planes":
+        yw_split = eng.yw.cpu().numpy().copy()
+        Pq = torch.as_tensor(split_planes(P), device='cuda')
+        ws = torch.empty(int(eng.lib.pmg_suffstats_bf16x3_workspace_size(T, L, N)), dtype=torch.uint8,
+                         device='cuda')
+        eng.yw.zero_()
+        eng.tw.zero_()
+        nat.check(eng.lib.pmg_suffstats_bf16x3(nat.ptr(Pq), L, nat.ptr(sp.ybt), T, sp.Tp, L, N, sp.Np,
+                                               nat.ptr(eng.yw), nat.ptr(eng.tw), nat.ptr(ws), ws.numel(),
+                                               nat.stream_handle()), "suffstats_bf16x3")
+        np.testing.assert_array_equal(eng.yw.cpu().numpy(), yw_split)
     yw, tw = O.get_statistics(np.log(P.astype(np.float64)), d['y'])
     np.testing.assert_allclose(eng.yw.cpu().numpy(), yw, rtol=1e-6, atol=1e-9)
     np.testing.assert_allclose(eng.tw.cpu().numpy(), tw, rtol=1e-6)
