@@ -928,7 +928,13 @@ class RestartBatchEM:
         self.mref = torch.empty((T, R), dtype=f64, device=dev)
         self.alpha = torch.empty((R, T, 2, L), dtype=f32, device=dev)
         self.logc = torch.empty((R, T), dtype=f64, device=dev)
-        self.P = torch.empty((T, LA), dtype=f32, device=dev)
+        self._P = torch.empty((T, LA), dtype=f32, device=dev)
+        # as DeviceEM: P as its exact bf16 planes between the backward and the statistics
+        # (both the batched and the one-restart fit take the same statistics kernel, so a
+        # restart alone on the batch's grid reproduces its batched fit)
+        self.use_planes = bool(self.PLANES and spikes.ybt is not None)
+        self.Pq = torch.empty((3, T, LA), dtype=torch.int16, device=dev) if self.use_planes else None
+        self._p_fresh = 'f32'
         self.tuning64 = torch.empty((LA, N), dtype=f64, device=dev)
         self.tuning32 = torch.empty((LA, N), dtype=f32, device=dev)
         self.yw = torch.empty((LA, N), dtype=f64, device=dev)
@@ -940,7 +946,8 @@ class RestartBatchEM:
             raise nat.NativeError(f"n_latent_bin={L} unsupported by the scan kernels (max 1024)")
         self.ws_fb = torch.zeros(fb, dtype=torch.uint8, device=dev)    # zero-filled once (include/pmg.h)
         self.slab = (fb // R) & ~255 if R > 1 else fb
-        ss_bytes = (self.lib.pmg_suffstats_bf16_workspace_size(T, LA, N) if spikes.ybt is not None
+        ss_bytes = (max(self.lib.pmg_suffstats_bf16_workspace_size(T, LA, N),
+                        self.lib.pmg_suffstats_bf16x3_workspace_size(T, LA, N)) if spikes.ybt is not None
                     else self.lib.pmg_suffstats_workspace_size(T, LA, spikes.Np))
         self.ws_ss = torch.empty(int(ss_bytes), dtype=torch.uint8, device=dev)
         self.ws_ad = AdamWorkspace(self.lib, self.dev)
@@ -951,6 +958,8 @@ class RestartBatchEM:
 
     _t = DeviceEM._t
     _seg_bits = DeviceEM._seg_bits
+    PLANES = True
+    P = DeviceEM.P
 
     def set_transition(self, tr):
         if isinstance(tr, DenseTransition):
@@ -973,8 +982,9 @@ class RestartBatchEM:
         if tuple(lp.shape) != (self.R, self.T, self.L):
             raise ValueError(f"log_posteriors must be {(self.R, self.T, self.L)}")
         stacked = lp.permute(1, 0, 2).contiguous()       # (T, R, L) = the stacked layout
-        nat.check(self.lib.pmg_exp(nat.ptr(stacked), stacked.numel(), nat.ptr(self.P), nat.stream_handle()),
+        nat.check(self.lib.pmg_exp(nat.ptr(stacked), stacked.numel(), nat.ptr(self._P), nat.stream_handle()),
                   "pmg_exp")
+        self._p_fresh = 'f32'
 
     # ------------------------------------------------------------------ M-step
     def m_step(self, W, mu, nu, count, cfg: AdamConfig, stats_out, lh_out, eh_out):
@@ -982,7 +992,12 @@ class RestartBatchEM:
         sh = nat.stream_handle()
         T, LA, N = self.T, self.R * self.L, self.N
         with self._t('suffstats'):
-            if self.sp.ybt is not None:
+            if self._p_fresh == 'planes':
+                nat.check(self.lib.pmg_suffstats_bf16x3(nat.ptr(self.Pq), LA, nat.ptr(self.sp.ybt), T, self.sp.Tp,
+                                                        LA, N, self.sp.Np, nat.ptr(self.yw), nat.ptr(self.tw),
+                                                        nat.ptr(self.ws_ss), self.ws_ss.numel(), sh),
+                          "pmg_suffstats_bf16x3")
+            elif self.sp.ybt is not None:
                 nat.check(self.lib.pmg_suffstats_bf16(nat.ptr(self.P), nat.ptr(self.sp.ybt), T, self.sp.Tp, LA, N,
                                                       self.sp.Np, nat.ptr(self.yw), nat.ptr(self.tw),
                                                       nat.ptr(self.ws_ss), self.ws_ss.numel(), sh),
@@ -1064,10 +1079,13 @@ class RestartBatchEM:
 
     def backward(self, likelihood_scale, gamma=None):
         """gamma: optional (R, T, 2, L) f32 posterior output."""
+        planes = self.use_planes
         args = (nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.alpha), self.T, self.R,
                 ctypes.byref(self._tr_c), float(likelihood_scale), self.Cb, int(self.warm[1]), float(self.scan.tol),
-                nat.ptr(self.P), nat.ptr(gamma), nat.ptr(self.ws_fb), self.ws_fb.numel(), nat.stream_handle())
-        ad = nat.PHASE_ADAPTIVE_WARMUP if self.scan.device_adaptive else 0
+                nat.ptr(self.Pq) if planes else nat.ptr(self._P), nat.ptr(gamma), nat.ptr(self.ws_fb),
+                self.ws_fb.numel(), nat.stream_handle())
+        ad = (nat.PHASE_ADAPTIVE_WARMUP if self.scan.device_adaptive else 0) | (nat.PHASE_P_BF16X3 if planes else 0)
+        self._p_fresh = 'planes' if planes else 'f32'
         with self._t('backward_smoother'):
             nat.check(self.lib.pmg_backward_smoother_batched(*args, 1 | ad), "pmg_backward_smoother_batched")
         with self._t('backward_repair'):
