@@ -484,6 +484,13 @@ __global__ void __launch_bounds__(512) k_ptb3q(const uint16_t* __restrict__ Pq, 
       tacc[j] = 0.f;
     }
   };
+  // the staged K-tile of global index ti: its rows join t_w if this neuron tile owns it;
+  // f32 sums close at the end of every 2-tile (kFlush) segment of the GLOBAL tile grid, so
+  // the rounding does not depend on where the K-slices start (nor on the latent count)
+  auto tw_tile = [&](int64_t ti) {
+    if (ti % nNT == nt) tw_add();
+    if (ti & 1) tw_flush();
+  };
 
   double acc64[2][16];
 #pragma unroll
@@ -515,7 +522,7 @@ __global__ void __launch_bounds__(512) k_ptb3q(const uint16_t* __restrict__ Pq, 
   if (kb < ke) {
     load(kb);
     store(0);
-    if (tile % nNT == nt) tw_add();
+    tw_tile(tile);
     load(kb + KB3);
     __syncthreads();
     int cur = 0;
@@ -523,7 +530,7 @@ __global__ void __launch_bounds__(512) k_ptb3q(const uint16_t* __restrict__ Pq, 
       mfma_k(cur, 0);
       mfma_k(cur, 16);
       store(cur ^ 1);                            // tile t0 + KB3 (loaded a tile ago)
-      if (t0 + KB3 < ke && (tile + 1) % nNT == nt) tw_add();
+      if (t0 + KB3 < ke) tw_tile(tile + 1);
       load(t0 + 2 * KB3);
       mfma_k(cur, 32);
       mfma_k(cur, 48);
@@ -536,7 +543,6 @@ __global__ void __launch_bounds__(512) k_ptb3q(const uint16_t* __restrict__ Pq, 
           acc64[1][i] += (double)c1[i];
           c0[i] = c1[i] = 0.f;
         }
-        tw_flush();
       }
     }
 #pragma unroll
