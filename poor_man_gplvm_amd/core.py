@@ -190,7 +190,7 @@ class PoissonGPLVMJump1D:
     def _observation(self, eng, hyperparam):
         """Hook: the Gaussian model switches the engine's emission here."""
 
-    def _scan_transition(self, mv, pmj, pjm, logK=None, logA=None):
+    def _scan_transition(self, mv, pmj, pjm, logK=None, logA=None, exact=None):
         """Device transition for a decode scan: this model's own (hyper-parameters), or,
         when log kernels are passed (the _decode_latent arguments), the device form of
         exactly those kernels.  Kernels equal to the model's own (1e-6) keep its
@@ -198,7 +198,8 @@ class PoissonGPLVMJump1D:
         the dense log-domain scans with the whole kernel (exact joint rows for every
         latent, see ScanConfig.decode_exact)."""
         tr = self._transition(mv, pmj, pjm)
-        exact = bool(getattr(self.scan_config, 'decode_exact', False))
+        if exact is None:
+            exact = bool(getattr(self.scan_config, 'decode_exact', False))
         if exact and not isinstance(tr, DenseTransition):
             tr = dense_transition(self.n_latent_bin, mv, pmj, pjm, self.custom_transition_kernel)
         if logK is None or logA is None:
@@ -220,14 +221,15 @@ class PoissonGPLVMJump1D:
         eng = self._decode_engine(y, tuning, hyperparam, ma_neuron, ma_latent, logK, logA)
         return self._decode_on(eng, hyperparam, ma_latent, likelihood_scale, joint, logK, logA)
 
-    def _decode_engine(self, y, tuning, hyperparam, ma_neuron, ma_latent, logK=None, logA=None):
+    def _decode_engine(self, y, tuning, hyperparam, ma_neuron, ma_latent, logK=None, logA=None, exact=None):
         """Device state of a decode: spikes uploaded and prepared, transition, masks and
-        tuning set (reusable across decodes of spike trains of the same shape)."""
+        tuning set (reusable across decodes of spike trains of the same shape).  exact:
+        the dense log-domain scans (None: ScanConfig.decode_exact)."""
         mv = hyperparam.get('movement_variance', self.movement_variance)
         pmj = hyperparam.get('p_move_to_jump', self.p_move_to_jump)
         pjm = hyperparam.get('p_jump_to_move', self.p_jump_to_move)
         ma = None if ma_neuron is None else np.asarray(ma_neuron, np.float32)
-        tr = self._scan_transition(mv, pmj, pjm, logK, logA)
+        tr = self._scan_transition(mv, pmj, pjm, logK, logA, exact)
         self._check_latent_mask(tr, ma_latent)
         sp = SpikeData(y if isinstance(y, torch.Tensor) else np.asarray(y), ma)
         eng = DeviceEM(sp, self.n_latent_bin, scan=self.scan_config)
