@@ -351,6 +351,23 @@ int pmg_dense_backward(const float* delta, const float* phi, const double* ll64,
                        const pmg_dense_transition* tr, double likelihood_scale, int32_t chunk, int32_t warmup,
                        double tol, float* P, float* gamma, float* log_gamma, float* rho, double* log_rho,
                        void* workspace, size_t workspace_bytes, void* stream);
+/* Phase-split forms (time shards of one recording): phase 1 = the      */
+/* chunk-parallel main pass (it also zeroes the repair / round counters), 2 = boundary */
+/* verification + relaxation (+ logZ); a phase-2 call after a boundary slot was        */
+/* overwritten (pmg_dense_state: the neighbour shard's carry) re-verifies and repairs   */
+/* from there, adding its repairs to the counters.  pmg_dense_state returns the f64     */
+/* log state slot (2 x pmg_dense_lpad(L) values, [d][j]) of chunk c, `which` as        */
+/* pmg_fwdbwd_state; null on bad arguments.                                             */
+int32_t pmg_dense_lpad(int32_t L);
+double* pmg_dense_state(void* workspace, int64_t T, int32_t L, int32_t chunk, int32_t which, int64_t c);
+int pmg_dense_forward_phase(const float* delta, const float* phi, const double* ll64, const double* m, int64_t T,
+                            const pmg_dense_transition* tr, double likelihood_scale, int32_t chunk, int32_t warmup,
+                            double tol, float* alpha, double* log_alpha, double* logc, double* logz, void* workspace,
+                            size_t workspace_bytes, void* stream, int32_t phase);
+int pmg_dense_backward_phase(const float* delta, const float* phi, const double* ll64, const double* log_alpha,
+                             int64_t T, const pmg_dense_transition* tr, double likelihood_scale, int32_t chunk,
+                             int32_t warmup, double tol, float* P, float* gamma, float* log_gamma, float* rho,
+                             double* log_rho, void* workspace, size_t workspace_bytes, void* stream, int32_t phase);
 /* Pairwise joint in log space (decode, dense scans): logS (2L x 2L) f64 =           */
 /* LSE_{t<T-1} log_alpha_t[x] + log_rho_{t+1}[x'], x = (d,i) (f64 inputs, f64 online  */
 /* sum); the caller forms the log joint logA[d,d'] + logK[d',i,j] + logS               */

@@ -63,6 +63,7 @@ EXPORTED_SYMBOLS = (
     "pmg_mstep_batched_workspace_size", "pmg_mstep_adam_batched_supported", "pmg_mstep_adam_batched",
     "pmg_emission_range_flag", "pmg_mstep_adam_status",
     "pmg_suffstats_bf16x3_workspace_size", "pmg_suffstats_bf16x3",
+    "pmg_dense_lpad", "pmg_dense_state", "pmg_dense_forward_phase", "pmg_dense_backward_phase",
 )
 
 
@@ -155,6 +156,12 @@ _SIGS = {
     "pmg_dense_backward": ([_P, _P, _P, _P, _I64, ctypes.POINTER(DenseTransition), _D, _I32, _I32, _D,
                             _P, _P, _P, _P, _P, _P, _SZ, _P], _I32),
     "pmg_joint_log_accumulate": ([_P, _P, _I64, _I32, _P, _P], _I32),
+    "pmg_dense_lpad": ([_I32], _I32),
+    "pmg_dense_state": ([_P, _I64, _I32, _I32, _I32, _I64], _P),
+    "pmg_dense_forward_phase": ([_P, _P, _P, _P, _I64, ctypes.POINTER(DenseTransition), _D, _I32, _I32, _D,
+                                 _P, _P, _P, _P, _P, _SZ, _P, _I32], _I32),
+    "pmg_dense_backward_phase": ([_P, _P, _P, _P, _I64, ctypes.POINTER(DenseTransition), _D, _I32, _I32, _D,
+                                  _P, _P, _P, _P, _P, _P, _SZ, _P, _I32], _I32),
     "pmg_joint_accumulate": ([_P, _P, _I64, _I32, _P, _P, _SZ, _P], _I32),
     "pmg_tuning_softplus_batched": ([_P, _P, _I32, _I32, _I32, _I32, _P, _P, _P], _I32),
     "pmg_emission_range_flag": ([_P, _I64, _I32, _I32], _P),

@@ -1071,10 +1071,32 @@ size_t pmg_dense_workspace_size(int64_t T, int32_t L, int32_t chunk) {
   return total;
 }
 
-int pmg_dense_forward(const float* delta, const float* phi, const double* ll64, const double* m, int64_t T,
-                      const pmg_dense_transition* tr, double likelihood_scale, int32_t chunk, int32_t warmup,
-                      double tol, float* alpha, double* log_alpha, double* logc, double* logz, void* workspace,
-                      size_t workspace_bytes, void* stream) {
+int32_t pmg_dense_lpad(int32_t L) {
+  const int JD = dense_jd(L);
+  return JD < 0 ? 0 : kDNT * JD;
+}
+
+double* pmg_dense_state(void* workspace, int64_t T, int32_t L, int32_t chunk, int32_t which, int64_t c) {
+  const int JD = dense_jd(L);
+  if (!workspace || JD < 0 || chunk <= 0 || T <= 0) return nullptr;
+  const int64_t M = (T + chunk - 1) / chunk;
+  if (c < 0 || c >= M) return nullptr;
+  DenseWork w = carve_dense(workspace, T, kDNT * JD, chunk);
+  double* base = nullptr;
+  switch (which) {
+    case PMG_STATE_FWD_IN: base = w.s_in; break;
+    case PMG_STATE_FWD_OUT: base = w.s_out; break;
+    case PMG_STATE_BWD_IN: base = w.b_in; break;
+    case PMG_STATE_BWD_FIRST: base = w.b_first; break;
+    default: return nullptr;
+  }
+  return base + (size_t)c * 2 * (kDNT * JD);
+}
+
+static int dense_forward_impl(const float* delta, const float* phi, const double* ll64, const double* m, int64_t T,
+                              const pmg_dense_transition* tr, double likelihood_scale, int32_t chunk, int32_t warmup,
+                              double tol, float* alpha, double* log_alpha, double* logc, double* logz,
+                              void* workspace, size_t workspace_bytes, void* stream, int phase) {
   DenseParams p;
   int rc = dense_params(p, tr, T, chunk, warmup, likelihood_scale, tol);
   if (rc) return rc;
@@ -1099,24 +1121,47 @@ int pmg_dense_forward(const float* delta, const float* phi, const double* ll64, 
   p.seg_chg = w.seg_chg;
   dense_kernel_t kf, kfr, kb, kbr;
   dense_kernels(p.Lp / kDNT, &kf, &kfr, &kb, &kbr);
-  // per-call words; the timeout word (kDErr) is sticky until the host reads it
-  PMG_HIP(hipMemsetAsync(p.ctl, 0, kDErr * sizeof(int), st));
-  PMG_HIP(hipMemsetAsync(p.ctl + kDErr + 1, 0, (16 - kDErr - 1) * sizeof(int), st));
-  hipLaunchKernelGGL(kf, dim3(p.M), dim3(kDNT), 0, st, p);
-  PMG_LAUNCH_CHECK();
-  if (p.M > 1) {
-    hipLaunchKernelGGL(k_dense_verify, dim3((p.M - 1 + 3) / 4), dim3(256), 0, st, w.s_in, (const double*)w.s_out, 1,
-                       p.M - 1, -1, p.L, p.Lp, p.tol, w.flags, (const float*)nullptr, 0, p.ctl + kDPending);
+  // per-pass words: repair / round counters at the main pass (a later phase-2 call, the
+  // time-shard carry hand-off, adds its repairs to them), the relaxation protocol words
+  // before each relaxation; the timeout word (kDErr) is sticky until the host reads it
+  if (phase & 1) {
+    PMG_HIP(hipMemsetAsync(p.ctl, 0, kDErr * sizeof(int), st));
+    hipLaunchKernelGGL(kf, dim3(p.M), dim3(kDNT), 0, st, p);
     PMG_LAUNCH_CHECK();
   }
-  PMG_HIP(launch_persistent(kfr, dim3(p.S), dim3(kDNT), 0, st, p));
+  if (phase & 2) {
+    PMG_HIP(hipMemsetAsync(p.ctl + kDErr + 1, 0, (16 - kDErr - 1) * sizeof(int), st));
+    if (p.M > 1) {
+      hipLaunchKernelGGL(k_dense_verify, dim3((p.M - 1 + 3) / 4), dim3(256), 0, st, w.s_in, (const double*)w.s_out,
+                         1, p.M - 1, -1, p.L, p.Lp, p.tol, w.flags, (const float*)nullptr, 0, p.ctl + kDPending);
+      PMG_LAUNCH_CHECK();
+    }
+    PMG_HIP(launch_persistent(kfr, dim3(p.S), dim3(kDNT), 0, st, p));
+  }
   return PMG_OK;
 }
 
-int pmg_dense_backward(const float* delta, const float* phi, const double* ll64, const double* log_alpha, int64_t T,
-                       const pmg_dense_transition* tr, double likelihood_scale, int32_t chunk, int32_t warmup,
-                       double tol, float* P, float* gamma, float* log_gamma, float* rho, double* log_rho,
-                       void* workspace, size_t workspace_bytes, void* stream) {
+int pmg_dense_forward(const float* delta, const float* phi, const double* ll64, const double* m, int64_t T,
+                      const pmg_dense_transition* tr, double likelihood_scale, int32_t chunk, int32_t warmup,
+                      double tol, float* alpha, double* log_alpha, double* logc, double* logz, void* workspace,
+                      size_t workspace_bytes, void* stream) {
+  return dense_forward_impl(delta, phi, ll64, m, T, tr, likelihood_scale, chunk, warmup, tol, alpha, log_alpha, logc,
+                            logz, workspace, workspace_bytes, stream, 3);
+}
+
+int pmg_dense_forward_phase(const float* delta, const float* phi, const double* ll64, const double* m, int64_t T,
+                            const pmg_dense_transition* tr, double likelihood_scale, int32_t chunk, int32_t warmup,
+                            double tol, float* alpha, double* log_alpha, double* logc, double* logz, void* workspace,
+                            size_t workspace_bytes, void* stream, int32_t phase) {
+  PMG_REQUIRE(phase >= 1 && phase <= 3, "pmg_dense_forward_phase: phase %d", phase);
+  return dense_forward_impl(delta, phi, ll64, m, T, tr, likelihood_scale, chunk, warmup, tol, alpha, log_alpha, logc,
+                            logz, workspace, workspace_bytes, stream, phase);
+}
+
+static int dense_backward_impl(const float* delta, const float* phi, const double* ll64, const double* log_alpha,
+                               int64_t T, const pmg_dense_transition* tr, double likelihood_scale, int32_t chunk,
+                               int32_t warmup, double tol, float* P, float* gamma, float* log_gamma, float* rho,
+                               double* log_rho, void* workspace, size_t workspace_bytes, void* stream, int phase) {
   DenseParams p;
   int rc = dense_params(p, tr, T, chunk, warmup, likelihood_scale, tol);
   if (rc) return rc;
@@ -1141,18 +1186,37 @@ int pmg_dense_backward(const float* delta, const float* phi, const double* ll64,
   p.seg_chg = w.seg_chg;
   dense_kernel_t kf, kfr, kb, kbr;
   dense_kernels(p.Lp / kDNT, &kf, &kfr, &kb, &kbr);
-  // per-call words; the timeout word (kDErr) is sticky until the host reads it
-  PMG_HIP(hipMemsetAsync(p.ctl, 0, kDErr * sizeof(int), st));
-  PMG_HIP(hipMemsetAsync(p.ctl + kDErr + 1, 0, (16 - kDErr - 1) * sizeof(int), st));
-  hipLaunchKernelGGL(kb, dim3(p.M), dim3(kDNT), 0, st, p);
-  PMG_LAUNCH_CHECK();
-  if (p.M > 1) {
+  // per-pass words as dense_forward_impl
+  if (phase & 1) {
+    PMG_HIP(hipMemsetAsync(p.ctl, 0, kDErr * sizeof(int), st));
+    hipLaunchKernelGGL(kb, dim3(p.M), dim3(kDNT), 0, st, p);
+    PMG_LAUNCH_CHECK();
+  }
+  if ((phase & 2) && p.M > 1) {
+    PMG_HIP(hipMemsetAsync(p.ctl + kDErr + 1, 0, (16 - kDErr - 1) * sizeof(int), st));
     hipLaunchKernelGGL(k_dense_verify, dim3((p.M - 1 + 3) / 4), dim3(256), 0, st, w.b_in, (const double*)w.b_first, 0,
                        p.M - 2, 1, p.L, p.Lp, p.tol, w.flags, (const float*)nullptr, p.C, p.ctl + kDPending);
     PMG_LAUNCH_CHECK();
     PMG_HIP(launch_persistent(kbr, dim3(p.S), dim3(kDNT), 0, st, p));
   }
   return PMG_OK;
+}
+
+int pmg_dense_backward(const float* delta, const float* phi, const double* ll64, const double* log_alpha, int64_t T,
+                       const pmg_dense_transition* tr, double likelihood_scale, int32_t chunk, int32_t warmup,
+                       double tol, float* P, float* gamma, float* log_gamma, float* rho, double* log_rho,
+                       void* workspace, size_t workspace_bytes, void* stream) {
+  return dense_backward_impl(delta, phi, ll64, log_alpha, T, tr, likelihood_scale, chunk, warmup, tol, P, gamma,
+                             log_gamma, rho, log_rho, workspace, workspace_bytes, stream, 3);
+}
+
+int pmg_dense_backward_phase(const float* delta, const float* phi, const double* ll64, const double* log_alpha,
+                             int64_t T, const pmg_dense_transition* tr, double likelihood_scale, int32_t chunk,
+                             int32_t warmup, double tol, float* P, float* gamma, float* log_gamma, float* rho,
+                             double* log_rho, void* workspace, size_t workspace_bytes, void* stream, int32_t phase) {
+  PMG_REQUIRE(phase >= 1 && phase <= 3, "pmg_dense_backward_phase: phase %d", phase);
+  return dense_backward_impl(delta, phi, ll64, log_alpha, T, tr, likelihood_scale, chunk, warmup, tol, P, gamma,
+                             log_gamma, rho, log_rho, workspace, workspace_bytes, stream, phase);
 }
 
 int pmg_joint_log_accumulate(const double* log_alpha, const double* log_rho, int64_t T, int32_t L, double* logS,

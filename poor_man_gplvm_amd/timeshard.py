@@ -90,14 +90,16 @@ class ShardLayout:
 
 
 def shard_layout(T: int, world: int, chunk: int | None = None, halo: int = 512,
-                 scan: ScanConfig | None = None) -> list[ShardLayout]:
+                 scan: ScanConfig | None = None, dense: bool = False) -> list[ShardLayout]:
     """Split [0, T) into `world` contiguous shards of whole chunks (the last shard takes
     the remainder), each extended by `halo` steps (rounded up to whole chunks) on the
-    sides that have a neighbour."""
+    sides that have a neighbour.  dense: the default chunk of the dense log-domain scans
+    (custom / wide continuous kernels)."""
     if world < 1 or T < 1:
         raise ValueError("need T >= 1 and world >= 1")
     scan = scan or ScanConfig()
-    C = int(chunk) if chunk else scan.chunk_for(int(math.ceil(T / world)))
+    Tw = int(math.ceil(T / world))
+    C = int(chunk) if chunk else (scan.chunk_dense_for(Tw) if dense else scan.chunk_for(Tw))
     n_chunks = (T + C - 1) // C
     if n_chunks < world:
         raise ValueError(f"T={T} gives {n_chunks} chunks of {C}: fewer than {world} shards")
@@ -363,7 +365,15 @@ class ShardEM(DeviceEM):
                                                 self.Tp_own, nat.stream_handle()), "pmg_spikes_bf16t")
 
     def state(self, which: int, c: int) -> torch.Tensor:
-        """(2*Lpad,) f32 view of a boundary slot inside the scan workspace."""
+        """(2*Lpad,) f32 view of a boundary slot inside the scan workspace (the dense
+        log-domain scans: (2*Lp,) f64 log state, pmg_dense_state)."""
+        if self.dense:
+            p = self.lib.pmg_dense_state(nat.ptr(self.ws_dense), self.T, self.L, self.Cd, int(which), int(c))
+            if not p:
+                raise nat.NativeError(f"pmg_dense_state({which}, {c}) failed")
+            off = int(p) - self.ws_dense.data_ptr()
+            lp = int(self.lib.pmg_dense_lpad(self.L))
+            return self.ws_dense[off:off + 16 * lp].view(torch.float64)
         p = self.lib.pmg_fwdbwd_state(nat.ptr(self.ws_fb), self.T, self.L, self.C, int(which), int(c))
         if not p:
             raise nat.NativeError(f"pmg_fwdbwd_state({which}, {c}) failed")
@@ -385,6 +395,15 @@ class ShardEM(DeviceEM):
                                                  nat.ptr(self.ws_ss), self.ws_ss.numel(), sh), "pmg_suffstats")
 
     def forward_phase2(self, likelihood_scale, logz_scratch):
+        if self.dense:
+            with self._t('forward_carry'):
+                nat.check(self.lib.pmg_dense_forward_phase(
+                    nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.ll64), nat.ptr(self.mref), self.T,
+                    ctypes.byref(self._tr_d), float(likelihood_scale), self.Cd, int(self.warm[0]),
+                    float(self.scan.tol), nat.ptr(self.alpha), nat.ptr(self.log_alpha), nat.ptr(self.logc),
+                    nat.ptr(logz_scratch), nat.ptr(self.ws_dense), self.ws_dense.numel(), nat.stream_handle(), 2),
+                    "pmg_dense_forward_phase")
+            return
         args = (nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.mref), self.T, ctypes.byref(self._tr_c),
                 float(likelihood_scale), self.C, int(self.warm[0]), float(self.scan.tol), nat.ptr(self.alpha),
                 nat.ptr(self.logc), nat.ptr(logz_scratch), nat.ptr(self.ws_fb), self.ws_fb.numel(),
@@ -394,6 +413,15 @@ class ShardEM(DeviceEM):
                       "pmg_forward_filter")
 
     def backward_phase2(self, likelihood_scale, P=True, gamma=None):
+        if self.dense:
+            with self._t('backward_carry'):
+                nat.check(self.lib.pmg_dense_backward_phase(
+                    nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.ll64), nat.ptr(self.log_alpha), self.T,
+                    ctypes.byref(self._tr_d), float(likelihood_scale), self.Cd, int(self.warm[1]),
+                    float(self.scan.tol), nat.ptr(self._P) if P else None, nat.ptr(gamma), None, None, None,
+                    nat.ptr(self.ws_dense), self.ws_dense.numel(), nat.stream_handle(), 2),
+                    "pmg_dense_backward_phase")
+            return
         args = (nat.ptr(self.delta), nat.ptr(self.phi), nat.ptr(self.alpha), self.T, ctypes.byref(self._tr_c),
                 float(likelihood_scale), self.C, int(self.warm[1]), float(self.scan.tol),
                 nat.ptr(self.P) if P else None, nat.ptr(gamma), None, nat.ptr(self.ws_fb),
@@ -421,10 +449,6 @@ class TimeShardedEM:
         B = np.asarray(basis, np.float32)
         self.L = B.shape[0]
         scan = scan or ScanConfig()
-        from .gp_kernel import DenseTransition
-        if isinstance(transition, DenseTransition):
-            raise NotImplementedError("time-sharded EM runs the banded scans only (the dense log-domain scans "
-                                      "have no carry hand-off yet)")
         self.shards = [ShardEM(lay, y, self.L, B, scan, ma_neuron, device) for lay in self.lays]
         for s in self.shards:
             s.adaptive = True       # one fit: adaptive warm-up across its E-steps
@@ -574,7 +598,9 @@ def run_em_timesharded(y, params, basis, log_posterior_init, n_iter, transition,
     if not hasattr(y, "shape"):
         y = np.asarray(y)
     T = int(y.shape[0])
-    lays = shard_layout(T, comm.world, chunk=chunk, halo=halo, scan=scan)
+    from .gp_kernel import DenseTransition
+    lays = shard_layout(T, comm.world, chunk=chunk, halo=halo, scan=scan,
+                        dense=isinstance(transition, DenseTransition))
     eng = TimeShardedEM(y, basis, transition, comm, lays, scan, ma_neuron, ma_latent,
                         neuron_sharded=neuron_sharded)
     if timer is not None:

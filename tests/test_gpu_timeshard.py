@@ -212,3 +212,55 @@ def test_timesharded_gloo_two_ranks_neuron_sharded_adam():
     np.testing.assert_array_equal(W0, info['params64'])
     np.testing.assert_array_equal(out[1], info['params64'])
     np.testing.assert_array_equal(tun, ref['tuning'])
+
+
+@pytest.mark.parametrize("world,chunk,halo", [(2, 16, 64), (5, 16, 32)])
+def test_timesharded_dense_rbf_golden(world, chunk, halo):
+    """Time shards on the dense log-domain scans (the carry hand-off through the f64 log
+    boundary slots, pmg_dense_state + phase-2 calls): the fixture's RBF kernel given as a
+    dense transition reproduces the one-iteration golden at the strict bars."""
+    import poor_man_gplvm_amd as P
+    from oracle import gplvm_oracle as O
+    from poor_man_gplvm_amd.timeshard import run_em_timesharded
+    f = np.load(os.path.join(HERE, 'golden', 'em_c1_one.npz'))
+    L = f['basis'].shape[0]
+    _, logK, _, logA = O.create_transition_prob_1d(L, float(f['mv']))
+    from poor_man_gplvm_amd.gp_kernel import transition_from_log_kernels
+    tr = transition_from_log_kernels(logK, logA, force_dense=True)
+    res, info = run_em_timesharded(f['y'].astype(np.float32), f['W0'], f['basis'], f['lp0'],
+                                   n_iter=int(f['n_iter']), transition=tr, world=world, chunk=chunk, halo=halo,
+                                   adam=P.AdamConfig(maxiter=int(f['maxiter']), tol=float(f['tol'])))
+    assert info['chunk'] == chunk
+    np.testing.assert_allclose(res['tuning'], f['tuning'], rtol=RT)
+    close_prob(res['posterior_latent_marg'], f['posterior'].astype(np.float64).sum(1))
+    argmax_match(res['posterior_latent_marg'], f['posterior'].sum(1))
+    np.testing.assert_allclose(res['log_marginal_l'], f['log_marginal_l'], rtol=1e-7)
+    assert res['m_step_res_l']['n_iter'] == list(f['m_n_iter'])
+
+
+@pytest.mark.parametrize("world", [2, 5])
+def test_timesharded_custom_kernel_vs_oracle(world):
+    """A custom continuous kernel (Laplacian, exp(-|i - j| / 3): no band form; the
+    reference chunks any kernel, decoder.py:258-332 with gp_kernel.py:61-66) over time
+    shards with short halos, so carries must be repaired, against the f64 oracle run
+    from the same (W0, lp0): one EM iteration of 40 Adam bodies."""
+    import poor_man_gplvm_amd as P
+    from oracle import gplvm_oracle as O
+    from poor_man_gplvm_amd.timeshard import run_em_timesharded
+    N, L, T = 30, 96, 1200
+    d = make(N, L, T)
+    x = np.arange(L, dtype=np.float64)
+    ck = np.exp(-np.abs(x[:, None] - x[None, :]) / 3.0)
+    _, logK, _, logA = O.create_transition_prob_1d(L, 1.0, custom_kernel=ck)
+    from poor_man_gplvm_amd.gp_kernel import transition_from_log_kernels
+    tr = transition_from_log_kernels(logK, logA, force_dense=True)
+    res, info = run_em_timesharded(d['y'], d['W0'], d['B'], d['lp0'], n_iter=1, transition=tr, world=world,
+                                   chunk=16, halo=16, adam=P.AdamConfig(maxiter=40, tol=0.0),
+                                   scan=P.ScanConfig(warmup=4))
+    assert max(r[0] for r in info['carry_rounds']) >= 1
+    ref = O.fit_em(d['y'], d['W0'].astype(np.float64), d['B'].astype(np.float64), d['lp0'].astype(np.float64),
+                   n_iter=1, m_step_maxiter=40, m_step_tol=0.0, custom_kernel=ck)
+    np.testing.assert_allclose(res['tuning'], ref['tuning'], rtol=RT)
+    close_prob(res['posterior_latent_marg'], ref['posterior_latent_marg'])
+    argmax_match(res['posterior_latent_marg'], ref['posterior_latent_marg'])
+    np.testing.assert_allclose(res['log_marginal_l'], ref['log_marginal_l'], rtol=1e-7)

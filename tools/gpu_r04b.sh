@@ -8,3 +8,4 @@ timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeou
 echo "tests rc=$?" >> gpurun_out/r04b_tests.txt
 timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-api-fit --warmup 5 --steps 20 > gpurun_out/r04b_bench.json 2> gpurun_out/r04b_bench.err && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r04b -o run -- python3 bench.py --no-cpu-baseline --no-api-fit --warmup 5 --steps 20 > gpurun_out/r04b_prof.log 2>&1
+timeout -k 10 300 python -u tools/api_fit_profile.py > gpurun_out/r04b_api_profile.json 2> gpurun_out/r04b_api_profile.err
