@@ -430,8 +430,10 @@ __global__ void __launch_bounds__(512) k_ptb3q(const uint16_t* __restrict__ Pq, 
   const int ch = tid & 15, rw = tid >> 4;
   const int col = mt * TM + 8 * ch;
   const bool col_ok = col + 8 <= ldp;          // chunks past the row feed only dropped outputs
+  // per-lane offsets only (a lane-dependent soffset would be a waterfall loop): rows rw
+  // and rw + 32; out-of-range chunks point past the descriptor (reads return 0)
   const uint32_t voffA = col_ok ? (uint32_t)(rw * ldp + col) * 2u : 0x80000000u;
-  const uint32_t half_off = (uint32_t)(32 * ldp) * 2u;
+  const uint32_t voffA2 = col_ok ? voffA + (uint32_t)(32 * ldp) * 2u : 0x80000000u;
   // B staging (as k_ptb3)
   const int n_l = tid >> 2, hq = tid & 3;
   const int ng = nt * TN + n_l;
@@ -447,7 +449,7 @@ __global__ void __launch_bounds__(512) k_ptb3q(const uint16_t* __restrict__ Pq, 
           const_cast<uint16_t*>(Pq + sp * pq_stride + tbase * (int64_t)ldp), (short)0, (int)(nrow * ldp * 2),
           0x00020000);
       qa[sp][0] = __builtin_amdgcn_raw_buffer_load_b128(rs, voffA, 0, 0);
-      qa[sp][1] = __builtin_amdgcn_raw_buffer_load_b128(rs, voffA, col_ok ? half_off : 0u, 0);
+      qa[sp][1] = __builtin_amdgcn_raw_buffer_load_b128(rs, voffA2, 0, 0);
     }
     const int64_t tb = t0 < Tp - KB3 ? t0 : Tp - KB3;
     rb0 = *reinterpret_cast<const uint4*>(yrow + tb);
@@ -488,8 +490,9 @@ __global__ void __launch_bounds__(512) k_ptb3q(const uint16_t* __restrict__ Pq, 
   // f32 sums close at the end of every 2-tile (kFlush) segment of the GLOBAL tile grid, so
   // the rounding does not depend on where the K-slices start (nor on the latent count)
   auto tw_tile = [&](int64_t ti) {
-    if (ti % nNT == nt) tw_add();
-    if (ti & 1) tw_flush();
+    const int t32 = __builtin_amdgcn_readfirstlane((int)ti);   // tile indices < 2^31
+    if (t32 % nNT == nt) tw_add();
+    if (t32 & 1) tw_flush();
   };
 
   double acc64[2][16];

@@ -163,7 +163,7 @@ def test_backward_planes_bit_identical(L, chunk, warm):
     otherwise, bit for bit, for every lane width (J = 1 .. 16 latents per lane; J < 4 takes
     the per-element stores) and through the relaxation (chunk 16, no warm-up: every
     boundary repaired, MODE 1 writes the planes); and the statistics on them equal the
-    statistics on f32 P (y_w bit for bit)."""
+    statistics on f32 P (y_w bit for bit, t_w to its f32 group sums)."""
     N, T = 48, 2500
     d = make(N, L, T)
     sp, eng = _engine(d, L, chunk=chunk, warmup=warm)
@@ -192,7 +192,9 @@ def test_backward_planes_bit_identical(L, chunk, warm):
     eng.m_step(W, W.clone(), W.clone(), torch.zeros(1, dtype=torch.int64, device='cuda'), AdamConfig(maxiter=1),
                stats, lh, lh.clone())
     np.testing.assert_array_equal(eng.yw.cpu().numpy(), yw_a)
-    np.testing.assert_allclose(eng.tw.cpu().numpy(), tw_a, rtol=1e-12)
+    # t_w: f32 partial sums over different time groupings in the two kernels (8 steps in
+    # k_ptb3, a thread's rows of a 2-tile segment in k_ptb3q), then f64: ~1e-8 apart
+    np.testing.assert_allclose(eng.tw.cpu().numpy(), tw_a, rtol=1e-7)
 
 
 def test_flat_tuning_cascade():
