@@ -53,6 +53,40 @@ def _np(t):
     return t.detach().cpu().numpy()
 
 
+class _PinnedCopies:
+    """Device -> host copies of the arrays a fit returns, into page-locked buffers
+    (PCIe DMA at full rate instead of the staged pageable path), issued without a host
+    sync: copies of intermediate results (the save_every snapshots) run on a side stream
+    beside the remaining EM iterations, and the host allocates the final buffers while
+    the device is still computing.  finish() synchronises and returns numpy views."""
+
+    def __init__(self, dev):
+        self.dev = dev
+        self.side = torch.cuda.Stream(dev)
+        self.items = []
+
+    def alloc(self, shape, dtype=torch.float32):
+        return torch.empty(shape, dtype=dtype, pin_memory=True)
+
+    def submit(self, t, host=None, side=False):
+        """Copy device tensor t (not written again before finish) to a pinned buffer."""
+        host = self.alloc(tuple(t.shape), t.dtype) if host is None else host
+        if side:
+            self.side.wait_stream(torch.cuda.current_stream(self.dev))
+            with torch.cuda.stream(self.side):
+                host.copy_(t, non_blocking=True)
+            t.record_stream(self.side)
+        else:
+            host.copy_(t, non_blocking=True)
+        self.items.append(host)
+        return host
+
+    def finish(self):
+        torch.cuda.current_stream(self.dev).synchronize()
+        self.side.synchronize()
+        return [h.numpy() for h in self.items]
+
+
 class PoissonGPLVMJump1D:
     """Poisson GPLVM with a smooth 1-d latent and jump dynamics (core.py:746)."""
 
@@ -725,10 +759,13 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
     gamma = torch.empty((T, 2, L), dtype=torch.float32, device=dev)
     lgam = torch.empty((T, 2, L), dtype=torch.float32, device=dev) if eng.dense else None
 
-    def log_post():
-        return _masked_log(_np(lgam) if eng.dense else _np(log_of(gamma)), mlat)
-    saved = {'log_posterior_all_saved': [], 'params_saved': [], 'tuning_saved': [], 'iter_saved': [],
-             'log_marginal_saved': []}
+    def log_post_dev():
+        return lgam.clone() if eng.dense else log_of(gamma)
+    # the returned arrays go to the host through pinned buffers without host syncs inside
+    # the loop: snapshots on a side stream beside the later iterations (their device
+    # copies are fresh tensors), the final arrays after the loop
+    cp = _PinnedCopies(dev)
+    saved_dev = []      # (i, log posterior, W f32, tuning) pinned host buffers per snapshot
     saved_idx = []
     import time
     for i in range(n_iter):
@@ -739,32 +776,44 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
         eng.e_step(likelihood_scale, logz[i:i + 1], gamma=gamma if want_gamma else None,
                    log_gamma=lgam if want_gamma else None)
         if i % save_every == 0:
-            saved['log_posterior_all_saved'].append(log_post())
-            saved['params_saved'].append(_np(W).astype(np.float32))
-            saved['tuning_saved'].append(_np(eng.tuning32))
-            saved['iter_saved'].append(i)
+            saved_dev.append((cp.submit(log_post_dev(), side=True), cp.submit(W.to(torch.float32), side=True),
+                              cp.submit(eng.tuning32.clone(), side=True)))
             saved_idx.append(i)
         if timing is not None:
             torch.cuda.synchronize()
             timing.append(time.perf_counter() - t0)
-    lz = _np(logz)
-    saved['log_marginal_saved'] = [float(lz[i]) for i in saved_idx]
-    m_step_res_l = _m_step_res(_np(stats), _np(lh), _np(eh), n_iter)
-    posterior = _np(gamma)
+    # final arrays: the sums over d and l on the device (posterior_latent_marg /
+    # posterior_dynamics_marg), every copy queued behind the last E-step
+    h_post = cp.submit(gamma)
+    h_lpf = cp.submit(log_post_dev())
+    h_plm = cp.submit(gamma.sum(dim=1))
+    h_pdm = cp.submit(gamma.sum(dim=2))
+    h_W = cp.submit(W.to(torch.float32))
+    h_tun = cp.submit(eng.tuning32)
+    h_st, h_lh, h_eh, h_lz = cp.submit(stats), cp.submit(lh), cp.submit(eh), cp.submit(logz)
+    cp.finish()
+    lz = h_lz.numpy()
+    saved = {'log_posterior_all_saved': [_masked_log(a.numpy(), mlat) for a, _, _ in saved_dev],
+             'params_saved': [b.numpy() for _, b, _ in saved_dev],
+             'tuning_saved': [c.numpy() for _, _, c in saved_dev],
+             'iter_saved': list(saved_idx),
+             'log_marginal_saved': [float(lz[i]) for i in saved_idx]}
+    m_step_res_l = _m_step_res(h_st.numpy(), h_lh.numpy(), h_eh.numpy(), n_iter)
+    posterior = h_post.numpy()
     res = {'log_posterior_all_saved': saved['log_posterior_all_saved'],
            'log_posterior_init': log_posterior_init,
            'params_saved': saved['params_saved'],
            'tuning_saved': saved['tuning_saved'],
            'iter_saved': saved['iter_saved'],
-           'params': _np(W).astype(np.float32),
-           'tuning': _np(eng.tuning32),
-           'log_posterior_final': log_post(),
+           'params': h_W.numpy(),
+           'tuning': h_tun.numpy(),
+           'log_posterior_final': _masked_log(h_lpf.numpy(), mlat),
            'log_marginal': float(lz[n_iter - 1]) if n_iter else float('nan'),
            'log_marginal_l': [float(v) for v in lz[:n_iter]],
            'log_marginal_saved': saved['log_marginal_saved'],
            'posterior': posterior,
-           'posterior_latent_marg': posterior.sum(axis=1),
-           'posterior_dynamics_marg': posterior.sum(axis=2),
+           'posterior_latent_marg': h_plm.numpy(),
+           'posterior_dynamics_marg': h_pdm.numpy(),
            'm_step_res_l': m_step_res_l}
     if noise_std is not None:
         eng.gaussian_status()

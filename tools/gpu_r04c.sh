@@ -1,0 +1,10 @@
+#!/bin/bash
+# round 4 c: planes statistics after the waterfall fix: focused tests, bench, kernel trace
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+  tests/test_gpu_parity.py -k "suffstats or planes or fit_em or adam_c3" > gpurun_out/r04c_tests.txt 2>&1
+echo "tests rc=$?" >> gpurun_out/r04c_tests.txt
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-api-fit --warmup 5 --steps 20 > gpurun_out/r04c_bench.json 2> gpurun_out/r04c_bench.err && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_r04c -o run -- python3 bench.py --no-cpu-baseline --no-api-fit --warmup 5 --steps 20 > gpurun_out/r04c_prof.log 2>&1
