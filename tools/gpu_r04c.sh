@@ -12,3 +12,4 @@ echo "c4 rc=$?" >> gpurun_out/r04c_c4.txt
 timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-api-fit --warmup 5 --steps 20 > gpurun_out/r04c_bench.json 2> gpurun_out/r04c_bench.err && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_r04c -o run -- python3 bench.py --no-cpu-baseline --no-api-fit --warmup 5 --steps 20 > gpurun_out/r04c_prof.log 2>&1
 timeout -k 10 300 python -u tools/api_fit_profile.py > gpurun_out/r04c_api_profile.json 2> gpurun_out/r04c_api_profile.err
+timeout -k 10 200 python -u tools/adam_prof.py > gpurun_out/r04c_adamprof.txt 2>&1
