@@ -22,6 +22,7 @@
 #include <stdlib.h>
 
 #include "pmg_common.h"
+#include "pmg_math64.h"
 
 namespace pmg {
 
@@ -232,33 +233,6 @@ __device__ __forceinline__ double rcp_nr(double x) {
   r = fma(r, fma(-x, r, 1.0), r);
   return r;
 }
-// softplus(x) = max(x, 0) + log1p(e) and sigmoid(x), e = exp(-|x|), in f32 from three
-// hardware transcendentals (exp2, log2, rcp; ~25 VALU instead of the ~300 of OCML's
-// compensated log1pf + two expf + an IEEE division):
-//   e      exp_acc (the f32 product's rounding error restored);
-//   log1p  e >= 2^-7: Goldberg's log(u) e / (u - 1), u = f32(1 + e), which cancels the
-//          rounding of u; e < 2^-7: e (1 - e (1/2 - e (1/3 - e / 4))) (truncation < e^4 / 5);
-//   sigmoid (x >= 0 ? 1 : e) / u.
-// Each is within a few f32 ulps; the caller corrects f to first order in the f64 residual
-// of x and evaluates the gradient factor and the loss in f64.
-struct SoftplusF32 {
-  float f, sg;
-};
-__device__ __forceinline__ float log_f32(float x) {   // natural log from v_log_f32 (x > 0, normal)
-  return __builtin_amdgcn_logf(x) * 0.693147180559945309f;
-}
-__device__ __forceinline__ SoftplusF32 softplus_sigmoid(float x) {
-  const float e = exp_acc(-fabsf(x));
-  const float u = 1.f + e;
-  const float ru = __builtin_amdgcn_rcpf(u);
-  const float lg = log_f32(u) * (e * __builtin_amdgcn_rcpf(u - 1.f));   // u > 1 on this branch
-  const float ps = e * fmaf(-e, fmaf(-e, fmaf(-e, 0.25f, 0.333333343f), 0.5f), 1.f);
-  SoftplusF32 o;
-  o.f = fmaxf(x, 0.f) + (e < 0.0078125f ? ps : lg);
-  o.sg = (x >= 0.f ? 1.f : e) * ru;
-  return o;
-}
-
 template <int CTRL, typename T>
 __device__ __forceinline__ T dpp_t(T v) {
   if constexpr (sizeof(T) == 8) return dpp_d<CTRL>(v);
@@ -475,15 +449,16 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
       if (owner) sG[((lb * A + slot) >> 1) * 2 * SP + 2 * s + (slot & 1)] = gv;
       const double xl = (ywd != 0.0) ? ywd * ((double)logf(f32 + 1e-20f) + (double)sg * r * rcp_nr((double)f32)) : 0.0;
 #else
-      const SoftplusF32 sp = softplus_sigmoid(Fh);
-      const float f32 = sp.f, sg = sp.sg;
-      const double fd = (double)f32 + (double)sg * r;
-      const double ifd = rcp_nr(fd + 1e-20);
-      const float gv = live ? (float)((ywd * ifd - twd) * (double)sg) : 0.f;
+      // softplus, its log and the sigmoid in f64 (pmg_math64.h): the loss feeds the stop
+      // rule, which compares consecutive losses to 1e-6 relative, so it must not carry
+      // f32 rounding (a few-ulp f32 softplus moved a stop decision by one body)
+      (void)Fh;
+      (void)r;
+      const Softplus64 sp = softplus64(F);
+      const double fd = sp.f;
+      const float gv = live ? (float)((ywd * rcp_nr(fd + 1e-20) - twd) * sp.sg) : 0.f;
       if (owner) sG[((lb * A + slot) >> 1) * 2 * SP + 2 * s + (slot & 1)] = gv;
-      // log f = log f32 + sigmoid r / f to first order (the f64 reciprocal of fd: the
-      // difference from 1 / f32 is second order in r)
-      const double xl = (ywd != 0.0) ? ywd * ((double)log_f32(f32 + 1e-20f) + (double)sg * r * ifd) : 0.0;
+      const double xl = (ywd != 0.0) ? ywd * sp.logf : 0.0;
 #endif
       lpart -= live ? xl - fd * twd : 0.0;
       __builtin_amdgcn_sched_barrier(0);

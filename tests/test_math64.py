@@ -1,0 +1,26 @@
+"""The f64 softplus / log / sigmoid of the Adam objective (csrc/pmg_math64.h) against the
+long-double C library: the stop rule compares consecutive losses to 1e-6 relative, so the
+loss terms must stay within a few f64 ulps (fit_tuning_helper.py:63-81 evaluates them in
+f64 through jax.nn.softplus and xlogy)."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+@pytest.mark.skipif(shutil.which('g++') is None, reason="needs g++")
+def test_math64_accuracy(tmp_path):
+    exe = tmp_path / 'math64_check'
+    subprocess.run(['g++', '-O2', '-std=c++17', '-I', os.path.join(ROOT, 'poor_man_gplvm_amd', 'csrc'),
+                    os.path.join(HERE, 'native', 'math64_check.cpp'), '-o', str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
+    softplus, logf, sigmoid, exp_, log_ = map(float, out)
+    assert softplus <= 4.0
+    assert logf <= 6.0
+    assert sigmoid <= 4.0
+    assert exp_ <= 2.0
+    assert log_ <= 3.0
