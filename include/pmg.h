@@ -482,6 +482,19 @@ size_t pmg_joint_workspace_size(int64_t T, int32_t L);
 int pmg_joint_accumulate(const float* alpha, const float* rho, int64_t T, int32_t L, double* S,
                          void* workspace, size_t workspace_bytes, void* stream);
 
+/* ------------------------------------------------------------------ */
+/* Page-locked HOST buffers for the arrays a fit returns (the host       */
+/* arrays of core.run_em's result dict, core.py:696-712).  The pages are */
+/* mapped, first-touched by `threads` host threads in parallel (as       */
+/* transparent huge pages if `huge`), then registered with HIP, so a     */
+/* device->host copy into them runs at full PCIe rate.  Host-only: no    */
+/* stream, no device work; safe to call from a side thread while the     */
+/* device computes.  Free with pmg_host_free(ptr, bytes).                */
+int pmg_host_alloc(size_t bytes, int32_t threads, int32_t huge, void** out);
+int pmg_host_free(void* ptr, size_t bytes);
+/* device -> host copy into such a buffer, enqueued on `stream`               */
+int pmg_copy_d2h(void* dst, const void* src, size_t bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

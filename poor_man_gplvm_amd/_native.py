@@ -11,6 +11,8 @@ from __future__ import annotations
 import ctypes
 import os
 
+import numpy as np
+
 import torch  # noqa: F401  (loads the HIP runtime before the library)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -64,6 +66,7 @@ EXPORTED_SYMBOLS = (
     "pmg_emission_range_flag", "pmg_mstep_adam_status",
     "pmg_suffstats_bf16x3_workspace_size", "pmg_suffstats_bf16x3",
     "pmg_dense_lpad", "pmg_dense_state", "pmg_dense_forward_phase", "pmg_dense_backward_phase",
+    "pmg_host_alloc", "pmg_host_free", "pmg_copy_d2h",
 )
 
 
@@ -139,6 +142,9 @@ _SIGS = {
     "pmg_mstep_adam": ([_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, ctypes.POINTER(AdamCfg),
                         _P, _P, _P, _P, _SZ, _P], _I32),
     "pmg_mstep_adam_status": ([_P, ctypes.POINTER(_I32), _P], _I32),
+    "pmg_host_alloc": ([_SZ, _I32, _I32, ctypes.POINTER(ctypes.c_void_p)], _I32),
+    "pmg_host_free": ([_P, _SZ], _I32),
+    "pmg_copy_d2h": ([_P, _P, _SZ, _P], _I32),
     "pmg_mstep_tiled_workspace_size": ([_I32, _I32, _I32], _SZ),
     "pmg_mstep_adam_tiled": ([_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, ctypes.POINTER(AdamCfg),
                               _P, _P, _P, _P, _SZ, _P], _I32),
@@ -219,3 +225,30 @@ def ptr(t) -> int | None:
 
 def stream_handle() -> int:
     return torch.cuda.current_stream().cuda_stream
+
+
+class HostBuffer:
+    """Page-locked host memory from pmg_host_alloc (first-touched by several threads as
+    huge pages, then registered with HIP), exposed through the numpy array interface and
+    freed when the last array viewing it goes away."""
+
+    THREADS = max(1, min(8, os.cpu_count() or 1))
+
+    def __init__(self, shape, dtype):
+        self.nbytes = int(np.prod(shape, dtype=np.int64)) * np.dtype(dtype).itemsize
+        p = ctypes.c_void_p()
+        lib = load()
+        check(lib.pmg_host_alloc(max(self.nbytes, 1), self.THREADS, 1, ctypes.byref(p)), "pmg_host_alloc")
+        self._lib, self.ptr = lib, p.value
+        self.__array_interface__ = {'shape': tuple(int(s) for s in shape), 'typestr': np.dtype(dtype).str,
+                                    'data': (self.ptr, False), 'version': 3}
+
+    def __del__(self):
+        if getattr(self, 'ptr', None):
+            self._lib.pmg_host_free(self.ptr, max(self.nbytes, 1))
+            self.ptr = None
+
+
+def host_array(shape, dtype) -> np.ndarray:
+    """A page-locked numpy array (device->host copies into it run at full PCIe rate)."""
+    return np.asarray(HostBuffer(shape, dtype))

@@ -53,38 +53,66 @@ def _np(t):
     return t.detach().cpu().numpy()
 
 
+_NP_DTYPE = {torch.float32: np.float32, torch.float64: np.float64, torch.int64: np.int64,
+             torch.int32: np.int32}
+
+
 class _PinnedCopies:
     """Device -> host copies of the arrays a fit returns, into page-locked buffers
-    (PCIe DMA at full rate instead of the staged pageable path), issued without a host
-    sync: copies of intermediate results (the save_every snapshots) run on a side stream
-    beside the remaining EM iterations, and the host allocates the final buffers while
-    the device is still computing.  finish() synchronises and returns numpy views."""
+    (`_native.host_array`: PCIe DMA at full rate instead of the staged pageable path),
+    issued without a host sync.  The large buffers are reserved up front on a helper
+    thread (the allocation is a C call that holds no Python lock, so it runs while the
+    host enqueues the EM iterations); copies of intermediate results (the save_every
+    snapshots) run on a side stream beside the remaining iterations.  finish()
+    synchronises and returns; the buffers are the numpy arrays handed to the caller."""
+
+    SMALL = 4 << 20
 
     def __init__(self, dev):
+        from concurrent.futures import ThreadPoolExecutor
         self.dev = dev
         self.side = torch.cuda.Stream(dev)
         self.items = []
+        self.keep = []
+        self.reserved = {}
+        self.pool = ThreadPoolExecutor(max_workers=1)
 
-    def alloc(self, shape, dtype=torch.float32):
-        return torch.empty(shape, dtype=dtype, pin_memory=True)
+    def reserve(self, key, shape, dtype=torch.float32):
+        """Start allocating a host buffer for a later submit(..., key=key)."""
+        self.reserved.setdefault(key, []).append(
+            self.pool.submit(nat.host_array, tuple(shape), _NP_DTYPE[dtype]))
 
-    def submit(self, t, host=None, side=False):
+    def submit(self, t, key=None, side=False):
         """Copy device tensor t (not written again before finish) to a pinned buffer."""
-        host = self.alloc(tuple(t.shape), t.dtype) if host is None else host
+        t = t.contiguous()
+        cur = torch.cuda.current_stream(self.dev)
         if side:
-            self.side.wait_stream(torch.cuda.current_stream(self.dev))
-            with torch.cuda.stream(self.side):
-                host.copy_(t, non_blocking=True)
-            t.record_stream(self.side)
+            self.side.wait_stream(cur)
+        st = self.side if side else cur
+        nbytes = t.numel() * t.element_size()
+        q = self.reserved.get(key)
+        if not q and nbytes < self.SMALL:
+            # small results (W, tuning, histories): torch's cached pinned blocks
+            h = torch.empty(tuple(t.shape), dtype=t.dtype, pin_memory=True)
+            with torch.cuda.stream(st):
+                h.copy_(t, non_blocking=True)
+            host = h.numpy()
         else:
-            host.copy_(t, non_blocking=True)
+            host = q.pop(0).result() if q else nat.host_array(tuple(t.shape), _NP_DTYPE[t.dtype])
+            if host.shape != tuple(t.shape) or host.dtype != _NP_DTYPE[t.dtype]:
+                raise ValueError("reserved host buffer does not match the tensor")
+            nat.check(nat.load().pmg_copy_d2h(host.ctypes.data, t.data_ptr(), nbytes, st.cuda_stream),
+                      "pmg_copy_d2h")
+        self.keep.append(t)            # alive until the copy is done (finish)
         self.items.append(host)
         return host
 
     def finish(self):
         torch.cuda.current_stream(self.dev).synchronize()
         self.side.synchronize()
-        return [h.numpy() for h in self.items]
+        self.keep.clear()
+        self.pool.shutdown(wait=False)
+        return self.items
 
 
 class PoissonGPLVMJump1D:
@@ -765,6 +793,11 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
     # the loop: snapshots on a side stream beside the later iterations (their device
     # copies are fresh tensors), the final arrays after the loop
     cp = _PinnedCopies(dev)
+    n_saved = len(range(0, n_iter, save_every))
+    for _ in range(n_saved):
+        cp.reserve('snap', (T, 2, L))
+    for key, shape in (('post', (T, 2, L)), ('lpf', (T, 2, L)), ('plm', (T, L))):
+        cp.reserve(key, shape)
     saved_dev = []      # (i, log posterior, W f32, tuning) pinned host buffers per snapshot
     saved_idx = []
     import time
@@ -776,7 +809,7 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
         eng.e_step(likelihood_scale, logz[i:i + 1], gamma=gamma if want_gamma else None,
                    log_gamma=lgam if want_gamma else None)
         if i % save_every == 0:
-            saved_dev.append((cp.submit(log_post_dev(), side=True), cp.submit(W.to(torch.float32), side=True),
+            saved_dev.append((cp.submit(log_post_dev(), key='snap', side=True), cp.submit(W.to(torch.float32), side=True),
                               cp.submit(eng.tuning32.clone(), side=True)))
             saved_idx.append(i)
         if timing is not None:
@@ -784,36 +817,36 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
             timing.append(time.perf_counter() - t0)
     # final arrays: the sums over d and l on the device (posterior_latent_marg /
     # posterior_dynamics_marg), every copy queued behind the last E-step
-    h_post = cp.submit(gamma)
-    h_lpf = cp.submit(log_post_dev())
-    h_plm = cp.submit(gamma.sum(dim=1))
+    h_post = cp.submit(gamma, key='post')
+    h_lpf = cp.submit(log_post_dev(), key='lpf')
+    h_plm = cp.submit(gamma.sum(dim=1), key='plm')
     h_pdm = cp.submit(gamma.sum(dim=2))
     h_W = cp.submit(W.to(torch.float32))
     h_tun = cp.submit(eng.tuning32)
     h_st, h_lh, h_eh, h_lz = cp.submit(stats), cp.submit(lh), cp.submit(eh), cp.submit(logz)
     cp.finish()
-    lz = h_lz.numpy()
-    saved = {'log_posterior_all_saved': [_masked_log(a.numpy(), mlat) for a, _, _ in saved_dev],
-             'params_saved': [b.numpy() for _, b, _ in saved_dev],
-             'tuning_saved': [c.numpy() for _, _, c in saved_dev],
+    lz = h_lz
+    saved = {'log_posterior_all_saved': [_masked_log(a, mlat) for a, _, _ in saved_dev],
+             'params_saved': [b for _, b, _ in saved_dev],
+             'tuning_saved': [c for _, _, c in saved_dev],
              'iter_saved': list(saved_idx),
              'log_marginal_saved': [float(lz[i]) for i in saved_idx]}
-    m_step_res_l = _m_step_res(h_st.numpy(), h_lh.numpy(), h_eh.numpy(), n_iter)
-    posterior = h_post.numpy()
+    m_step_res_l = _m_step_res(h_st, h_lh, h_eh, n_iter)
+    posterior = h_post
     res = {'log_posterior_all_saved': saved['log_posterior_all_saved'],
            'log_posterior_init': log_posterior_init,
            'params_saved': saved['params_saved'],
            'tuning_saved': saved['tuning_saved'],
            'iter_saved': saved['iter_saved'],
-           'params': h_W.numpy(),
-           'tuning': h_tun.numpy(),
-           'log_posterior_final': _masked_log(h_lpf.numpy(), mlat),
+           'params': h_W,
+           'tuning': h_tun,
+           'log_posterior_final': _masked_log(h_lpf, mlat),
            'log_marginal': float(lz[n_iter - 1]) if n_iter else float('nan'),
            'log_marginal_l': [float(v) for v in lz[:n_iter]],
            'log_marginal_saved': saved['log_marginal_saved'],
            'posterior': posterior,
-           'posterior_latent_marg': h_plm.numpy(),
-           'posterior_dynamics_marg': h_pdm.numpy(),
+           'posterior_latent_marg': h_plm,
+           'posterior_dynamics_marg': h_pdm,
            'm_step_res_l': m_step_res_l}
     if noise_std is not None:
         eng.gaussian_status()
