@@ -336,6 +336,8 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
   __shared__ double sYw[SP][kThreads];
   __shared__ double sTw[kThreads];
   __shared__ double sF[SP][kThreads];
+  __shared__ __attribute__((aligned(16))) double sLog[2 * kLogTab];   // log_tab's table
+  for (int q = tid; q < kLogTab; q += blockDim.x) log_tab_entry(q, sLog[2 * q], sLog[2 * q + 1]);
 #pragma unroll
   for (int s = 0; s < SP; ++s) {
     sYw[s][tid] = (is_row && s < S) ? p.yw[(size_t)lrow * p.N + n0 + s] : 0.0;
@@ -449,14 +451,16 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
       if (owner) sG[((lb * A + slot) >> 1) * 2 * SP + 2 * s + (slot & 1)] = gv;
       const double xl = (ywd != 0.0) ? ywd * ((double)logf(f32 + 1e-20f) + (double)sg * r * rcp_nr((double)f32)) : 0.0;
 #else
-      // softplus, its log and the sigmoid in f64 (pmg_math64.h): the loss feeds the stop
-      // rule, which compares consecutive losses to 1e-6 relative, so it must not carry
-      // f32 rounding (a few-ulp f32 softplus moved a stop decision by one body)
+      // softplus and its log to a few f64 ulps (pmg_math64.h, table log): the loss feeds
+      // the stop rule, which compares consecutive losses to 1e-6 relative, so it must not
+      // carry f32 rounding (a few-ulp f32 softplus moved a stop decision by one body).
+      // The sigmoid (f32) only scales G = y_w / f - t_w, which cancels near the optimum
+      // and so is formed in f64 before its f32 rounding.
       (void)Fh;
       (void)r;
-      const Softplus64 sp = softplus64(F);
+      const SoftplusT sp = softplus_tab(F, sLog);
       const double fd = sp.f;
-      const float gv = live ? (float)((ywd * rcp_nr(fd + 1e-20) - twd) * sp.sg) : 0.f;
+      const float gv = live ? (float)(ywd * rcp_nr(fd + 1e-20) - twd) * sp.sg : 0.f;
       if (owner) sG[((lb * A + slot) >> 1) * 2 * SP + 2 * s + (slot & 1)] = gv;
       const double xl = (ywd != 0.0) ? ywd * sp.logf : 0.0;
 #endif

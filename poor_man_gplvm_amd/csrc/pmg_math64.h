@@ -11,6 +11,7 @@
 // the C library: tests/test_math64.py builds it with g++).
 #pragma once
 #include <math.h>
+#include <string.h>
 
 #ifdef __HIPCC__
 #define PMG_HD __host__ __device__ __forceinline__
@@ -100,6 +101,81 @@ PMG_HD double log64(double x) {
   const double t = atanh2_series(div64(m - 1.0, m + 1.0));
   const double kd = (double)k;
   return fma(kd, 6.93147180369123816490e-01, fma(kd, 1.90821492927058770002e-10, t));
+}
+
+// ---------------------------------------------------------------------------------
+// Table-driven log for the hot loop (k_adam): 128 intervals of [1, 2), entry j holding
+// (1 / c_j, -log(1 / c_j)) with c_j = 1 + (j + 1/2) / 128, except entry 0 = (1, 0) so that
+// u in [1, 1 + 1/128) reduces EXACTLY to r = u - 1 (log1p of tiny arguments keeps its
+// relative accuracy).  log x = k ln2 + (-log(1 / c_j)) + log1p(r), r = x 2^-k / c_j - 1 in
+// one fma, |r| < 1/128, log1p(r) to degree 8 (r^9 / 9 < 2^-63 |r|).  The table is built on
+// the device from log64 (log_tab_entry), so host and device share one definition.
+// ---------------------------------------------------------------------------------
+constexpr int kLogTab = 128;
+
+PMG_HD void log_tab_entry(int j, double& invc, double& nlc) {
+  if (j == 0) {
+    invc = 1.0;
+    nlc = 0.0;
+    return;
+  }
+  invc = div64(1.0, 1.0 + (j + 0.5) / (double)kLogTab);
+  nlc = -log64(invc);
+}
+
+// log x for normal positive x; tab[2 j] = 1 / c_j, tab[2 j + 1] = -log(1 / c_j)
+PMG_HD double log_tab(double x, const double* tab) {
+  int k;
+  const double m = 2.0 * frexp(x, &k);          // [1, 2)
+  const double kd = (double)(k - 1);
+#ifdef __HIP_DEVICE_COMPILE__
+  const int j = (int)((__double2hiint(m) >> 13) & (kLogTab - 1));
+#else
+  long long bits;
+  memcpy(&bits, &m, 8);
+  const int j = (int)((bits >> 45) & (kLogTab - 1));
+#endif
+  const double invc = tab[2 * j], nlc = tab[2 * j + 1];
+  const double r = fma(m, invc, -1.0);
+  double p = -1.0 / 8.0;
+  p = fma(p, r, 1.0 / 7.0);
+  p = fma(p, r, -1.0 / 6.0);
+  p = fma(p, r, 1.0 / 5.0);
+  p = fma(p, r, -1.0 / 4.0);
+  p = fma(p, r, 1.0 / 3.0);
+  p = fma(p, r, -1.0 / 2.0);
+  const double lp = fma(r * r, p, r);            // log1p(r)
+  const double hi = fma(kd, 6.93147180369123816490e-01, nlc);
+  return hi + fma(kd, 1.90821492927058770002e-10, lp);
+}
+
+// softplus, its log and the sigmoid with the table log: log1p(e) = log(u) + (e - (u - 1)) / u,
+// u = 1 + e rounded (u - 1 and e - (u - 1) are exact; the correction is below ulp(u), so an
+// approximate reciprocal suffices).  The sigmoid is returned to f32 accuracy: it only scales
+// the f32 gradient factor G.
+struct SoftplusT {
+  double f, logf;
+  float sg;
+};
+PMG_HD SoftplusT softplus_tab(double F, const double* tab) {
+  const double e = exp_neg64(-fabs(F));
+  const double u = 1.0 + e;
+#ifdef __HIP_DEVICE_COMPILE__
+  const double ru = __builtin_amdgcn_rcp(u);
+#else
+  const double ru = 1.0 / u;
+#endif
+  const double l1p = log_tab(u, tab) + (e - (u - 1.0)) * ru;
+  SoftplusT o;
+  o.f = fmax(F, 0.0) + l1p;
+  o.logf = log_tab(o.f + 1e-20, tab);
+  const float e32 = (float)e;
+#ifdef __HIP_DEVICE_COMPILE__
+  o.sg = (F >= 0.0 ? 1.0f : e32) * __builtin_amdgcn_rcpf(1.0f + e32);
+#else
+  o.sg = (F >= 0.0 ? 1.0f : e32) / (1.0f + e32);
+#endif
+  return o;
 }
 
 // softplus(F) = max(F, 0) + log1p(e^-|F|), its log, and sigmoid(F) = (F >= 0 ? 1 : e) / (1 + e)

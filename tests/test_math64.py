@@ -18,9 +18,15 @@ def test_math64_accuracy(tmp_path):
     subprocess.run(['g++', '-O2', '-std=c++17', '-I', os.path.join(ROOT, 'poor_man_gplvm_amd', 'csrc'),
                     os.path.join(HERE, 'native', 'math64_check.cpp'), '-o', str(exe)], check=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
-    softplus, logf, sigmoid, exp_, log_ = map(float, out)
+    softplus, logf, sigmoid, exp_, log_, t_softplus, t_logf, t_sigmoid_rel, t_log = map(float, out)
+    # series forms (f64 ulps; log(f) in eps relative to max(1, |log f|))
     assert softplus <= 4.0
     assert logf <= 6.0
     assert sigmoid <= 4.0
     assert exp_ <= 2.0
     assert log_ <= 3.0
+    # table forms used by k_adam: softplus and its log to a few f64 ulps, the sigmoid to f32
+    assert t_softplus <= 5.0
+    assert t_logf <= 7.0
+    assert t_log <= 3.0
+    assert t_sigmoid_rel <= 3e-7
