@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 
 import numpy as np
 
@@ -229,24 +230,67 @@ def stream_handle() -> int:
 
 class HostBuffer:
     """Page-locked host memory from pmg_host_alloc (first-touched by several threads as
-    huge pages, then registered with HIP), exposed through the numpy array interface and
-    freed when the last array viewing it goes away."""
+    huge pages, then registered with HIP), exposed through the numpy array interface.
+    When the last array viewing it goes away the block returns to a process-wide cache
+    (up to HOST_CACHE_BYTES; beyond that it is unregistered and unmapped), so repeated
+    fits and decodes of one shape reuse their buffers instead of re-pinning (allocation
+    ~4 ms and release ~20 ms per 410 MB)."""
 
     THREADS = max(1, min(8, os.cpu_count() or 1))
 
     def __init__(self, shape, dtype):
-        self.nbytes = int(np.prod(shape, dtype=np.int64)) * np.dtype(dtype).itemsize
-        p = ctypes.c_void_p()
-        lib = load()
-        check(lib.pmg_host_alloc(max(self.nbytes, 1), self.THREADS, 1, ctypes.byref(p)), "pmg_host_alloc")
-        self._lib, self.ptr = lib, p.value
+        self.nbytes = max(int(np.prod(shape, dtype=np.int64)) * np.dtype(dtype).itemsize, 1)
+        self._lib = load()
+        self.ptr = _host_cache_take(self.nbytes)
+        if self.ptr is None:
+            p = ctypes.c_void_p()
+            check(self._lib.pmg_host_alloc(self.nbytes, self.THREADS, 1, ctypes.byref(p)), "pmg_host_alloc")
+            self.ptr = p.value
         self.__array_interface__ = {'shape': tuple(int(s) for s in shape), 'typestr': np.dtype(dtype).str,
                                     'data': (self.ptr, False), 'version': 3}
 
     def __del__(self):
-        if getattr(self, 'ptr', None):
-            self._lib.pmg_host_free(self.ptr, max(self.nbytes, 1))
-            self.ptr = None
+        ptr, self.ptr = getattr(self, 'ptr', None), None
+        if ptr and not _host_cache_give(ptr, self.nbytes):
+            self._lib.pmg_host_free(ptr, self.nbytes)
+
+
+HOST_CACHE_BYTES = 8 << 30
+_host_cache = {}            # nbytes -> [ptr, ...]
+_host_cache_total = 0
+_host_cache_lock = threading.Lock()
+
+
+def _host_cache_take(nbytes):
+    global _host_cache_total
+    with _host_cache_lock:
+        q = _host_cache.get(nbytes)
+        if q:
+            _host_cache_total -= nbytes
+            return q.pop()
+    return None
+
+
+def _host_cache_give(ptr, nbytes):
+    global _host_cache_total
+    with _host_cache_lock:
+        if _host_cache_total + nbytes > HOST_CACHE_BYTES:
+            return False
+        _host_cache.setdefault(nbytes, []).append(ptr)
+        _host_cache_total += nbytes
+        return True
+
+
+def release_host_cache():
+    """Unregister and unmap every cached page-locked block."""
+    global _host_cache_total
+    with _host_cache_lock:
+        items = [(p, n) for n, q in _host_cache.items() for p in q]
+        _host_cache.clear()
+        _host_cache_total = 0
+    lib = load()
+    for p, n in items:
+        lib.pmg_host_free(p, n)
 
 
 def host_array(shape, dtype) -> np.ndarray:

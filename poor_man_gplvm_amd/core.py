@@ -308,6 +308,12 @@ class PoissonGPLVMJump1D:
         pjm = hyperparam.get('p_jump_to_move', self.p_jump_to_move)
         dev = eng.dev
         T, L = eng.T, self.n_latent_bin
+        # the (T, 2, L) / (T, L) results go to page-locked host buffers, allocated on a
+        # helper thread while the device runs the scans (as run_em's)
+        cp = _PinnedCopies(dev)
+        for key, shape in (('lpost', (T, 2, L)), ('lcaus', (T, 2, L)), ('gamma', (T, 2, L)), ('ll', (T, L)),
+                           ('plm', (T, L))):
+            cp.reserve(key, shape)
         logz = torch.zeros(1, dtype=torch.float64, device=dev)
         gamma = torch.empty((T, 2, L), dtype=torch.float32, device=dev)
         rho = (torch.zeros((T, 2, L), dtype=torch.float64 if eng.dense else torch.float32, device=dev)
@@ -316,17 +322,27 @@ class PoissonGPLVMJump1D:
         eng.e_step(likelihood_scale, logz, gamma=gamma, rho=rho, log_gamma=lgam)
         eng.check_status()
         ml = None if ma_latent is None else np.asarray(ma_latent).astype(bool)
-        if eng.dense:     # the log-domain scans hold the exact log posteriors
-            log_post, log_causal = _np(lgam), _np(eng.log_alpha).astype(np.float32)
-        else:
-            log_post, log_causal = _np(log_of(gamma)), _np(log_of(eng.alpha))
+        # the log-domain scans hold the exact log posteriors (f64 causal ones, cast on the device)
+        h_lpost = cp.submit(lgam if eng.dense else log_of(gamma), key='lpost')
+        h_lcaus = cp.submit(eng.log_alpha.to(torch.float32) if eng.dense else log_of(eng.alpha), key='lcaus')
+        h_gamma = cp.submit(gamma, key='gamma')
+        h_plm = cp.submit(gamma.sum(dim=1), key='plm')
+        h_pdm = cp.submit(gamma.sum(dim=2))
+        h_logc = cp.submit(eng.logc.to(torch.float32))
+        h_ll = cp.submit(eng.loglik(), key='ll')
+        h_lz = cp.submit(logz)
+        if joint:
+            h_S = cp.submit(eng.joint_log(rho) if eng.dense else eng.joint(rho))
+        cp.finish()
         out = {
-            'log_posterior_all': _masked_log(log_post, ml),
-            'log_marginal_final': float(_np(logz)[0]),
-            'posterior_all': _np(gamma),
-            'log_causal_posterior_all': _masked_log(log_causal, ml),
-            'log_one_step_predictive_marginals_all': _np(eng.logc).astype(np.float32),
-            'log_likelihood_all': _np(eng.loglik()),
+            'log_posterior_all': _masked_log(h_lpost, ml),
+            'log_marginal_final': float(h_lz[0]),
+            'posterior_all': h_gamma,
+            'log_causal_posterior_all': _masked_log(h_lcaus, ml),
+            'log_one_step_predictive_marginals_all': h_logc,
+            'log_likelihood_all': h_ll,
+            '_posterior_latent_marg': h_plm,      # sums over d / l formed on the device
+            '_posterior_dynamics_marg': h_pdm,
         }
         if joint:
             if logK is None or logA is None:
@@ -334,13 +350,12 @@ class PoissonGPLVMJump1D:
             logK = np.asarray(logK, np.float64)
             logA = np.asarray(logA, np.float64)
             if eng.dense:   # rho holds log(rho): the joint is accumulated in log space
-                logS4 = _np(eng.joint_log(rho)).reshape(2, L, 2, L).transpose(0, 2, 1, 3)
+                logS4 = h_S.reshape(2, L, 2, L).transpose(0, 2, 1, 3)
                 with np.errstate(invalid='ignore'):
                     lj = np.asarray(logA, np.float64)[:, :, None, None] + logK[None] + logS4
                 lj = np.where(np.isnan(lj), -np.inf, lj)
             else:
-                S = _np(eng.joint(rho))  # (2L, 2L) f64
-                S4 = S.reshape(2, L, 2, L).transpose(0, 2, 1, 3)          # [d, d', i, j]
+                S4 = h_S.reshape(2, L, 2, L).transpose(0, 2, 1, 3)        # [d, d', i, j]
                 lj = log_joint_from_counts(S4, logK, logA, ml)
             out['log_accumulated_joint'] = lj
         return out
@@ -399,8 +414,8 @@ class PoissonGPLVMJump1D:
     def _decode_result(self, r, t_l=None):
         """decode_latent's returned dict from a _decode_on result (core.py:477-497)."""
         posterior_all = r['posterior_all']
-        plm = posterior_all.sum(axis=1)
-        pdm = posterior_all.sum(axis=2)
+        plm = r['_posterior_latent_marg'] if '_posterior_latent_marg' in r else posterior_all.sum(axis=1)
+        pdm = r['_posterior_dynamics_marg'] if '_posterior_dynamics_marg' in r else posterior_all.sum(axis=2)
         if t_l is not None and nap is not None:
             plm = nap.TsdFrame(d=plm, t=t_l)
             pdm = nap.TsdFrame(d=pdm, t=t_l)
