@@ -26,6 +26,8 @@
 
 namespace pmg {
 
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
@@ -248,13 +250,11 @@ __global__ void __launch_bounds__(512, MT == 1 ? 4 : 2) k_emission_i8(
     if constexpr (LL) {
       const unsigned long long vu = (unsigned long long)__double_as_longlong(v);
       const uint32_t ol = lvalid ? 2u * od : kNoWrite;
-      __builtin_amdgcn_raw_buffer_store_b32((uint32_t)vu, rl, ol, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(vu >> 32), rl, ol + 4, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)vu, (uint32_t)(vu >> 32)}, rl, ol, 0, 0);
     }
     const uint32_t orb = r == 0 ? (uint32_t)(tr * nblk + blk) * 8u : kNoWrite;
     const unsigned long long mu = (unsigned long long)__double_as_longlong(mx);
-    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)mu, rr, orb, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(mu >> 32), rr, orb + 4, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)mu, (uint32_t)(mu >> 32)}, rr, orb, 0, 0);
   }
 }
 
@@ -494,13 +494,11 @@ __global__ void __launch_bounds__(1024) k_emission_pipe(
       if constexpr (LL) {
         const unsigned long long vu = (unsigned long long)__double_as_longlong(v);
         const uint32_t ol = ol0 + (uint32_t)(ri * L) * 8u;
-        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)vu, rl, ol, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(vu >> 32), rl, ol + 4, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)vu, (uint32_t)(vu >> 32)}, rl, ol, 0, 0);
       }
       const uint32_t ob = ob0 + (uint32_t)(ri * nblk) * 8u;
       const unsigned long long mu = (unsigned long long)__double_as_longlong(mx);
-      __builtin_amdgcn_raw_buffer_store_b32((uint32_t)mu, rr, ob, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(mu >> 32), rr, ob + 4, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)mu, (uint32_t)(mu >> 32)}, rr, ob, 0, 0);
     }
   }
 }
@@ -733,13 +731,11 @@ __global__ void __launch_bounds__(512) k_emission_yreg(
         if constexpr (LL) {
           const unsigned long long vu = (unsigned long long)__double_as_longlong(v);
           const uint32_t ol = ol0 + (uint32_t)(ri * L) * 8u;
-          __builtin_amdgcn_raw_buffer_store_b32((uint32_t)vu, rl, ol, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(vu >> 32), rl, ol + 4, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)vu, (uint32_t)(vu >> 32)}, rl, ol, 0, 0);
         }
         const uint32_t ob = ob0 + (uint32_t)(ri * nblk) * 8u;
         const unsigned long long mu = (unsigned long long)__double_as_longlong(mx);
-        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)mu, rr, ob, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(mu >> 32), rr, ob + 4, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)mu, (uint32_t)(mu >> 32)}, rr, ob, 0, 0);
       }
     }
   }
