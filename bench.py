@@ -360,6 +360,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--chunk-bwd", type=int, default=0, help="backward chunk (0: ScanConfig default, 2x forward)")
     ap.add_argument("--warm-steps", type=int, default=48)
+    ap.add_argument("--scan-tol", type=float, default=0.0, help="boundary tolerance (0: ScanConfig default)")
     ap.add_argument("--warm-fb", type=str, default="", help="fixed forward,backward warm-up (no adaptation)")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--shard", default="restarts", choices=["restarts", "time"],
@@ -404,6 +405,8 @@ def main():
     y, B, W0, lp0 = synth(N, T, L, rank=rank)
     dev = torch.device("cuda", local)
     scan = ScanConfig(chunk=args.chunk or None, warmup=args.warm_steps, chunk_bwd=args.chunk_bwd or None)
+    if args.scan_tol > 0:
+        scan.tol = args.scan_tol
     sp = SpikeData(y)
     eng = DeviceEM(sp, L, basis=B, scan=scan)
     eng.adaptive = True          # as run_em: adaptive warm-up across the fit's E-steps

@@ -278,8 +278,9 @@ class DeviceEM:
                         self.lib.pmg_suffstats_bf16x3_workspace_size(T, L, N)) if spikes.ybt is not None
                     else self.lib.pmg_suffstats_workspace_size(T, L, spikes.Np))
         self.ws_ss = torch.empty(int(ss_bytes), dtype=torch.uint8, device=dev)
-        if self.ws_fb.numel() == 0:
-            raise nat.NativeError(f"n_latent_bin={L} unsupported by the scan kernels (max 1024)")
+        if self.ws_fb.numel() == 0 and L <= 1024:
+            raise nat.NativeError(f"pmg_fwdbwd_workspace_size(T={T}, L={L}) returned 0")
+        # L > 1024: only the dense log-domain scans (set_transition refuses a banded one)
         self.ws_ad = AdamWorkspace(self.lib, self.dev)
         self.warm = [int(self.scan.warmup), int(self.scan.warmup)]   # forward, backward
         self._clean = [0, 0]
@@ -342,6 +343,9 @@ class DeviceEM:
         if isinstance(tr, DenseTransition):
             self._set_dense(tr)
             return
+        if self.L > 1024:
+            raise nat.NativeError(f"n_latent_bin={self.L}: the banded scans hold L <= 1024; pass a DenseTransition "
+                                  "(gp_kernel.make_transition / dense_transition)")
         self.dense = False
         self._tr = tr
         self._invz = torch.as_tensor(tr.invz, device=self.dev)
@@ -380,7 +384,7 @@ class DeviceEM:
         self.Cd = self.scan.chunk_dense_for(self.T)
         need = int(self.lib.pmg_dense_workspace_size(self.T, self.L, self.Cd))
         if need == 0:
-            raise nat.NativeError(f"n_latent_bin={self.L} unsupported by the dense scans (max 1024)")
+            raise nat.NativeError(f"n_latent_bin={self.L} unsupported by the dense scans (max 2048)")
         if self.ws_dense is None or self.ws_dense.numel() < need:
             # zero-filled: it holds the sticky relaxation timeout words (include/pmg.h)
             self.ws_dense = torch.zeros(need, dtype=torch.uint8, device=self.dev)

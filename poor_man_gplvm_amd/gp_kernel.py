@@ -98,6 +98,8 @@ class BandedTransition:
 def banded_transition(n_latent_bin, movement_variance=1.0, p_move_to_jump=0.01,
                       p_jump_to_move=0.01, custom_kernel=None) -> BandedTransition:
     """Compact (Toeplitz band + row normaliser) form of the continuous kernel."""
+    if n_latent_bin > 1024:
+        raise NotImplementedError("the banded scans hold n_latent_bin <= 1024 (larger: the dense scans)")
     if custom_kernel is not None:
         raise NotImplementedError(
             "custom_transition_kernel (a dense L x L continuous kernel, gp_kernel.py:61-66) is not "
@@ -181,7 +183,7 @@ def transition_from_log_kernels(log_latent_transition_kernel_l, log_dynamics_tra
     if not np.all(rowmax > 0):
         raise ValueError("continuous kernel has an all-zero row")
     dense = DenseTransition(L=L, logK0=lk[0].copy(), A=np.exp(la))
-    if force_dense:
+    if force_dense or L > 1024:     # the banded scans hold L <= 1024
         return dense
     dia = np.diagonal(K0)
     if not np.all(dia >= rowmax * (1 - rtol)):

@@ -165,3 +165,29 @@ def test_decode_latent_outputs_finite_with_unvisited_bins():
     ref = O.decode_latent(y, tun)
     for k in ('p_transition_latent', 'p_transition_full', 'p_transition_dynamics', 'p_joint_latent'):
         np.testing.assert_allclose(r[k], ref[k], rtol=1e-5, atol=1e-12, err_msg=k)
+
+
+def test_large_latent_count_vs_oracle():
+    """n_latent_bin > 1024 (the reference scans any L, decoder.py:151-172): the banded
+    scans hold L <= 1024, so the model takes the dense log-domain scans with 8 latents per
+    thread (L <= 2048).  Decode (posterior, log marginal, one-step predictive) and one EM
+    iteration (tuning, posterior) against the f64 oracle."""
+    import poor_man_gplvm_amd as P
+    N, L, T = 24, 1280, 200
+    d = make(N, L, T)
+    m = P.PoissonGPLVMJump1D(N, n_latent_bin=L, tuning_lengthscale=10.)
+    from poor_man_gplvm_amd.gp_kernel import DenseTransition, dense_transition
+    assert isinstance(m._transition(1.0, 0.01, 0.01), DenseTransition)
+    r = m.decode_latent(d['y'], tuning=d['tuning'])
+    ref = O.decode_latent(d['y'], d['tuning'])
+    close_prob(r['posterior_all'], ref['posterior_all'])
+    argmax_match(r['posterior_latent_marg'], ref['posterior_latent_marg'])
+    assert abs(r['log_marginal_final'] - ref['log_marginal_final']) <= 1e-7 * abs(ref['log_marginal_final'])
+    np.testing.assert_allclose(r['log_one_step_predictive_marginals_all'],
+                               ref['log_one_step_predictive_marginals_all'], rtol=1e-6, atol=1e-5)
+    res, _ = P.run_em(d['y'].astype(np.float32), d['W0'], d['B'], d['lp0'], n_iter=1,
+                      transition=dense_transition(L, 1.0), adam=P.AdamConfig(maxiter=40, tol=0.0))
+    ref = O.fit_em(d['y'], d['W0'].astype(np.float64), d['B'].astype(np.float64), d['lp0'].astype(np.float64),
+                   n_iter=1, m_step_maxiter=40, m_step_tol=0.0)
+    np.testing.assert_allclose(res['tuning'], ref['tuning'], rtol=1e-5)
+    close_prob(res['posterior_latent_marg'], ref['posterior_latent_marg'])
