@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4 i: k_adam instruction mix (PMC) over controlled 300-body M-steps at C3
+# k_adam instruction mix (PMC, three counter passes) over controlled 300-body M-steps at C3 (tools/adam_prof.py); summary: profiles/r04_adam_pmc_c3.json
 set -o pipefail
 mkdir -p gpurun_out/r04i
 export TMPDIR=/tmp
