@@ -603,6 +603,40 @@ __global__ void __launch_bounds__(kTwM * kTwG) k_tw_reduce(const double* __restr
   }
 }
 
+// y_w (k_atb_reduce's per-element sums) and t_w (k_tw_reduce's) in ONE launch of
+// 1024-thread blocks: blocks [0, nA) reduce y_w elements, the rest t_w rows, each with the
+// arithmetic and order of the two separate kernels (bit-identical); one launch fewer per
+// EM iteration
+__global__ void __launch_bounds__(kTwM * kTwG) k_ss_reduce(const double* __restrict__ part, int nKS, int Mp, int Npd,
+                                                           int L, int N, double* __restrict__ yw,
+                                                           const double* __restrict__ twpart, double* __restrict__ tw,
+                                                           int nA) {
+  if ((int)blockIdx.x < nA) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)L * Npd) return;
+    const int m = (int)(i / Npd), n = (int)(i % Npd);
+    if (n >= N) return;
+    double s = 0.0;
+    for (int k = 0; k < nKS; ++k) s += part[((size_t)k * Mp + m) * Npd + n];
+    yw[(size_t)m * N + n] = s;
+    return;
+  }
+  __shared__ double sp[kTwG][kTwM];
+  const int mi = threadIdx.x % kTwM, g = threadIdx.x / kTwM;
+  const int m = ((int)blockIdx.x - nA) * kTwM + mi;
+  double s = 0.0;
+  if (m < L)
+    for (int k = g; k < 4 * nKS; k += kTwG) s += twpart[(size_t)k * Mp + m];
+  sp[g][mi] = s;
+  __syncthreads();
+  if (g == 0 && m < L) {
+    double t = 0.0;
+#pragma unroll
+    for (int q = 0; q < kTwG; ++q) t += sp[q][mi];
+    tw[m] = t;
+  }
+}
+
 // the same over `rows` partial rows (k_ptb3q: nKS x nNT)
 __global__ void __launch_bounds__(kTwM * kTwG) k_tw_reduce_n(const double* __restrict__ twpart, int rows, int Mp,
                                                              int L, double* __restrict__ tw) {
@@ -727,11 +761,10 @@ int pmg_suffstats_bf16(const float* P, const uint16_t* ybt, int64_t T, int64_t T
                      nKS, Mp, Npd, part, twpart);
   PMG_LAUNCH_CHECK();
   const int64_t total = (int64_t)L * Npd;
-  hipLaunchKernelGGL(k_atb_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
-                     (const double*)part, nKS, Mp, Npd, L, N, N, yw, -1, (double*)nullptr);
-  PMG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_tw_reduce, dim3((unsigned)((L + kTwM - 1) / kTwM)), dim3(kTwM * kTwG), 0, st,
-                     (const double*)twpart, nKS, Mp, L, tw);
+  const int nA = (int)((total + kTwM * kTwG - 1) / (kTwM * kTwG));
+  const int nT = (L + kTwM - 1) / kTwM;
+  hipLaunchKernelGGL(k_ss_reduce, dim3((unsigned)(nA + nT)), dim3(kTwM * kTwG), 0, st, (const double*)part, nKS,
+                     Mp, Npd, L, N, yw, (const double*)twpart, tw, nA);
   PMG_LAUNCH_CHECK();
   return PMG_OK;
 }
