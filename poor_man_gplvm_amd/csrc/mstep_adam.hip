@@ -305,7 +305,10 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
   const int S = (p.N - n0) < p.S ? (p.N - n0) : p.S;  // neurons owned (<= SP)
   const int L = p.L, NB = p.NB;
   const double sd = p.prior_std, isd2 = 1.0 / (sd * sd);
-  const double lconst = log(sd) + 0.5 * log(2.0 * M_PI);
+  // the prior's normaliser, read from LDS in the update (a register held across the loop
+  // is one the allocator would rather spill)
+  __shared__ double sLconst;
+  if (threadIdx.x == 0) sLconst = log(sd) + 0.5 * log(2.0 * M_PI);
 
   // ---- thread roles ------------------------------------------------------------
   const int lb = wid * 4 + (lane >> 4);                // l-block (rows lb*A ..)
@@ -567,7 +570,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
       const double gr = -(double)gsum + w_cur * isd2;
       // the prior and |g|^2 terms once per neuron group (row block 0)
       gsq = rb == 0 ? gr * gr : 0.0;
-      lpart += rb == 0 ? 0.5 * w_cur * w_cur * isd2 + lconst : 0.0;
+      lpart += rb == 0 ? 0.5 * w_cur * w_cur * isd2 + sLconst : 0.0;
       const double w_old = w_cur;
       if (!eval_only) {  // optax 0.2.2 scale_by_adam + scale(-lr)
         const double mu = (1.0 - p.b1) * gr + p.b1 * mu_cur;
@@ -721,31 +724,47 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
     p.stats[3] = loss0;
     p.count[0] = count0 + (eval_only ? 0 : (stop_j + 1));
   }
-}
-
-// Histories (fit_tuning_helper.py:147-149, :175-176) from the published partials, summed
-// in the decision's order: loss_hist[0] = loss of body 0, loss_hist[j+1] = loss of body j
-// (j + 1 < n_iter); the same for the gradient norm; final_error = norm of the last body.
-__global__ void __launch_bounds__(64) k_adam_hist(AdamParams p_arg) {
-  const AdamParams p = adam_view(p_arg);
-  const int lane = threadIdx.x;
-  const int n_iter = (int)p.stats[0];
-  if (n_iter <= 0) return;
-  for (int i = blockIdx.x; i < n_iter; i += gridDim.x) {
-    const int j = (i == 0) ? 0 : i - 1;
-    unsigned long long lv[kPartPerLane], gv[kPartPerLane];
+  // ---- histories (fit_tuning_helper.py:147-149, :175-176), entries i = g, g + G, ... ----
+  // loss_hist[0] = loss of body 0, loss_hist[i] = loss of body i - 1; the same for the
+  // gradient norm; final_error = the norm of the last body.  Summed in the decision's
+  // order (load_parts / sum_parts).  Every body <= stop_j has all its loss partials (the
+  // decision read them); its |g|^2 partials were stored right after them and are polled
+  // until they have landed.
+  if (ctl && !sCtl[2]) {
+    const int n_iter = eval_only ? 1 : stop_j + 2;
+    for (int i = g; i < n_iter; i += p.G) {
+      const int j = i == 0 ? 0 : i - 1;
+      unsigned long long lv[kPartPerLane], gv[kPartPerLane];
+      load_parts(p, j, lane, lv);
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      bool ok = false;
+      while (!ok) {
 #pragma unroll
-    for (int q = 0; q < kPartPerLane; ++q) {
-      const int gi = lane + 64 * q;
-      lv[q] = gi < p.G ? p.lpart[(size_t)j * p.G + gi] : 0ull;
-      gv[q] = gi < p.G ? p.gpart[(size_t)j * p.G + gi] : 0ull;
-    }
-    const double loss = sum_parts(lv);
-    const double err = sqrt(sum_parts(gv));
-    if (lane == 0) {
-      p.loss_hist[i] = loss;
-      p.err_hist[i] = err;
-      if (i == n_iter - 1) p.stats[2] = err;
+        for (int q = 0; q < kPartPerLane; ++q) {
+          const int gi = lane + 64 * q;
+          gv[q] = gi < p.G ? ld_bits(&p.gpart[(size_t)j * p.G + gi]) : 0ull;
+        }
+        ok = true;
+#pragma unroll
+        for (int q = 0; q < kPartPerLane; ++q) ok &= (gv[q] != kSentinel) && (lv[q] != kSentinel);
+        ok = __all(ok);
+        if (!ok) {
+          load_parts(p, j, lane, lv);
+          __builtin_amdgcn_s_sleep(1);
+          if (__builtin_amdgcn_s_memrealtime() - t0 > p.spin) {
+            if (lane == 0) atomicOr(p.timeout, 1);
+            break;
+          }
+        }
+      }
+      if (!ok) break;
+      const double loss = sum_parts(lv);
+      const double err = sqrt(sum_parts(gv));
+      if (lane == 0) {
+        p.loss_hist[i] = loss;
+        p.err_hist[i] = err;
+        if (i == n_iter - 1) p.stats[2] = err;
+      }
     }
   }
 }
@@ -985,8 +1004,6 @@ static int adam_run(double* W, double* mu, double* nu, int64_t* count, const flo
     PMG_LAUNCH_CHECK();
     // rg x G workgroups, at most one per CU (adam_batch_geometry): all co-resident
     PMG_HIP(launch_persistent(kern.fn, dim3(G, rg), dim3(kThreads), kern.lds, st, q));
-    hipLaunchKernelGGL(k_adam_hist, dim3(64, rg), dim3(64), 0, st, q);
-    PMG_LAUNCH_CHECK();
   }
   if (prof) {
     long long h[64 * 16];
