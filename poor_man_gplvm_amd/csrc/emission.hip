@@ -27,9 +27,11 @@
 namespace pmg {
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
+
 
 constexpr int kDig = 5;
 constexpr double kQScale = 4294967296.0;  // 2^32
@@ -519,7 +521,12 @@ __global__ void __launch_bounds__(1024) k_emission_pipe(
 // - LDS image: 8-row x 128-B pieces; row segment s sits at s ^ ((row >> 1) & 7) (DMA
 //   source and read), so the ds_read_b128 B-fragment reads of 16 rows hit 16 distinct
 //   bank quads.
-// - Per-latent constants (lconst) live in LDS for the whole launch; gconst rows in VGPRs.
+// - Per-latent constants (lconst) live in LDS for the whole launch.
+// - The MFMAs take the digit planes as the A operand and the spikes as B, so the output
+//   tile is transposed: a lane holds ONE time row (its gconst in one register) and 16 of
+//   the item's 32 latents, 4 runs of 4 consecutive ones.  The block max is then 15 register
+//   maxima and one half-wave swap per row (it was a 5-step cross-lane reduction per output
+//   row), and delta leaves as 16-B stores: emission 164 -> 140 us at C3.
 // Bit-identical to k_emission_i8 (same int32 digit sums, same f64 epilogue).
 constexpr int RT = 256, RLW = 32;                       // time bins, latents per work item
 constexpr int RLC_MAX = 4096;                            // latents of the LDS lconst table
@@ -531,17 +538,6 @@ template <int CK> struct YRing {
   static constexpr int RPP = 1024 / CK;                  // digit rows per piece
   static constexpr int NSEG = CK / 16;                   // 16-B segments per row
 };
-
-// 32-lane (half-wave) max of f32 values as order-preserving int keys: v_max_i32 folds the
-// DPP moves (no canonicalising max(x, x) as the f32 form needs); the key map is an involution
-__device__ __forceinline__ int fkey(float f) {
-  const int b = __float_as_int(f);
-  return b ^ (int)((unsigned)(b >> 31) >> 1);
-}
-template <int CTRL>
-__device__ __forceinline__ int dpp_imax(int v) {
-  return max(v, __builtin_amdgcn_update_dpp((int)0x80000000, v, CTRL, 0xf, 0xf, false));
-}
 
 template <int CK, int KC, bool LL, bool MASK>
 __global__ void __launch_bounds__(512) k_emission_yreg(
@@ -606,10 +602,13 @@ __global__ void __launch_bounds__(512) k_emission_yreg(
   for (int x = 0; x < RNS - 1 && x < S; ++x) PMG_YR_ISSUE(x)
 
   v4i ya[Kp / 32];                  // A fragments: y[t0 + 32 wid + r][32 ks + 16 h .. +16]
-  double gcr[16];                   // gconst of the lane's 16 output rows
+  double gcv = 0.0;                 // gconst of the lane's time row t0 + 32 wid + r
+  // VMEM stores per epilogue, a lower bound over both store forms (4 x 16 B delta + 1 rblk
+  // (+ 8 x 16 B ll) when L % 4 == 0, 16 + 1 (+ 16) otherwise): the counted waits below
+  // must never assume more younger stores than were issued
+  constexpr int NST = LL ? 13 : 5;
   v16i acc[kDig];
   int cur_tt = -1;
-  constexpr int NST = LL ? 48 : 32;  // VMEM stores per epilogue (k_emission_pipe's count)
   for (int xi = 0; xi < mine; ++xi) {
     const int it = i0 + xi;
     const int tt = it / nLT;
@@ -624,11 +623,10 @@ __global__ void __launch_bounds__(512) k_emission_yreg(
       const int8_t* yrow = yq + ty * Kp + 16 * h;
 #pragma unroll
       for (int ks = 0; ks < Kp / 32; ++ks) ya[ks] = *reinterpret_cast<const v4i*>(yrow + 32 * ks);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        int64_t tg = t0 + 32 * wid + 4 * h + (i & 3) + 8 * (i >> 2);
+      {
+        int64_t tg = t0 + 32 * wid + r;
         tg = tg < T ? tg : T - 1;
-        gcr[i] = gconst[tg];
+        gcv = gconst[tg];
       }
       __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
       cur_tt = tt;
@@ -650,14 +648,24 @@ __global__ void __launch_bounds__(512) k_emission_yreg(
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       }
       const int8_t* sq = smem + (x % RNS) * RSTAGE;
+      // B fragments one k-step ahead: the 5 reads of k-step ks + 1 are issued before ks's
+      // MFMAs (the scheduling barriers keep them there; hipcc's own schedule waited on each
+      // read right before its MFMA, 2 % of the kernel)
+      v4i bq[2][kDig];
+#pragma unroll
+      for (int d = 0; d < kDig; ++d) bq[0][d] = *reinterpret_cast<const v4i*>(sq + d * RLW * CK + bb);
 #pragma unroll
       for (int ks = 0; ks < CK / 32; ++ks) {
-        const int bo = bb ^ (32 * ks);
+        if (ks + 1 < CK / 32) {
+          const int bn = bb ^ (32 * (ks + 1));
 #pragma unroll
-        for (int d = 0; d < kDig; ++d) {
-          const v4i b = *reinterpret_cast<const v4i*>(sq + d * RLW * CK + bo);
-          acc[d] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ya[(CK / 32) * c + ks], b, acc[d], 0, 0, 0);
+          for (int d = 0; d < kDig; ++d) bq[(ks + 1) & 1][d] = *reinterpret_cast<const v4i*>(sq + d * RLW * CK + bn);
         }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int d = 0; d < kDig; ++d)
+          acc[d] = __builtin_amdgcn_mfma_i32_32x32x32_i8(bq[ks & 1][d], ya[(CK / 32) * c + ks], acc[d], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
         if (ks == 0) {
           // the next DMA behind the first k-step's MFMAs (their issue hides its SALU work)
           __builtin_amdgcn_sched_barrier(0);
@@ -667,76 +675,85 @@ __global__ void __launch_bounds__(512) k_emission_yreg(
       }
     }
 
-    // epilogue (k_emission_i8's arithmetic)
-    const int nblk = Lp >> 5;
-    const int blk = l0 >> 5;
-    const int l = l0 + r;
-    const bool lvalid = l < L;
-    const double lc = slc[l];
-    const int64_t nrow64 = T - t0 < RT ? T - t0 : RT;
-    const int nrow = (int)nrow64;
-    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(delta + t0 * (int64_t)L, (short)0,
-                                                                         nrow * L * 4, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(rblk + t0 * (int64_t)nblk, (short)0,
-                                                                         nrow * nblk * 8, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
-        LL ? (void*)(ll64 + t0 * (int64_t)L) : (void*)delta, (short)0, LL ? nrow * L * 8 : 0, 0x00020000);
-    const int trb = 32 * wid + 4 * h;
-    uint32_t od0 = lvalid ? (uint32_t)(trb * L + l) * 4u : 0x80000000u;
-    uint32_t ob0 = r == 0 ? (uint32_t)(trb * nblk + blk) * 8u : 0x80000000u;
-    uint32_t ol0 = lvalid ? (uint32_t)(trb * L + l) * 8u : 0x80000000u;
-    asm volatile("" : "+v"(od0), "+v"(ob0));
-    if constexpr (LL) asm volatile("" : "+v"(ol0));
-    // Two halves of 8 rows: (1) ll in f64 and its f32 block-max key, (2) the 8 half-wave
-    // max reductions interleaved, (3) outputs.  Digit pairs combine exactly in int32 first
-    // (|a0 + 256 a1| <= 127 * 128 * 512 * 257 < 2^31 for Kp <= 512), so q is the same
-    // integer as k_emission_i8's Horner sum.
+    // epilogue (k_emission_i8's arithmetic) on the transposed tile: the MFMAs ran with the
+    // operands swapped, so lane (r, h) holds time row t0 + 32 wid + r and, in register
+    // i = 4 g + e, latent l0 + 8 g + 4 h + e.  The block max over the item's 32 latents is
+    // a register max plus one half-wave swap, and each group of 4 latents one 16-B store.
+    {
+      const int nblk = Lp >> 5;
+      const int blk = l0 >> 5;
+      const int64_t nrow64 = T - t0 < RT ? T - t0 : RT;
+      const int nrow = (int)nrow64;
+      const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(delta + t0 * (int64_t)L, (short)0,
+                                                                           nrow * L * 4, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(rblk + t0 * (int64_t)nblk, (short)0,
+                                                                           nrow * nblk * 8, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+          LL ? (void*)(ll64 + t0 * (int64_t)L) : (void*)delta, (short)0, LL ? nrow * L * 8 : 0, 0x00020000);
+      const int tr = 32 * wid + r;
+      const bool tvalid = tr < nrow;
+      double vv[16];
+      float fm = -INFINITY;
 #pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-      double vv[8];
-      int kk[8];
+      for (int g = 0; g < 4; ++g) {
+        const double* lcg = slc + l0 + 8 * g + 4 * h;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int i = 8 * hf + j;
-        const int lo = acc[0][i] + (acc[1][i] << 8);
-        const int mid = acc[2][i] + (acc[3][i] << 8);
-        const double q = fma(fma((double)acc[4][i], 65536.0, (double)mid), 65536.0, (double)lo);
-        double v = q * kQInv + lc - gcr[i];   // lc = -lamsum: (q/2^32 - lamsum) - gc as k_emission_i8
-        if constexpr (MASK) v = v == INFINITY ? -1e20 : v;   // masked latent (lc = +inf)
-        vv[j] = v;                                            // padding latents: lc = -inf
-        kk[j] = fkey((float)v);
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) kk[j] = dpp_imax<0xB1>(kk[j]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) kk[j] = dpp_imax<0x4E>(kk[j]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) kk[j] = dpp_imax<0x141>(kk[j]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) kk[j] = dpp_imax<0x140>(kk[j]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const auto pr = __builtin_amdgcn_permlane16_swap(kk[j], kk[j], false, false);
-        kk[j] = max((int)pr[0], (int)pr[1]);
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int i = 8 * hf + j;
-        const int ri = (i & 3) + 8 * (i >> 2);
-        const double v = vv[j];
-        const double mx = (double)__int_as_float(fkey(__int_as_float(kk[j])));
-        const float dv = (float)(v - mx);
-        const uint32_t od = od0 + (uint32_t)(ri * L) * 4u;
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dv), rd, od, 0, 0);
-        if constexpr (LL) {
-          const unsigned long long vu = (unsigned long long)__double_as_longlong(v);
-          const uint32_t ol = ol0 + (uint32_t)(ri * L) * 8u;
-          __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)vu, (uint32_t)(vu >> 32)}, rl, ol, 0, 0);
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * g + e;
+          // digit pairs combine exactly in int32 first (|a0 + 256 a1| < 2^31 for Kp <= 512)
+          const int lo = acc[0][i] + (acc[1][i] << 8);
+          const int mid = acc[2][i] + (acc[3][i] << 8);
+          const double q = fma(fma((double)acc[4][i], 65536.0, (double)mid), 65536.0, (double)lo);
+          double v = q * kQInv + lcg[e] - gcv;   // lc = -lamsum: (q/2^32 - lamsum) - gc
+          if constexpr (MASK) v = v == INFINITY ? -1e20 : v;   // masked latent (lc = +inf)
+          vv[i] = v;                                            // padding latents: lc = -inf
+          fm = fmaxf(fm, (float)v);
         }
-        const uint32_t ob = ob0 + (uint32_t)(ri * nblk) * 8u;
-        const unsigned long long mu = (unsigned long long)__double_as_longlong(mx);
-        __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)mu, (uint32_t)(mu >> 32)}, rr, ob, 0, 0);
       }
+      {
+        const auto pr = __builtin_amdgcn_permlane32_swap(__float_as_int(fm), __float_as_int(fm), false, false);
+        fm = fmaxf(__int_as_float((int)pr[0]), __int_as_float((int)pr[1]));
+      }
+      const double mx = (double)fm;
+      const bool vec4 = (L & 3) == 0;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int lg = l0 + 8 * g + 4 * h;
+        float dv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dv[e] = (float)(vv[4 * g + e] - mx);
+        if (vec4) {
+          const uint32_t od = (tvalid && lg < L) ? (uint32_t)(tr * L + lg) * 4u : 0x80000000u;
+          __builtin_amdgcn_raw_buffer_store_b128(
+              (v4u){__float_as_uint(dv[0]), __float_as_uint(dv[1]), __float_as_uint(dv[2]), __float_as_uint(dv[3])},
+              rd, od, 0, 0);
+          if constexpr (LL) {
+            const uint32_t ol = (tvalid && lg < L) ? (uint32_t)(tr * L + lg) * 8u : 0x80000000u;
+            const unsigned long long a0 = __double_as_longlong(vv[4 * g]), a1 = __double_as_longlong(vv[4 * g + 1]);
+            const unsigned long long a2 = __double_as_longlong(vv[4 * g + 2]), a3 = __double_as_longlong(vv[4 * g + 3]);
+            __builtin_amdgcn_raw_buffer_store_b128(
+                (v4u){(uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32)}, rl, ol, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(
+                (v4u){(uint32_t)a2, (uint32_t)(a2 >> 32), (uint32_t)a3, (uint32_t)(a3 >> 32)}, rl,
+                ol == 0x80000000u ? ol : ol + 16u, 0, 0);
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool ok = tvalid && lg + e < L;
+            const uint32_t od = ok ? (uint32_t)(tr * L + lg + e) * 4u : 0x80000000u;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dv[e]), rd, od, 0, 0);
+            if constexpr (LL) {
+              const uint32_t ol = ok ? (uint32_t)(tr * L + lg + e) * 8u : 0x80000000u;
+              const unsigned long long vu = __double_as_longlong(vv[4 * g + e]);
+              __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)vu, (uint32_t)(vu >> 32)}, rl, ol, 0, 0);
+            }
+          }
+        }
+      }
+      const uint32_t ob = (h == 0 && tvalid) ? (uint32_t)(tr * nblk + blk) * 8u : 0x80000000u;
+      const unsigned long long mu = (unsigned long long)__double_as_longlong(mx);
+      __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)mu, (uint32_t)(mu >> 32)}, rr, ob, 0, 0);
     }
   }
 #undef PMG_YR_ISSUE

@@ -689,7 +689,7 @@ def test_emission_range_flag_raises():
 
 
 @pytest.mark.parametrize("L,T,N", [(512, 3000, 64), (100, 1000, 64), (256, 700, 64), (96, 1300, 300),
-                                   (512, 9000, 512), (160, 1500, 700)])
+                                   (512, 9000, 512), (160, 1500, 700), (130, 1100, 200), (37, 600, 64)])
 @pytest.mark.parametrize("with_ll,masked", [(True, False), (False, False), (False, True)])
 def test_emission_time_tile_invariant(L, T, N, with_ll, masked, monkeypatch):
     """The int8-MFMA emission kernels -- k_emission_i8 with one or two 32-step time
