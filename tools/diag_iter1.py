@@ -20,7 +20,6 @@ def main():
     ap.add_argument("--iters", type=int, default=4)
     ap.add_argument("--warms", default="48,128")
     ap.add_argument("--out", default=None)
-    ap.add_argument("--first", default="0", help="ScanConfig.first_warmup values, comma list")
     ap.add_argument("--segs", default="0", help="relaxation segments per sequence, comma list (0: library default)")
     a = ap.parse_args()
     import numpy as np
@@ -33,9 +32,8 @@ def main():
     dev = torch.device("cuda", 0)
     adam = AdamConfig(lr=0.01, maxiter=1000, tol=1e-6, prior_std=1.0)
     lines = []
-    for warm, segs, first in [(int(w), int(sg), int(f)) for w in a.warms.split(",") for sg in a.segs.split(",")
-                              for f in a.first.split(",")]:
-        eng = DeviceEM(SpikeData(y), L, basis=B, scan=ScanConfig(warmup=warm, relax_segments=segs, first_warmup=first))
+    for warm, segs in [(int(w), int(sg)) for w in a.warms.split(",") for sg in a.segs.split(",")]:
+        eng = DeviceEM(SpikeData(y), L, basis=B, scan=ScanConfig(warmup=warm, relax_segments=segs))
         eng.adaptive = True
         eng.set_transition(banded_transition(L, 1.0, 0.01, 0.01))
         W = torch.empty((B.shape[1], N), dtype=torch.float64, device=dev)
@@ -66,7 +64,7 @@ def main():
                 eng.timer = None
                 if rep:
                     s = timer.summary()
-                    line = {"warm": warm, "segs": segs, "first": first, "iter": i + 1, "wall_ms": round(1e3 * wall, 3),
+                    line = {"warm": warm, "segs": segs, "iter": i + 1, "wall_ms": round(1e3 * wall, 3),
                             "sections_ms": {k: round(v[1], 4) for k, v in s.items()},
                             "repairs": list(eng.repairs()), "relax_rounds": list(eng.relax_rounds()),
                             "adam_iters": float(stats[i, 0].item()), "logz": float(logz[i].item())}
