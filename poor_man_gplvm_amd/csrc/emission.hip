@@ -37,47 +37,64 @@ constexpr int kDig = 5;
 constexpr double kQScale = 4294967296.0;  // 2^32
 constexpr double kQInv = 1.0 / 4294967296.0;
 
-// One wave per latent row: log(lam) -> 5 int8 digits, lamsum = sum_n m_n lam, and the
-// pipelined kernel's per-latent constant lconst = -lamsum (+inf: latent masked by
-// ma_latent, -inf: padding row l >= L).
+// One 4-wave workgroup per latent row: log(lam) -> 5 int8 digits, lamsum = sum_n m_n lam,
+// and the pipelined kernel's per-latent constant lconst = -lamsum (+inf: latent masked by
+// ma_latent, -inf: padding row l >= L).  Wave w takes the neuron groups j = w, w + 4, ...
+// (neurons n = 64 j + lane); the products m_n lam pass through LDS so wave 0 adds each
+// lane's values in ascending j, the order of a one-wave-per-row loop.
+constexpr int kRpBlk = 16;   // neuron groups per LDS round
 __global__ void __launch_bounds__(256) k_rates_prepare(
     const double* __restrict__ tuning, int L, int N, const float* __restrict__ ma, double dt,
     int Lp, int Kp, int8_t* __restrict__ qd, double* __restrict__ lamsum, int* __restrict__ bad,
     const uint8_t* __restrict__ ma_latent, double* __restrict__ lconst) {
-  const int lane = threadIdx.x & 63;
-  const int l = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (l >= Lp) return;
+  __shared__ double sml[kRpBlk][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int l = blockIdx.x;
+  if (l >= Lp) return;                                      // uniform per workgroup
   const size_t plane = (size_t)Lp * Kp;
+  const int nj = Kp / 64;
   double ls = 0.0;
   int flag = 0;
-  for (int n = lane; n < Kp; n += 64) {
-    int8_t dg[kDig] = {0, 0, 0, 0, 0};
-    if (l < L && n < N) {
-      const double lam = tuning[(size_t)l * N + n] * dt + 1e-20;
-      const double lg = log(lam);
-      if (!(fabs(lg) < 60.0)) flag = 1;
-      long long q = llrint(lg * kQScale);
+  for (int jb = 0; jb < nj; jb += kRpBlk) {
+    for (int j = jb + w; j < nj && j < jb + kRpBlk; j += 4) {
+      const int n = 64 * j + lane;
+      int8_t dg[kDig] = {0, 0, 0, 0, 0};
+      double mlam = 0.0;
+      if (l < L && n < N) {
+        const double lam = tuning[(size_t)l * N + n] * dt + 1e-20;
+        const double lg = log(lam);
+        if (!(fabs(lg) < 60.0)) flag = 1;
+        long long q = llrint(lg * kQScale);
 #pragma unroll
-      for (int d = 0; d < kDig - 1; ++d) {
-        const long long rr = ((q + 128) & 255) - 128;
-        dg[d] = (int8_t)rr;
-        q = (q - rr) >> 8;
+        for (int d = 0; d < kDig - 1; ++d) {
+          const long long rr = ((q + 128) & 255) - 128;
+          dg[d] = (int8_t)rr;
+          q = (q - rr) >> 8;
+        }
+        dg[kDig - 1] = (int8_t)q;  // |q| <= 61 for |lg| < 60
+        const float m = ma ? ma[n] : 1.f;
+        mlam = (double)m * lam;
       }
-      dg[kDig - 1] = (int8_t)q;  // |q| <= 61 for |lg| < 60
-      const float m = ma ? ma[n] : 1.f;
-      ls += (double)m * lam;
-    }
-    const size_t o = (size_t)l * Kp + n;
+      sml[j - jb][lane] = mlam;
+      const size_t o = (size_t)l * Kp + n;
 #pragma unroll
-    for (int d = 0; d < kDig; ++d) qd[d * plane + o] = dg[d];
+      for (int d = 0; d < kDig; ++d) qd[d * plane + o] = dg[d];
+    }
+    __syncthreads();
+    if (w == 0 && l < L)
+      for (int j = jb; j < nj && j < jb + kRpBlk; ++j)
+        if (64 * j + lane < N) ls += sml[j - jb][lane];
+    __syncthreads();
   }
-  ls = wave_sum_f64(ls);
-  if (lane == 0) {
-    lamsum[l] = ls;
-    lconst[l] = l >= L ? -INFINITY : (ma_latent && ma_latent[l] == 0) ? INFINITY : -ls;
+  if (__syncthreads_or(flag)) {
+    if (threadIdx.x == 0) atomicOr(bad, 1);
   }
-  if (__ballot(flag)) {
-    if (lane == 0) atomicOr(bad, 1);
+  if (w == 0) {
+    ls = wave_sum_f64(ls);
+    if (lane == 0) {
+      lamsum[l] = ls;
+      lconst[l] = l >= L ? -INFINITY : (ma_latent && ma_latent[l] == 0) ? INFINITY : -ls;
+    }
   }
 }
 
@@ -922,7 +939,7 @@ int pmg_emission_poisson(const int8_t* yq, const double* gconst, const double* t
   double* lamsum = c.take<double>(Lp);
   int* bad = c.take<int>(4);   // sticky range flag (zero-filled workspace; the caller clears it)
   double* lconst = c.take<double>(Lp);
-  hipLaunchKernelGGL(k_rates_prepare, dim3((Lp + 3) / 4), dim3(256), 0, st, tuning64, L, N,
+  hipLaunchKernelGGL(k_rates_prepare, dim3(Lp), dim3(256), 0, st, tuning64, L, N,
                      ma_neuron_1d, dt, Lp, Kp, qd, lamsum, bad, ma_latent, lconst);
   PMG_LAUNCH_CHECK();
   const int64_t Tp = round_up(T, 64);   // rows of yq (pmg_spikes_prepare zero-pads to Tp)
