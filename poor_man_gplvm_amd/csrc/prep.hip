@@ -103,8 +103,9 @@ __global__ void __launch_bounds__(256) k_rowref(const double* __restrict__ rblk,
   const int b = lane % NBP;
   const int nb = nblk / R;
   const bool live = row < T * R && b < nb;
-  const int64_t t = live ? row / R : 0;
-  const int g = live ? (int)(row - t * R) : 0;
+  // R == 1 (one model): no 64-bit division by R (a ~150-instruction sequence per lane)
+  const int64_t t = !live ? 0 : R == 1 ? row : row / R;
+  const int g = live && R != 1 ? (int)(row - t * R) : 0;
   const int64_t o = t * nblk + (int64_t)g * nb + b;
   const double v = live ? rblk[o] : -INFINITY;
   double mx = v;
