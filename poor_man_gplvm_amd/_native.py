@@ -232,7 +232,7 @@ class HostBuffer:
     """Page-locked host memory from pmg_host_alloc (first-touched by several threads as
     huge pages, then registered with HIP), exposed through the numpy array interface.
     When the last array viewing it goes away the block returns to a process-wide cache
-    (up to HOST_CACHE_BYTES; beyond that it is unregistered and unmapped), so repeated
+    (at most HOST_CACHE_BYTES, least recently returned blocks evicted first), so repeated
     fits and decodes of one shape reuse their buffers instead of re-pinning (allocation
     ~4 ms and release ~20 ms per 410 MB)."""
 
@@ -251,12 +251,25 @@ class HostBuffer:
 
     def __del__(self):
         ptr, self.ptr = getattr(self, 'ptr', None), None
-        if ptr and not _host_cache_give(ptr, self.nbytes):
-            self._lib.pmg_host_free(ptr, self.nbytes)
+        if ptr:
+            _host_cache_give(ptr, self.nbytes, self._lib)
 
 
-HOST_CACHE_BYTES = 8 << 30
-_host_cache = {}            # nbytes -> [ptr, ...]
+def _default_cache_bytes():
+    """PMG_HOST_CACHE_BYTES, else min(2 GiB, 1/32 of the host's physical memory): page-locked
+    memory cannot be swapped and every rank of a node holds its own cache."""
+    env = os.environ.get("PMG_HOST_CACHE_BYTES")
+    if env:
+        return max(0, int(env))
+    try:
+        phys = os.sysconf("SC_PAGE_SIZE") * os.sysconf("SC_PHYS_PAGES")
+    except (ValueError, OSError, AttributeError):
+        phys = 64 << 30
+    return int(min(2 << 30, phys // 32))
+
+
+HOST_CACHE_BYTES = _default_cache_bytes()
+_host_cache = []            # [(nbytes, ptr)], least recently returned first
 _host_cache_total = 0
 _host_cache_lock = threading.Lock()
 
@@ -264,28 +277,46 @@ _host_cache_lock = threading.Lock()
 def _host_cache_take(nbytes):
     global _host_cache_total
     with _host_cache_lock:
-        q = _host_cache.get(nbytes)
-        if q:
-            _host_cache_total -= nbytes
-            return q.pop()
+        for i in range(len(_host_cache) - 1, -1, -1):
+            if _host_cache[i][0] == nbytes:
+                _host_cache_total -= nbytes
+                return _host_cache.pop(i)[1]
     return None
 
 
-def _host_cache_give(ptr, nbytes):
+def _host_cache_give(ptr, nbytes, lib=None):
+    """Return a block to the cache, evicting the least recently returned blocks to stay
+    within HOST_CACHE_BYTES; a block larger than the cap is released at once."""
     global _host_cache_total
+    evict = []
     with _host_cache_lock:
-        if _host_cache_total + nbytes > HOST_CACHE_BYTES:
-            return False
-        _host_cache.setdefault(nbytes, []).append(ptr)
-        _host_cache_total += nbytes
-        return True
+        if nbytes > HOST_CACHE_BYTES:
+            evict.append((ptr, nbytes))
+        else:
+            while _host_cache and _host_cache_total + nbytes > HOST_CACHE_BYTES:
+                n, p = _host_cache.pop(0)
+                _host_cache_total -= n
+                evict.append((p, n))
+            _host_cache.append((nbytes, ptr))
+            _host_cache_total += nbytes
+    if evict:
+        lib = lib or load()
+        for p, n in evict:
+            lib.pmg_host_free(p, n)
+    return True
+
+
+def host_cache_bytes():
+    """Bytes of page-locked blocks held by the cache."""
+    with _host_cache_lock:
+        return _host_cache_total
 
 
 def release_host_cache():
     """Unregister and unmap every cached page-locked block."""
     global _host_cache_total
     with _host_cache_lock:
-        items = [(p, n) for n, q in _host_cache.items() for p in q]
+        items = [(p, n) for n, p in _host_cache]
         _host_cache.clear()
         _host_cache_total = 0
     lib = load()

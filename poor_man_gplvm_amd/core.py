@@ -67,15 +67,24 @@ class _PinnedCopies:
     synchronises and returns; the buffers are the numpy arrays handed to the caller."""
 
     SMALL = 4 << 20
+    # page-locked bytes reserved ahead of the loop for snapshots; further snapshots get
+    # their buffer when they are submitted (a small save_every must not pin n_iter copies
+    # of (T, 2, L) up front)
+    RESERVE_BYTES = 2 << 30
 
     def __init__(self, dev):
         from concurrent.futures import ThreadPoolExecutor
         self.dev = dev
         self.side = torch.cuda.Stream(dev)
         self.items = []
-        self.keep = []
         self.reserved = {}
         self.pool = ThreadPoolExecutor(max_workers=1)
+
+    def reserve_upto(self, key, shape, count, dtype=torch.float32):
+        """reserve() up to `count` buffers, within RESERVE_BYTES."""
+        nbytes = int(np.prod(shape)) * torch.tensor([], dtype=dtype).element_size()
+        for _ in range(min(int(count), max(1, self.RESERVE_BYTES // max(nbytes, 1)))):
+            self.reserve(key, shape, dtype)
 
     def reserve(self, key, shape, dtype=torch.float32):
         """Start allocating a host buffer for a later submit(..., key=key)."""
@@ -83,11 +92,15 @@ class _PinnedCopies:
             self.pool.submit(nat.host_array, tuple(shape), _NP_DTYPE[dtype]))
 
     def submit(self, t, key=None, side=False):
-        """Copy device tensor t (not written again before finish) to a pinned buffer."""
+        """Copy device tensor t (not written again before finish) to a pinned buffer.
+        The caller may drop t at once: a side-stream copy records its use on the side
+        stream, so the caching allocator frees the memory only after the copy (same-stream
+        copies are ordered before any later use of the memory anyway)."""
         t = t.contiguous()
         cur = torch.cuda.current_stream(self.dev)
         if side:
             self.side.wait_stream(cur)
+            t.record_stream(self.side)
         st = self.side if side else cur
         nbytes = t.numel() * t.element_size()
         q = self.reserved.get(key)
@@ -103,14 +116,12 @@ class _PinnedCopies:
                 raise ValueError("reserved host buffer does not match the tensor")
             nat.check(nat.load().pmg_copy_d2h(host.ctypes.data, t.data_ptr(), nbytes, st.cuda_stream),
                       "pmg_copy_d2h")
-        self.keep.append(t)            # alive until the copy is done (finish)
         self.items.append(host)
         return host
 
     def finish(self):
         torch.cuda.current_stream(self.dev).synchronize()
         self.side.synchronize()
-        self.keep.clear()
         self.pool.shutdown(wait=False)
         return self.items
 
@@ -809,8 +820,7 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
     # copies are fresh tensors), the final arrays after the loop
     cp = _PinnedCopies(dev)
     n_saved = len(range(0, n_iter, save_every))
-    for _ in range(n_saved):
-        cp.reserve('snap', (T, 2, L))
+    cp.reserve_upto('snap', (T, 2, L), n_saved)
     for key, shape in (('post', (T, 2, L)), ('lpf', (T, 2, L)), ('plm', (T, L))):
         cp.reserve(key, shape)
     saved_dev = []      # (i, log posterior, W f32, tuning) pinned host buffers per snapshot

@@ -109,6 +109,11 @@ class ScanConfig:
         return 2 * self.chunk_for(T)
 
 
+def planes_ok(T, ld):
+    """pmg_suffstats_bf16x3's operand bounds: ld % 8 == 0 and planes below 2 GiB."""
+    return ld % 8 == 0 and T * ld * 2 < (1 << 31)
+
+
 def default_device():
     if not torch.cuda.is_available():
         raise nat.NativeError("poor_man_gplvm_amd needs a ROCm GPU (torch.cuda.is_available() is False)")
@@ -261,7 +266,7 @@ class DeviceEM:
         self._P = torch.empty((T, L), dtype=f32, device=dev)
         # integer spikes: the backward writes P as its three exact bf16 planes, the operands
         # of the statistics GEMMs (PMG_PHASE_P_BF16X3), instead of f32 P
-        self.use_planes = bool(self.PLANES and spikes.ybt is not None and L % 8 == 0)
+        self.use_planes = bool(self.PLANES and spikes.ybt is not None and planes_ok(T, L))
         self.Pq = torch.empty((3, T, L), dtype=torch.int16, device=dev) if self.use_planes else None
         self._p_fresh = 'f32'       # which of _P / Pq holds the current posterior marginal
         self.tuning64 = torch.empty((L, N), dtype=f64, device=dev)
@@ -275,7 +280,8 @@ class DeviceEM:
         self.ws_fb = torch.zeros(int(self.lib.pmg_fwdbwd_workspace_size(T, L, min(self.C, self.Cb))),
                                  dtype=torch.uint8, device=dev)
         ss_bytes = (max(self.lib.pmg_suffstats_bf16_workspace_size(T, L, N),
-                        self.lib.pmg_suffstats_bf16x3_workspace_size(T, L, N)) if spikes.ybt is not None
+                        self.lib.pmg_suffstats_bf16x3_workspace_size(T, L, N) if self.use_planes else 0)
+                    if spikes.ybt is not None
                     else self.lib.pmg_suffstats_workspace_size(T, L, spikes.Np))
         self.ws_ss = torch.empty(int(ss_bytes), dtype=torch.uint8, device=dev)
         if self.ws_fb.numel() == 0 and L <= 1024:
@@ -939,7 +945,7 @@ class RestartBatchEM:
         # as DeviceEM: P as its exact bf16 planes between the backward and the statistics
         # (both the batched and the one-restart fit take the same statistics kernel, so a
         # restart alone on the batch's grid reproduces its batched fit)
-        self.use_planes = bool(self.PLANES and spikes.ybt is not None)
+        self.use_planes = bool(self.PLANES and spikes.ybt is not None and planes_ok(T, LA))
         self.Pq = torch.empty((3, T, LA), dtype=torch.int16, device=dev) if self.use_planes else None
         self._p_fresh = 'f32'
         self.tuning64 = torch.empty((LA, N), dtype=f64, device=dev)
@@ -954,7 +960,8 @@ class RestartBatchEM:
         self.ws_fb = torch.zeros(fb, dtype=torch.uint8, device=dev)    # zero-filled once (include/pmg.h)
         self.slab = (fb // R) & ~255 if R > 1 else fb
         ss_bytes = (max(self.lib.pmg_suffstats_bf16_workspace_size(T, LA, N),
-                        self.lib.pmg_suffstats_bf16x3_workspace_size(T, LA, N)) if spikes.ybt is not None
+                        self.lib.pmg_suffstats_bf16x3_workspace_size(T, LA, N) if self.use_planes else 0)
+                    if spikes.ybt is not None
                     else self.lib.pmg_suffstats_workspace_size(T, LA, spikes.Np))
         self.ws_ss = torch.empty(int(ss_bytes), dtype=torch.uint8, device=dev)
         self.ws_ad = AdamWorkspace(self.lib, self.dev)

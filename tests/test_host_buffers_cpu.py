@@ -21,16 +21,38 @@ def test_host_alloc_fails_cleanly_without_gpu():
 
 
 def test_host_cache_accounting(monkeypatch):
+    """The cache holds at most HOST_CACHE_BYTES: returning a block that does not fit
+    evicts the least recently returned blocks (unmapped at once), and a block larger than
+    the whole cap is released instead of cached."""
+    freed = []
+    fake = type("L", (), {"pmg_host_free": lambda self, p, n: freed.append((p, n))})()
+    monkeypatch.setattr(nat, "load", lambda: fake)
     monkeypatch.setattr(nat, "HOST_CACHE_BYTES", 3 * 4096)
-    monkeypatch.setattr(nat, "_host_cache", {})
+    monkeypatch.setattr(nat, "_host_cache", [])
     monkeypatch.setattr(nat, "_host_cache_total", 0)
     assert nat._host_cache_give(0x1000, 4096) and nat._host_cache_give(0x2000, 4096)
-    assert nat._host_cache_give(0x3000, 8192) is False          # over the cap: the caller frees it
-    assert nat._host_cache_total == 8192
-    assert nat._host_cache_take(8192) is None                   # no block of that size
-    assert nat._host_cache_take(4096) in (0x1000, 0x2000)
-    assert nat._host_cache_total == 4096
-    freed = []
-    monkeypatch.setattr(nat, "load", lambda: type("L", (), {"pmg_host_free": lambda self, p, n: freed.append((p, n))})())
+    assert nat._host_cache_give(0x3000, 8192)                   # evicts 0x1000, the oldest
+    assert freed == [(0x1000, 4096)] and nat.host_cache_bytes() == 3 * 4096
+    assert nat._host_cache_give(0x4000, 4 * 4096)               # larger than the cap: freed
+    assert freed[-1] == (0x4000, 4 * 4096) and nat.host_cache_bytes() == 3 * 4096
+    assert nat._host_cache_take(8192) == 0x3000
+    assert nat._host_cache_take(8192) is None                   # no block of that size left
+    assert nat.host_cache_bytes() == 4096
     nat.release_host_cache()
-    assert len(freed) == 1 and nat._host_cache_total == 0 and nat._host_cache == {}
+    assert freed[-1] == (0x2000, 4096) and nat._host_cache_total == 0 and nat._host_cache == []
+
+
+def test_host_cache_default_cap():
+    """Default cap: at most 2 GiB and at most 1/32 of physical memory; the environment
+    variable overrides it."""
+    import os
+    assert 0 < nat._default_cache_bytes() <= 2 << 30
+    old = os.environ.get("PMG_HOST_CACHE_BYTES")
+    os.environ["PMG_HOST_CACHE_BYTES"] = "12345"
+    try:
+        assert nat._default_cache_bytes() == 12345
+    finally:
+        if old is None:
+            del os.environ["PMG_HOST_CACHE_BYTES"]
+        else:
+            os.environ["PMG_HOST_CACHE_BYTES"] = old
