@@ -227,7 +227,10 @@ def bench_timeshard(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    if world > 1:
+    # RCCL whenever torchrun launched us (also at one rank: the DistComm / RCCL path of
+    # the time shards then runs its collectives on device buffers), else virtual shards
+    rccl = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
+    if rccl:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         world = dist.get_world_size()       # n_gpus = the world RCCL sees
     from poor_man_gplvm_amd.engine import AdamConfig, ScanConfig, KernelTimer
@@ -238,7 +241,7 @@ def bench_timeshard(args):
     t_syn = time.perf_counter()
     y, B, W0, lp0 = synth_long(N, T, L) if T > 200000 else synth(N, T, L)
     t_syn = time.perf_counter() - t_syn
-    comm = DistComm() if world > 1 else LocalComm(args.virtual)
+    comm = DistComm() if rccl else LocalComm(args.virtual)
     scan = ScanConfig(chunk=args.chunk or None, warmup=args.warm_steps)
     lays = shard_layout(T, comm.world, chunk=args.chunk or None, halo=args.halo, scan=scan)
     eng = TimeShardedEM(y, B, banded_transition(L, 1.0, 0.01, 0.01), comm, lays, scan,
@@ -287,17 +290,17 @@ def bench_timeshard(args):
     torch.cuda.synchronize()
     timer = KernelTimer()
     eng.set_timer(timer)
-    if world > 1:
+    if rccl:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.warmup, n_all):
         em_iter(i)
     torch.cuda.synchronize()
-    if world > 1:
+    if rccl:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if rccl:
         te = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
         elapsed = float(te.item())
@@ -341,9 +344,10 @@ def bench_timeshard(args):
         "warmup_iteration_s": [round(v, 4) for v in warm_s],
         "synth_s": round(t_syn, 1),
     }
+    out["comm"] = "rccl" if rccl else f"local x{args.virtual}"
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if rccl:
         dist.destroy_process_group()
 
 

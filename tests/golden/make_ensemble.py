@@ -1,5 +1,5 @@
 """Rounding-ensemble fixtures for the long M-step tests (run from the repo root:
-`python tests/golden/make_ensemble.py [adam|c1|c3] [workers]`).
+`python tests/golden/make_ensemble.py [adam|c1|c3|c4] [workers]`).
 
 A long Adam loop at the C3 shape is chaotic at the f64 ulp: after ~650 bodies, elements
 with gradients near zero take +-lr steps whose sign is decided by rounding, so two f64
@@ -18,6 +18,10 @@ Fixtures:
                         fit_em n_iter=20, maxiter 1000, tol 1e-6), base run + ensemble
   c3_em_ensemble.npz    the one-EM-iteration C3 case of c3_sample.npz (864 Adam bodies,
                         then the E-step at T=5000): ensemble spread of tuning and posterior
+  adam_c4_ensemble.npz  the first M-step of the C4 shape (N = L = 1024, 154 basis columns,
+                        T = 1e6: bench.synth_long), the 1000-body loop under tol 1e-6, on
+                        the statistics of the posterior init (P = f32(exp(lp0)), as the
+                        device sets it); the test runs it through the time-sharded path
 Test infrastructure only (imports the oracle)."""
 import os
 import sys
@@ -153,13 +157,65 @@ def c3_case(pool):
           % (max(tun_dev), np.median(tun_dev), max(post_dev), max(tw_dev), max(lml_dev), flips))
 
 
+# ----------------------------------------------------------------------------- C4 first M-step
+C4 = dict(N=1024, T=1000000, L=1024)
+C4_STATS = os.path.join(os.environ.get('TMPDIR', '/tmp'), 'pmg_c4_first_mstep_stats.npz')
+
+
+def _c4_stats():
+    """y_w = P^T y, t_w = sum_t P over the whole C4 recording, P = f32(exp(lp0)) (the
+    device's pmg_exp of the f32 posterior init), accumulated in f64 per 10k-row block."""
+    if os.path.exists(C4_STATS):
+        z = np.load(C4_STATS)
+        return z['W0'], z['B'], z['yw'], z['tw']
+    from bench import synth_long
+    y, B, W0, lp0 = synth_long(C4['N'], C4['T'], C4['L'])
+    yw = np.zeros((C4['L'], C4['N']))
+    tw = np.zeros(C4['L'])
+    for k in range(0, C4['T'], 10000):
+        P = np.exp(np.asarray(lp0[k:k + 10000], np.float64)).astype(np.float32).astype(np.float64)
+        yb = np.asarray(y[k:k + 10000], np.float64)
+        yw += P.T @ yb
+        tw += P.sum(0)
+    W0, B = W0.astype(np.float64), B.astype(np.float64)
+    np.savez(C4_STATS, W0=W0, B=B, yw=yw, tw=tw)
+    return W0, B, yw, tw
+
+
+def _c4_member(k):
+    W0, B, yw, tw = _c4_stats()
+    if k >= 0:
+        rng = np.random.default_rng(4000 + k)
+        yw = yw * (1 + EPS * rng.standard_normal(yw.shape))
+        tw = tw * (1 + EPS * rng.standard_normal(tw.shape))
+    r = O.adam_run(W0, O.adam_init(W0), 1.0, B, yw, tw, maxiter=1000, tol=1e-6)
+    return k, r['params'], r['n_iter'], r['loss_history'][:r['n_iter']]
+
+
+def c4_case(pool):
+    W0, B, yw, tw = _c4_stats()       # once, before the members load it
+    res = dict((k, (p, n, lh)) for k, p, n, lh in pool.map(_c4_member, range(-1, K)))
+    p0, n0, lh0 = res[-1]
+    t0 = O.get_tuning_softplus(p0, B)
+    tun_dev = [_rel(O.get_tuning_softplus(res[k][0], B), t0) for k in range(K)]
+    n_iter = [res[k][1] for k in range(K)]
+    lh_dev = [_rel(res[k][2][:min(n0, res[k][1])], lh0[:min(n0, res[k][1])]) for k in range(K)]
+    rows = np.random.default_rng(7).choice(C4['L'], 16, replace=False)
+    np.savez_compressed(os.path.join(HERE, 'adam_c4_ensemble.npz'), params=p0, n_iter=n0, loss_history=lh0,
+                        ens_tuning_dev=np.array(tun_dev), ens_n_iter=np.array(n_iter),
+                        ens_loss_history_dev=np.array(lh_dev), eps=EPS, tw=tw, yw_rows=rows,
+                        yw_sample=yw[rows], yw_total=yw.sum())
+    print('adam C4: n_iter', n0, 'ensemble n_iter', sorted(set(n_iter)), 'tuning dev max %.3e median %.3e'
+          % (max(tun_dev), np.median(tun_dev)), 'loss history dev max %.1e' % max(lh_dev))
+
+
 def main():
     which = sys.argv[1:2] or ['adam', 'c1', 'c3']
     workers = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     os.environ.setdefault('OMP_NUM_THREADS', '1')
     with get_context('spawn').Pool(workers) as pool:
         for w in which:
-            {'adam': adam_case, 'c1': c1_case, 'c3': c3_case}[w](pool)
+            {'adam': adam_case, 'c1': c1_case, 'c3': c3_case, 'c4': c4_case}[w](pool)
 
 
 if __name__ == '__main__':

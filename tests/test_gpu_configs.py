@@ -257,6 +257,72 @@ def test_c4_time_sharded_vs_single():
     assert torch.equal(torch.argmax(Psh, 1)[clear], torch.argmax(P1, 1)[clear])
 
 
+def test_c4_stop_rule_time_sharded_vs_f64_ensemble():
+    """C4's first M-step under the reference's stop rule (fit_tuning_helper.py:154-164:
+    maxiter 1000, tol 1e-6) on the time-sharded path at its own size: N = L = 1024 (154
+    basis columns), T = 1e6 (bench.synth_long), 8 time shards (virtual, one GPU: LocalComm
+    plays RCCL's part), statistics all-reduced over the shards, then the neuron-sharded
+    speculative Adam (each shard its own 128-neuron block, the loss partials reduced per
+    16-body batch, the host applying the stop rule and replaying to the stop body).
+    Against tests/golden/adam_c4_ensemble.npz (make_ensemble.c4_case): the f64 oracle's
+    loop on the statistics of the same posterior init, plus K = 16 runs whose statistics
+    are perturbed by 1e-15 relative (member k seeded 4000 + k).  Bars: the statistics
+    match the oracle's (the device's f32 exp of the init rounds P within an ulp: 1e-7);
+    the iteration count is the oracle's or one the ensemble reached; the loss history
+    within rel 1e-9 or 1.5x the ensemble's; tuning within 1.5x the ensemble's spread,
+    capped at 3.5e-4 (measured: all 17 oracle runs stop after 812 bodies, their loss
+    histories agree to 1.7e-11, their tuning ends up to 2.0e-4 apart)."""
+    import sys
+    import poor_man_gplvm_amd as P
+    from poor_man_gplvm_amd.timeshard import LocalComm, TimeShardedEM, shard_layout
+    sys.path.insert(0, os.path.dirname(HERE))
+    from bench import synth_long
+    from oracle import gplvm_oracle as O
+    e = np.load(os.path.join(HERE, 'golden', 'adam_c4_ensemble.npz'))
+    assert len(e['ens_tuning_dev']) == 16 and float(e['eps']) == 1e-15
+    N, T, L, R = 1024, 1000000, 1024, 8
+    y, B, W0, lp0 = synth_long(N, T, L)
+    sc = P.ScanConfig()
+    lays = shard_layout(T, R, halo=512, scan=sc)
+    eng = TimeShardedEM(y, B, P.banded_transition(L, 1.0), LocalComm(R), lays, sc, neuron_sharded=True)
+    for s in eng.shards:
+        s.set_log_posterior(np.asarray(lp0[s.lay.ext_start:s.lay.ext_stop]))
+    dev = torch.device('cuda', 0)
+    f64 = torch.float64
+    W = torch.as_tensor(W0.astype(np.float64), device=dev).contiguous()
+    Ws = [W] + [W.clone() for _ in range(R - 1)]
+    mus = [torch.zeros_like(W) for _ in range(R)]
+    nus = [torch.zeros_like(W) for _ in range(R)]
+    cnts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(R)]
+    st = torch.zeros(4, dtype=f64, device=dev)
+    lh = torch.zeros(1000, dtype=f64, device=dev)
+    eh = torch.zeros(1000, dtype=f64, device=dev)
+    eng.m_step(Ws, mus, nus, cnts, P.AdamConfig(maxiter=1000, tol=1e-6), st, lh, eh)
+    for s in eng.shards:
+        s.check_status()
+    yw = eng.shards[0].yw.cpu().numpy()
+    tw = eng.shards[0].tw.cpu().numpy()
+    np.testing.assert_allclose(tw, e['tw'], rtol=1e-7)
+    np.testing.assert_allclose(yw[e['yw_rows']], e['yw_sample'], rtol=1e-7, atol=1e-9)
+    n = int(st[0].item())
+    n0 = int(e['n_iter'])
+    assert n == n0 or n in set(e['ens_n_iter'].tolist()), (n, n0, sorted(set(e['ens_n_iter'].tolist())))
+    k = min(n, n0)
+    lh_bar = max(1e-9, 1.5 * float(np.max(e['ens_loss_history_dev'])))
+    lh_dev = float(np.max(np.abs(lh.cpu().numpy()[:k] / e['loss_history'][:k] - 1)))
+    tun = O.get_tuning_softplus(Ws[0].cpu().numpy(), B.astype(np.float64))
+    ref = O.get_tuning_softplus(e['params'], B.astype(np.float64))
+    tun_dev = float(np.max(np.abs(tun / ref - 1)))
+    tun_bar = min(1.5 * float(np.max(e['ens_tuning_dev'])), 3.5e-4)
+    print(f"C4 first M-step, 8 time shards, neuron-sharded Adam: n_iter {n} (oracle {n0}, ensemble "
+          f"{sorted(set(e['ens_n_iter'].tolist()))}), loss history {lh_dev:.2e} (bar {lh_bar:.2e}), "
+          f"tuning {tun_dev:.3e} (bar {tun_bar:.3e})")
+    assert lh_dev <= lh_bar
+    assert tun_dev <= tun_bar
+    for Wr in Ws[1:]:       # every shard holds the gathered W
+        assert torch.equal(Wr, Ws[0])
+
+
 def test_c5_restarts():
     from poor_man_gplvm_amd import model_selection_helper as MS
     N, L, T, R = 256, 256, 50000, 8
