@@ -374,6 +374,14 @@ int pmg_dense_backward_phase(const float* delta, const float* phi, const double*
 /* (decoder.py:215-221).  Every entry is finite wherever the reference's is.           */
 int pmg_joint_log_accumulate(const double* log_alpha, const double* log_rho, int64_t T, int32_t L, double* logS,
                              void* stream);
+/* The same with a caller-owned workspace of pmg_joint_log_workspace_size bytes, which  */
+/* lets the time axis split over more workgroups (their (max, sum) partials are folded  */
+/* in split order).  Per block of 64 steps the logs are shifted by their row / column  */
+/* maxima and exponentiated once per (row, step), the block sum is an f64 contraction, */
+/* and an entry whose block sum leaves f64's range is summed term by term in log space. */
+size_t pmg_joint_log_workspace_size(int64_t T, int32_t L);
+int pmg_joint_log_accumulate_ws(const double* log_alpha, const double* log_rho, int64_t T, int32_t L, double* logS,
+                                void* workspace, size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------ */
 /* Sufficient statistics -- fit_tuning_helper.get_statistics             */

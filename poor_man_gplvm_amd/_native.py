@@ -68,6 +68,7 @@ EXPORTED_SYMBOLS = (
     "pmg_suffstats_bf16x3_workspace_size", "pmg_suffstats_bf16x3",
     "pmg_dense_lpad", "pmg_dense_state", "pmg_dense_forward_phase", "pmg_dense_backward_phase",
     "pmg_host_alloc", "pmg_host_free", "pmg_copy_d2h",
+    "pmg_joint_log_workspace_size", "pmg_joint_log_accumulate_ws",
 )
 
 
@@ -163,6 +164,8 @@ _SIGS = {
     "pmg_dense_backward": ([_P, _P, _P, _P, _I64, ctypes.POINTER(DenseTransition), _D, _I32, _I32, _D,
                             _P, _P, _P, _P, _P, _P, _SZ, _P], _I32),
     "pmg_joint_log_accumulate": ([_P, _P, _I64, _I32, _P, _P], _I32),
+    "pmg_joint_log_workspace_size": ([_I64, _I32], _SZ),
+    "pmg_joint_log_accumulate_ws": ([_P, _P, _I64, _I32, _P, _P, _SZ, _P], _I32),
     "pmg_dense_lpad": ([_I32], _I32),
     "pmg_dense_state": ([_P, _I64, _I32, _I32, _I32, _I64], _P),
     "pmg_dense_forward_phase": ([_P, _P, _P, _P, _I64, ctypes.POINTER(DenseTransition), _D, _I32, _I32, _D,

@@ -22,6 +22,7 @@
 #include <math.h>
 
 #include "pmg_common.h"
+#include "pmg_math64.h"
 
 #pragma clang fp contract(on)
 
@@ -894,17 +895,43 @@ __global__ void __launch_bounds__(kDNT) k_dense_backward_relax(DenseParams p) {
 // so that log joint = logA + logK + logS (decoder.py:215-221 accumulates the same sum
 // with logaddexp).  The linear T-contraction (pmg_joint_accumulate) cannot hold it
 // when a far move makes rho ~ e^{+1000} against K ~ e^{-1000} (latent-only chains).
-// One 64 x 64 tile of (x, x') per workgroup, 4 x 4 pairs per thread, time staged in LDS.
+//
+// Blocked form (round 5): per 64 x 64 tile of (x, x') and per block of kJB time steps,
+// the block's log values are shifted by their row maxima mx_x and column maxima my_x'
+// (over the block's steps), exponentiated ONCE per (row, step) and (column, step) in
+// f64, and the block sum s = sum_t e^{la_t[x] - mx_x} e^{lr_t[x'] - my_x'} is a plain
+// f64 contraction (16 FMAs per step per thread); it is folded into the entry's running
+// (m, sum) pair at reference mx_x + my_x'.  That is 128 exps per step per tile instead of
+// 4096.  Every product is <= 1 and the row's and column's largest are 1, so s loses
+// nothing unless the row's and the column's peaks inside the block are more than ~650
+// nats apart in the product: a block sum below 1e-280 is recomputed for that entry term
+// by term in log space (the per-pair form of round 4), so no entry's value depends on
+// the range of f64.  The time axis is split over gridDim.z workgroups (occupancy); their
+// (m, sum) partials are combined in split order by k_joint_log_combine.
 // ---------------------------------------------------------------------------
-constexpr int kJT = 64, kJS = 32;
+constexpr int kJT = 64, kJB = 64;
+constexpr int kJointSplits = 8;   // time splits of the joint (workspace partials)
+
+__device__ __forceinline__ void lse_fold(double& m, double& sm, double r, double s) {
+  if (!(s > 0.0)) return;
+  if (r > m) {
+    sm = (m > -INFINITY) ? fma(sm, exp_neg64(m - r), s) : s;
+    m = r;
+  } else {
+    sm = fma(s, exp_neg64(r - m), sm);
+  }
+}
 
 __global__ void __launch_bounds__(256) k_joint_log(const double* __restrict__ la, const double* __restrict__ lr,
-                                                   int64_t T, int L2, double* __restrict__ logS) {
-  // f64 operands and sums: an entry of a rarely visited row is a ratio of sums of terms
-  // far below the total (log values like -1000, whose f32 rounding is 6e-5 absolute)
-  __shared__ double sa[kJS][kJT], sr[kJS][kJT];
+                                                   int64_t T, int L2, int64_t steps_per_split,
+                                                   double* __restrict__ part, double* __restrict__ logS) {
+  __shared__ double ea[kJB][kJT], eb[kJB][kJT];   // log values, then their shifted exps
+  __shared__ double mx[kJT], my[kJT];
   const int x0 = blockIdx.x * kJT, y0 = blockIdx.y * kJT;
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int64_t ta = (int64_t)blockIdx.z * steps_per_split;
+  int64_t tb = ta + steps_per_split;
+  if (tb > T - 1) tb = T - 1;
   double m[4][4], sm[4][4];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
@@ -913,54 +940,81 @@ __global__ void __launch_bounds__(256) k_joint_log(const double* __restrict__ la
       m[a][b] = -INFINITY;
       sm[a][b] = 0.0;
     }
-  for (int64_t t0 = 0; t0 < T - 1; t0 += kJS) {
-    for (int k = threadIdx.x; k < kJS * kJT; k += 256) {
+  for (int64_t t0 = ta; t0 < tb; t0 += kJB) {
+    for (int k = threadIdx.x; k < kJB * kJT; k += 256) {
       const int tt = k / kJT, c = k % kJT;
       const int64_t t = t0 + tt;
-      const bool ok = t < T - 1;
-      sa[tt][c] = (ok && x0 + c < L2) ? la[t * L2 + x0 + c] : -INFINITY;
-      sr[tt][c] = (ok && y0 + c < L2) ? lr[(t + 1) * L2 + y0 + c] : -INFINITY;
+      const bool ok = t < tb;
+      ea[tt][c] = (ok && x0 + c < L2) ? la[t * L2 + x0 + c] : -INFINITY;
+      eb[tt][c] = (ok && y0 + c < L2) ? lr[(t + 1) * L2 + y0 + c] : -INFINITY;
     }
     __syncthreads();
-    // two passes over the staged block: its max per pair, then the exps relative to the
-    // new max (branch-free; the block's f32 exps of f64 differences are exact to
-    // ~|x| 6e-8 of a term e^x of the sum)
-    double bm[4][4];
+    {   // row / column maxima over the block: two threads per column
+      const int col = threadIdx.x >> 1, half = threadIdx.x & 1;
+      double v = -INFINITY;
+      if (col < kJT) {
+        for (int tt = half; tt < kJB; tt += 2) v = fmax(v, ea[tt][col]);
+      } else {
+        for (int tt = half; tt < kJB; tt += 2) v = fmax(v, eb[tt][col - kJT]);
+      }
+      v = fmax(v, __shfl_xor(v, 1, 64));
+      if (half == 0) {
+        if (col < kJT) mx[col] = v;
+        else my[col - kJT] = v;
+      }
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < kJB * kJT; k += 256) {
+      const int tt = k / kJT, c = k % kJT;
+      const double ma = mx[c], mb = my[c];
+      ea[tt][c] = ma > -INFINITY ? exp_neg64(ea[tt][c] - ma) : 0.0;
+      eb[tt][c] = mb > -INFINITY ? exp_neg64(eb[tt][c] - mb) : 0.0;
+    }
+    __syncthreads();
+    double s[4][4];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) bm[a][b] = m[a][b];
-    for (int tt = 0; tt < kJS; ++tt) {
+      for (int b = 0; b < 4; ++b) s[a][b] = 0.0;
+    for (int tt = 0; tt < kJB; ++tt) {
       double av[4], rv[4];
 #pragma unroll
-      for (int a = 0; a < 4; ++a) av[a] = sa[tt][ty * 4 + a];
+      for (int a = 0; a < 4; ++a) av[a] = ea[tt][ty * 4 + a];
 #pragma unroll
-      for (int b = 0; b < 4; ++b) rv[b] = sr[tt][tx * 4 + b];
+      for (int b = 0; b < 4; ++b) rv[b] = eb[tt][tx * 4 + b];
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) bm[a][b] = fmax(bm[a][b], av[a] + rv[b]);
+        for (int b = 0; b < 4; ++b) s[a][b] = fma(av[a], rv[b], s[a][b]);
     }
+    bool redo = false;
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
-        if (bm[a][b] > m[a][b]) {
-          sm[a][b] *= (double)exp_lg((float)(m[a][b] - bm[a][b]));
-          m[a][b] = bm[a][b];
-        }
+        const double r = mx[ty * 4 + a] + my[tx * 4 + b];
+        if (!(r > -INFINITY)) continue;                 // a masked row or column: no terms
+        if (s[a][b] >= 1e-280) lse_fold(m[a][b], sm[a][b], r, s[a][b]);
+        else redo = true;
       }
-    for (int tt = 0; tt < kJS; ++tt) {
-      double av[4], rv[4];
-#pragma unroll
-      for (int a = 0; a < 4; ++a) av[a] = sa[tt][ty * 4 + a];
-#pragma unroll
-      for (int b = 0; b < 4; ++b) rv[b] = sr[tt][tx * 4 + b];
+    if (redo) {
+      // term by term in log space for the entries whose block sum left f64's range (the
+      // rows' and columns' peaks far apart inside the block); the logs from global memory
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b)
-          if (m[a][b] > -INFINITY) sm[a][b] += (double)exp_lg((float)((av[a] + rv[b]) - m[a][b]));
+        for (int b = 0; b < 4; ++b) {
+          const int x = x0 + ty * 4 + a, y = y0 + tx * 4 + b;
+          const double r = mx[ty * 4 + a] + my[tx * 4 + b];
+          if (!(r > -INFINITY) || s[a][b] >= 1e-280 || x >= L2 || y >= L2) continue;
+          const int64_t te = t0 + kJB < tb ? t0 + kJB : tb;
+          double bm = -INFINITY;
+          for (int64_t t = t0; t < te; ++t) bm = fmax(bm, la[t * L2 + x] + lr[(t + 1) * L2 + y]);
+          if (!(bm > -INFINITY)) continue;
+          double bs = 0.0;
+          for (int64_t t = t0; t < te; ++t) bs += exp_neg64((la[t * L2 + x] + lr[(t + 1) * L2 + y]) - bm);
+          lse_fold(m[a][b], sm[a][b], bm, bs);
+        }
     }
     __syncthreads();
   }
@@ -969,8 +1023,27 @@ __global__ void __launch_bounds__(256) k_joint_log(const double* __restrict__ la
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int x = x0 + ty * 4 + a, y = y0 + tx * 4 + b;
-      if (x < L2 && y < L2) logS[(size_t)x * L2 + y] = sm[a][b] > 0.0 ? m[a][b] + log(sm[a][b]) : -INFINITY;
+      if (x >= L2 || y >= L2) continue;
+      if (part) {
+        double* q = part + ((size_t)blockIdx.z * L2 * L2 + (size_t)x * L2 + y) * 2;
+        q[0] = m[a][b];
+        q[1] = sm[a][b];
+      } else {
+        logS[(size_t)x * L2 + y] = sm[a][b] > 0.0 ? m[a][b] + log(sm[a][b]) : -INFINITY;
+      }
     }
+}
+
+// the splits' (m, sum) partials of every entry, folded in split order
+__global__ void k_joint_log_combine(const double* __restrict__ part, int nsplit, int64_t n, double* __restrict__ logS) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double m = -INFINITY, sm = 0.0;
+  for (int z = 0; z < nsplit; ++z) {
+    const double* q = part + ((size_t)z * n + i) * 2;
+    lse_fold(m, sm, q[0], q[1]);
+  }
+  logS[i] = sm > 0.0 ? m + log(sm) : -INFINITY;
 }
 
 // ---------------------------------------------------------------------------
@@ -1221,14 +1294,42 @@ int pmg_dense_backward_phase(const float* delta, const float* phi, const double*
                              log_gamma, rho, log_rho, workspace, workspace_bytes, stream, phase);
 }
 
-int pmg_joint_log_accumulate(const double* log_alpha, const double* log_rho, int64_t T, int32_t L, double* logS,
-                             void* stream) {
+size_t pmg_joint_log_workspace_size(int64_t T, int32_t L) {
+  if (T <= 0 || L <= 0) return 0;
+  const int64_t n = (int64_t)(2 * L) * (2 * L);
+  return (size_t)kJointSplits * (size_t)n * 2 * sizeof(double) + 256;
+}
+
+int pmg_joint_log_accumulate_ws(const double* log_alpha, const double* log_rho, int64_t T, int32_t L, double* logS,
+                                void* workspace, size_t workspace_bytes, void* stream) {
   PMG_REQUIRE(log_alpha && log_rho && logS && T > 0 && L > 0, "pmg_joint_log_accumulate: bad argument");
   const int L2 = 2 * L;
-  dim3 grid((L2 + kJT - 1) / kJT, (L2 + kJT - 1) / kJT);
-  hipLaunchKernelGGL(k_joint_log, grid, dim3(256), 0, as_stream(stream), log_alpha, log_rho, T, L2, logS);
+  const int64_t n = (int64_t)L2 * L2;
+  // time splits: enough workgroups to fill the chip (one 64 x 64 tile each), each split
+  // at least a few blocks long
+  int nsplit = 1;
+  if (workspace) {
+    PMG_REQUIRE(workspace_bytes >= pmg_joint_log_workspace_size(T, L), "pmg_joint_log_accumulate: workspace too small");
+    const int64_t tiles = (int64_t)((L2 + kJT - 1) / kJT) * ((L2 + kJT - 1) / kJT);
+    while (nsplit < kJointSplits && tiles * nsplit < 1024 && (T - 1) / (2 * nsplit) >= 4 * kJB) nsplit *= 2;
+  }
+  const int64_t per = ((T - 1 + nsplit - 1) / nsplit + kJB - 1) / kJB * kJB;
+  dim3 grid((L2 + kJT - 1) / kJT, (L2 + kJT - 1) / kJT, nsplit);
+  double* part = nsplit > 1 ? static_cast<double*>(workspace) : nullptr;
+  hipLaunchKernelGGL(k_joint_log, grid, dim3(256), 0, as_stream(stream), log_alpha, log_rho, T, L2, per > 0 ? per : kJB,
+                     part, logS);
   PMG_LAUNCH_CHECK();
+  if (part) {
+    hipLaunchKernelGGL(k_joint_log_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), part,
+                       nsplit, n, logS);
+    PMG_LAUNCH_CHECK();
+  }
   return PMG_OK;
+}
+
+int pmg_joint_log_accumulate(const double* log_alpha, const double* log_rho, int64_t T, int32_t L, double* logS,
+                             void* stream) {
+  return pmg_joint_log_accumulate_ws(log_alpha, log_rho, T, L, logS, nullptr, 0, stream);
 }
 
 }  // extern "C"

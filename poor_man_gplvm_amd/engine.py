@@ -810,9 +810,11 @@ class DeviceEM:
     def joint_log(self, log_rho):
         """Dense scans: log S[x,x'] = LSE_t log alpha_t[x] + log rho_{t+1}[x'] (2L x 2L, f64)."""
         S = torch.empty((2 * self.L, 2 * self.L), dtype=torch.float64, device=self.dev)
+        ws = torch.empty(int(self.lib.pmg_joint_log_workspace_size(self.T, self.L)), dtype=torch.uint8, device=self.dev)
         with self._t('joint_log'):
-            nat.check(self.lib.pmg_joint_log_accumulate(nat.ptr(self.log_alpha), nat.ptr(log_rho), self.T, self.L,
-                                                        nat.ptr(S), nat.stream_handle()), "pmg_joint_log_accumulate")
+            nat.check(self.lib.pmg_joint_log_accumulate_ws(nat.ptr(self.log_alpha), nat.ptr(log_rho), self.T, self.L,
+                                                           nat.ptr(S), nat.ptr(ws), ws.numel(), nat.stream_handle()),
+                      "pmg_joint_log_accumulate")
         return S
 
     def joint(self, rho):

@@ -191,3 +191,39 @@ def test_large_latent_count_vs_oracle():
                    n_iter=1, m_step_maxiter=40, m_step_tol=0.0)
     np.testing.assert_allclose(res['tuning'], ref['tuning'], rtol=1e-5)
     close_prob(res['posterior_latent_marg'], ref['posterior_latent_marg'])
+
+
+@pytest.mark.parametrize("T,L,spread,ws", [(300, 40, 5.0, False), (3000, 40, 40.0, True), (700, 72, 400.0, True),
+                                           (2000, 33, 1500.0, True)])
+def test_joint_log_accumulate_vs_logsumexp(T, L, spread, ws):
+    """pmg_joint_log_accumulate(_ws): logS[x, x'] = LSE_t la_t[x] + lr_{t+1}[x'] against an
+    f64 scipy logsumexp, rel 1e-12 on logS (every entry finite where the reference's is),
+    for log inputs that drift by up to `spread` nats within a few steps (random walks, so
+    row and column peaks sit at different times: spread 1500 forces the term-by-term
+    fallback of blocks whose shifted sum leaves f64's range), with a fully masked row and
+    column (-inf) and the time-split workspace path."""
+    from scipy.special import logsumexp
+    from poor_man_gplvm_amd import _native as nat
+    rng = np.random.default_rng(int(T + L + spread))
+    L2 = 2 * L
+    la = np.cumsum(rng.standard_normal((T, L2)) * spread / 8, axis=0)
+    lr = np.cumsum(rng.standard_normal((T, L2)) * spread / 8, axis=0)
+    la[:, 3] = -np.inf
+    lr[:, L2 - 5] = -np.inf
+    lib = nat.load()
+    a = torch.as_tensor(la, device='cuda')
+    r = torch.as_tensor(lr, device='cuda')
+    S = torch.empty((L2, L2), dtype=torch.float64, device='cuda')
+    if ws:
+        w = torch.empty(int(lib.pmg_joint_log_workspace_size(T, L)), dtype=torch.uint8, device='cuda')
+        nat.check(lib.pmg_joint_log_accumulate_ws(nat.ptr(a), nat.ptr(r), T, L, nat.ptr(S), nat.ptr(w), w.numel(),
+                                                  nat.stream_handle()), "joint")
+    else:
+        nat.check(lib.pmg_joint_log_accumulate(nat.ptr(a), nat.ptr(r), T, L, nat.ptr(S), nat.stream_handle()), "joint")
+    got = S.cpu().numpy()
+    with np.errstate(invalid='ignore'):
+        ref = logsumexp(la[:-1, :, None] + lr[1:, None, :], axis=0)
+    fin = np.isfinite(ref)
+    assert np.array_equal(np.isfinite(got), fin)
+    assert np.all(np.isneginf(got[~fin]))
+    np.testing.assert_allclose(got[fin], ref[fin], rtol=1e-12, atol=1e-9)
