@@ -269,7 +269,8 @@ def test_c4_stop_rule_time_sharded_vs_f64_ensemble():
     are perturbed by 1e-15 relative (member k seeded 4000 + k).  Bars: the statistics
     match the oracle's (the device's f32 exp of the init rounds P within an ulp: 1e-7);
     the iteration count is the oracle's or one the ensemble reached; the loss history
-    within rel 1e-9 or 1.5x the ensemble's; tuning within 1.5x the ensemble's spread,
+    within 3x the measured statistics offset (the loss is linear in y_w, t_w) or 1.5x
+    the ensemble's spread; tuning within 1.5x the ensemble's spread,
     capped at 3.5e-4 (measured: all 17 oracle runs stop after 812 bodies, their loss
     histories agree to 1.7e-11, their tuning ends up to 2.0e-4 apart)."""
     import sys
@@ -304,17 +305,24 @@ def test_c4_stop_rule_time_sharded_vs_f64_ensemble():
     tw = eng.shards[0].tw.cpu().numpy()
     np.testing.assert_allclose(tw, e['tw'], rtol=1e-7)
     np.testing.assert_allclose(yw[e['yw_rows']], e['yw_sample'], rtol=1e-7, atol=1e-9)
+    # how far the device's statistics sit from the oracle's: P = expf(lp0) in f32 (within
+    # an ulp of the oracle's correctly rounded f32(exp)), so ~1e-9 relative, far above the
+    # ensemble's 1e-15; the loss is linear in them, so its history carries the same offset
+    ys = e['yw_sample']
+    d_stats = max(float(np.max(np.abs(tw / e['tw'] - 1))),
+                  float(np.max(np.abs(yw[e['yw_rows']][ys != 0] / ys[ys != 0] - 1))))
     n = int(st[0].item())
     n0 = int(e['n_iter'])
     assert n == n0 or n in set(e['ens_n_iter'].tolist()), (n, n0, sorted(set(e['ens_n_iter'].tolist())))
     k = min(n, n0)
-    lh_bar = max(1e-9, 1.5 * float(np.max(e['ens_loss_history_dev'])))
+    lh_bar = max(1.5 * float(np.max(e['ens_loss_history_dev'])), 3 * d_stats, 1e-12)
     lh_dev = float(np.max(np.abs(lh.cpu().numpy()[:k] / e['loss_history'][:k] - 1)))
     tun = O.get_tuning_softplus(Ws[0].cpu().numpy(), B.astype(np.float64))
     ref = O.get_tuning_softplus(e['params'], B.astype(np.float64))
     tun_dev = float(np.max(np.abs(tun / ref - 1)))
     tun_bar = min(1.5 * float(np.max(e['ens_tuning_dev'])), 3.5e-4)
-    print(f"C4 first M-step, 8 time shards, neuron-sharded Adam: n_iter {n} (oracle {n0}, ensemble "
+    print(f"C4 first M-step, 8 time shards, neuron-sharded Adam: statistics {d_stats:.1e} from the oracle's, "
+          f"n_iter {n} (oracle {n0}, ensemble "
           f"{sorted(set(e['ens_n_iter'].tolist()))}), loss history {lh_dev:.2e} (bar {lh_bar:.2e}), "
           f"tuning {tun_dev:.3e} (bar {tun_bar:.3e})")
     assert lh_dev <= lh_bar
