@@ -20,7 +20,7 @@ def main():
         if m:
             labels[m.group(1)] = i
     for i, l in enumerate(body):
-        m = re.search(r"s_cbranch_\w+\s+(\.LBB\w+)", l)
+        m = re.search(r"s_c?branch\w*\s+(\.LBB\w+)", l)
         if m and m.group(1) in labels and labels[m.group(1)] < i:
             a = labels[m.group(1)]
             seg = body[a:i + 1]
