@@ -795,20 +795,31 @@ def decode_leg(y, tuning, L, reps=2):
 def api_fit_wall(y, B, W0, lp0, L, n_iter=20):
     """Wall time of the public PoissonGPLVMJump1D.fit_em(n_iter=20) on the same data,
     end to end: host->device upload of y, 20 EM iterations, and the result dict
-    (posterior (T,2,L), log posteriors, histories) copied back to numpy."""
+    (posterior (T,2,L), log posteriors, histories) copied back to numpy.  Cold: the
+    process's first public fit (its page-locked result buffers are allocated and pinned
+    on the way); warm: a second fit after the first result was dropped (the buffers come
+    from the pinned-block cache)."""
+    import gc
     import torch
     from poor_man_gplvm_amd import PoissonGPLVMJump1D
-    m = PoissonGPLVMJump1D(y.shape[1], n_latent_bin=L, tuning_lengthscale=10.0, movement_variance=1.0)
-    m.tuning_basis = B
-    m.params = W0
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    res = m.fit_em(y, n_iter=n_iter, log_posterior_init=lp0)
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    return {"n_iter": n_iter, "wall_s": wall, "em_iters_per_s": n_iter / wall,
-            "log_marginal": float(res["log_marginal"]),
-            "note": "includes PCIe upload of y and the copy of every returned (T,2,L)/(T,L) array to host"}
+
+    def one():
+        m = PoissonGPLVMJump1D(y.shape[1], n_latent_bin=L, tuning_lengthscale=10.0, movement_variance=1.0)
+        m.tuning_basis = B
+        m.params = W0
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = m.fit_em(y, n_iter=n_iter, log_posterior_init=lp0)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, float(res["log_marginal"])
+
+    cold, lm = one()
+    gc.collect()
+    warm, _ = one()
+    return {"n_iter": n_iter, "wall_s": cold, "em_iters_per_s": n_iter / cold,
+            "wall_s_warm": warm, "em_iters_per_s_warm": n_iter / warm, "log_marginal": lm,
+            "note": "includes PCIe upload of y and the copy of every returned (T,2,L)/(T,L) array to host; "
+                    "wall_s = cold (first public fit of the process), wall_s_warm = a second fit"}
 
 
 if __name__ == "__main__":
