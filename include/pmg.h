@@ -405,6 +405,12 @@ int pmg_suffstats_bf16(const float* P, const uint16_t* ybt, int64_t T, int64_t T
 int pmg_exp(const float* logp, int64_t n, float* p, void* stream);
 /* out = log(x) elementwise (log-space outputs; log(0) = -inf). */
 int pmg_log(const float* x, int64_t n, float* out, void* stream);
+/* The returned arrays of a posterior gamma (T, 2, L) f32 in one pass: log_out (T, 2, L) =
+ * logf(gamma) (as pmg_log), plm (T, L) = gamma[t,0,l] + gamma[t,1,l] (posterior_latent_marg)
+ * and pdm (T, 2) = sum_l gamma[t,d,l] (posterior_dynamics_marg, f64 sum rounded once) --
+ * core.py:696-712 / decoder.py:300-315 form them with jnp sums.  Any output may be NULL. */
+int pmg_posterior_outputs(const float* gamma, int64_t T, int32_t L, float* log_out, float* plm, float* pdm,
+                          void* stream);
 /* out[t, n] = y[(t - shift[n]) mod T, n] for y, out (T, N) row-major f32, shift (N,) int64
  * (device): every neuron's column rolled by its own shift, the np.roll of
  * test.circular_shuffle_data (reference poor_man_gplvm/test.py:10-24).  y != out. */

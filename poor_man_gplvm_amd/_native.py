@@ -68,7 +68,7 @@ EXPORTED_SYMBOLS = (
     "pmg_suffstats_bf16x3_workspace_size", "pmg_suffstats_bf16x3",
     "pmg_dense_lpad", "pmg_dense_state", "pmg_dense_forward_phase", "pmg_dense_backward_phase",
     "pmg_host_alloc", "pmg_host_free", "pmg_copy_d2h",
-    "pmg_joint_log_workspace_size", "pmg_joint_log_accumulate_ws",
+    "pmg_joint_log_workspace_size", "pmg_joint_log_accumulate_ws", "pmg_posterior_outputs",
 )
 
 
@@ -136,6 +136,7 @@ _SIGS = {
     "pmg_suffstats_bf16x3": ([_P, _I64, _P, _I64, _I64, _I32, _I32, _I32, _P, _P, _P, _SZ, _P], _I32),
     "pmg_exp": ([_P, _I64, _P, _P], _I32),
     "pmg_log": ([_P, _I64, _P, _P], _I32),
+    "pmg_posterior_outputs": ([_P, _I64, _I32, _P, _P, _P, _P], _I32),
     "pmg_roll_columns": ([_P, _I64, _I32, _P, _P, _P], _I32),
     "pmg_emission_latent_mask": ([_P, _P, _I64, _I32, _P, _P, _P, _P], _I32),
     "pmg_emission_latent_mask_batched": ([_P, _P, _I64, _I32, _P, _I32, _P, _P, _P], _I32),

@@ -24,7 +24,8 @@ import numpy as np
 import torch
 
 from . import _native as nat
-from .engine import AdamConfig, DeviceEM, RestartBatchEM, ScanConfig, SpikeData, default_device, log_of
+from .engine import (AdamConfig, DeviceEM, RestartBatchEM, ScanConfig, SpikeData, default_device, log_of,
+                     posterior_outputs)
 from .gp_kernel import (DenseTransition, banded_transition, create_transition_prob_1d, dense_transition,
                         generate_basis, make_transition, transition_from_log_kernels)
 
@@ -66,7 +67,6 @@ class _PinnedCopies:
     snapshots) run on a side stream beside the remaining iterations.  finish()
     synchronises and returns; the buffers are the numpy arrays handed to the caller."""
 
-    SMALL = 4 << 20
     # page-locked bytes reserved ahead of the loop for snapshots; further snapshots get
     # their buffer when they are submitted (a small save_every must not pin n_iter copies
     # of (T, 2, L) up front)
@@ -104,18 +104,11 @@ class _PinnedCopies:
         st = self.side if side else cur
         nbytes = t.numel() * t.element_size()
         q = self.reserved.get(key)
-        if not q and nbytes < self.SMALL:
-            # small results (W, tuning, histories): torch's cached pinned blocks
-            h = torch.empty(tuple(t.shape), dtype=t.dtype, pin_memory=True)
-            with torch.cuda.stream(st):
-                h.copy_(t, non_blocking=True)
-            host = h.numpy()
-        else:
-            host = q.pop(0).result() if q else nat.host_array(tuple(t.shape), _NP_DTYPE[t.dtype])
-            if host.shape != tuple(t.shape) or host.dtype != _NP_DTYPE[t.dtype]:
-                raise ValueError("reserved host buffer does not match the tensor")
-            nat.check(nat.load().pmg_copy_d2h(host.ctypes.data, t.data_ptr(), nbytes, st.cuda_stream),
-                      "pmg_copy_d2h")
+        host = q.pop(0).result() if q else nat.host_array(tuple(t.shape), _NP_DTYPE[t.dtype])
+        if host.shape != tuple(t.shape) or host.dtype != _NP_DTYPE[t.dtype]:
+            raise ValueError("reserved host buffer does not match the tensor")
+        nat.check(nat.load().pmg_copy_d2h(host.ctypes.data, t.data_ptr(), nbytes, st.cuda_stream),
+                  "pmg_copy_d2h")
         self.items.append(host)
         return host
 
@@ -334,11 +327,12 @@ class PoissonGPLVMJump1D:
         eng.check_status()
         ml = None if ma_latent is None else np.asarray(ma_latent).astype(bool)
         # the log-domain scans hold the exact log posteriors (f64 causal ones, cast on the device)
-        h_lpost = cp.submit(lgam if eng.dense else log_of(gamma), key='lpost')
+        lg, plm, pdm = posterior_outputs(gamma, log=not eng.dense)
+        h_lpost = cp.submit(lgam if eng.dense else lg, key='lpost')
         h_lcaus = cp.submit(eng.log_alpha.to(torch.float32) if eng.dense else log_of(eng.alpha), key='lcaus')
         h_gamma = cp.submit(gamma, key='gamma')
-        h_plm = cp.submit(gamma.sum(dim=1), key='plm')
-        h_pdm = cp.submit(gamma.sum(dim=2))
+        h_plm = cp.submit(plm, key='plm')
+        h_pdm = cp.submit(pdm)
         h_logc = cp.submit(eng.logc.to(torch.float32))
         h_ll = cp.submit(eng.loglik(), key='ll')
         h_lz = cp.submit(logz)
@@ -420,7 +414,7 @@ class PoissonGPLVMJump1D:
         eng.check_status()
         return {'log_marginal_final': float(_np(logz)[0]),
                 'log_one_step_predictive_marginals_all': _np(eng.logc).astype(np.float32),
-                'posterior_dynamics_marg': _np(gamma.sum(dim=2))}
+                'posterior_dynamics_marg': _np(posterior_outputs(gamma, log=False)[2])}
 
     def _decode_result(self, r, t_l=None):
         """decode_latent's returned dict from a _decode_on result (core.py:477-497)."""
@@ -599,8 +593,13 @@ class PoissonGPLVMJump1D:
         self._m_step_step_size, self._m_step_maxiter, self._m_step_tol = m_step_step_size, m_step_maxiter, m_step_tol
         if save_every is None:
             save_every = n_iter
-        _, log_latent_transition_kernel_l, _, log_dynamics_transition_kernel = create_transition_prob_1d(
-            self.n_latent_bin, movement_variance, p_move_to_jump, p_jump_to_move, self.custom_transition_kernel)
+        # the host-side log kernels the model keeps (core.py:683-684) are formed on a helper
+        # thread while the device runs the fit
+        from concurrent.futures import ThreadPoolExecutor
+        pool = ThreadPoolExecutor(max_workers=1)
+        log_kernels = pool.submit(create_transition_prob_1d, self.n_latent_bin, movement_variance, p_move_to_jump,
+                                  p_jump_to_move, self.custom_transition_kernel)
+        pool.shutdown(wait=False)
         if ma_neuron is None:
             ma_neuron = self.ma_neuron_default
         if ma_latent is None:
@@ -620,6 +619,7 @@ class PoissonGPLVMJump1D:
                      adam=AdamConfig(lr=m_step_step_size, maxiter=m_step_maxiter, tol=m_step_tol,
                                      prior_std=hp['param_prior_std']),
                      scan=self.scan_config, noise_std=getattr(self, '_fit_noise_std', None))
+        _, log_latent_transition_kernel_l, _, log_dynamics_transition_kernel = log_kernels.result()
         self.params = res['params']
         self.tuning = res['tuning']
         self.fit_info = info
@@ -786,6 +786,16 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
     if save_every is None:
         save_every = n_iter
     ma = None if ma_neuron is None else np.asarray(ma_neuron, np.float32)
+    dev = default_device()
+    # the returned arrays go to the host through pinned buffers without host syncs inside
+    # the loop: snapshots on a side stream beside the later iterations (their device
+    # copies are fresh tensors), the final arrays after the loop.  The large buffers are
+    # allocated on a helper thread from here on, beside the uploads and the loop.
+    cp = _PinnedCopies(dev)
+    n_saved = len(range(0, n_iter, save_every))
+    cp.reserve_upto('snap', (T, 2, L), n_saved)
+    for key, shape in (('post', (T, 2, L)), ('lpf', (T, 2, L)), ('plm', (T, L))):
+        cp.reserve(key, shape)
     sp = SpikeData(y, ma)
     eng = DeviceEM(sp, L, basis=B, scan=scan)
     eng.adaptive = True          # adaptive warm-up across this fit's E-steps
@@ -815,14 +825,6 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
 
     def log_post_dev():
         return lgam.clone() if eng.dense else log_of(gamma)
-    # the returned arrays go to the host through pinned buffers without host syncs inside
-    # the loop: snapshots on a side stream beside the later iterations (their device
-    # copies are fresh tensors), the final arrays after the loop
-    cp = _PinnedCopies(dev)
-    n_saved = len(range(0, n_iter, save_every))
-    cp.reserve_upto('snap', (T, 2, L), n_saved)
-    for key, shape in (('post', (T, 2, L)), ('lpf', (T, 2, L)), ('plm', (T, L))):
-        cp.reserve(key, shape)
     saved_dev = []      # (i, log posterior, W f32, tuning) pinned host buffers per snapshot
     saved_idx = []
     import time
@@ -834,25 +836,29 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
         eng.e_step(likelihood_scale, logz[i:i + 1], gamma=gamma if want_gamma else None,
                    log_gamma=lgam if want_gamma else None)
         if i % save_every == 0:
-            saved_dev.append((cp.submit(log_post_dev(), key='snap', side=True), cp.submit(W.to(torch.float32), side=True),
-                              cp.submit(eng.tuning32.clone(), side=True)))
+            # the (T, 2, L) log posterior (a fresh tensor) on the side stream; W and the
+            # tuning (written again by the next iterations) on this stream, W as f64 (cast
+            # on the host: no cast kernel)
+            saved_dev.append((cp.submit(log_post_dev(), key='snap', side=True), cp.submit(W),
+                              cp.submit(eng.tuning32)))
             saved_idx.append(i)
         if timing is not None:
             torch.cuda.synchronize()
             timing.append(time.perf_counter() - t0)
     # final arrays: the sums over d and l on the device (posterior_latent_marg /
     # posterior_dynamics_marg), every copy queued behind the last E-step
+    lg, plm, pdm = posterior_outputs(gamma, log=not eng.dense)
     h_post = cp.submit(gamma, key='post')
-    h_lpf = cp.submit(log_post_dev(), key='lpf')
-    h_plm = cp.submit(gamma.sum(dim=1), key='plm')
-    h_pdm = cp.submit(gamma.sum(dim=2))
-    h_W = cp.submit(W.to(torch.float32))
+    h_lpf = cp.submit(lgam if eng.dense else lg, key='lpf')
+    h_plm = cp.submit(plm, key='plm')
+    h_pdm = cp.submit(pdm)
+    h_W = cp.submit(W)
     h_tun = cp.submit(eng.tuning32)
     h_st, h_lh, h_eh, h_lz = cp.submit(stats), cp.submit(lh), cp.submit(eh), cp.submit(logz)
     cp.finish()
     lz = h_lz
     saved = {'log_posterior_all_saved': [_masked_log(a, mlat) for a, _, _ in saved_dev],
-             'params_saved': [b for _, b, _ in saved_dev],
+             'params_saved': [b.astype(np.float32) for _, b, _ in saved_dev],
              'tuning_saved': [c for _, _, c in saved_dev],
              'iter_saved': list(saved_idx),
              'log_marginal_saved': [float(lz[i]) for i in saved_idx]}
@@ -863,7 +869,7 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
            'params_saved': saved['params_saved'],
            'tuning_saved': saved['tuning_saved'],
            'iter_saved': saved['iter_saved'],
-           'params': h_W,
+           'params': h_W.astype(np.float32),
            'tuning': h_tun,
            'log_posterior_final': _masked_log(h_lpf, mlat),
            'log_marginal': float(lz[n_iter - 1]) if n_iter else float('nan'),

@@ -187,7 +187,12 @@ __global__ void k_adam_prologue(AdamParams p_arg, size_t n) {
 //              (LDS, fixed order) by the element-update threads.
 // Everything but the G broadcast and the cross-wave sum stays in registers.
 // ---------------------------------------------------------------------------
-constexpr int kNW = kThreads / 64;          // waves (the last one also runs the decision)
+constexpr int kNW = kThreads / 64;          // waves
+// The decision pipeline runs on wave kCtl before barrier 1: waves w and w + 4 share a
+// SIMD and the older one (w < 4) is issued first, so it ends phases A+B ~1,500 ticks
+// before its partner and waits at barrier 1 -- the decision fills that wait instead of
+// holding barrier 2 open after the element update (round 4: the last wave, after it).
+constexpr int kCtl = 3;
 constexpr int kRefresh = 16;
 typedef float f2v __attribute__((ext_vector_type(2)));   // row pairs: v_pk_fma_f32 operands
 
@@ -297,7 +302,7 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index: uniform (SGPR)
-  const bool ctl = wid == kNW - 1;                     // runs the decision pipeline
+  const bool ctl = wid == kCtl;                        // runs the decision pipeline
   const int g = blockIdx.x;
   const int rb = g / p.Gg, gg = g - rb * p.Gg;         // row block, neuron group
   const int r0 = rb * 32 * A;                          // first row of this workgroup
@@ -506,6 +511,88 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
 #pragma unroll
         for (int k4 = 0; k4 < BC; ++k4) sPart[(wid * SP + s) * 16 * BC + qb * BC + k4] = gp[s][k4];
     }
+    if (p.prof && g == 0 && tid == kCtl * 64 && k < 64) p.prof[k * 16 + 5] = __builtin_amdgcn_s_memtime();
+    if (ctl && k > 0) {
+      // ---- decision pipeline (control wave) over bodies dj .. k-1 ---------------
+      // Partials are pre-filled with a signalling-NaN sentinel (never produced by
+      // arithmetic) and each is written once by one 8-byte atomic store, so a load
+      // returns either the sentinel (not published yet) or the final value.  Loads
+      // for bodies dj and dj+1 are kept in flight across bodies; the wave blocks
+      // (bounded spin) only when the pipeline is kLag bodies behind.
+      const int last = k - 1;                // latest body this workgroup has published
+      for (int rep = 0; rep < 2; ++rep) {
+        const bool must = eval_only || (last - dj) >= kLag;
+        if (!issued0 || dj > last) break;
+        bool ok = true;
+#pragma unroll
+        for (int q = 0; q < kPartPerLane; ++q) ok &= (lv0[q] != kSentinel);
+        ok = __all(ok);
+        if (p.prof && g == 0 && lane == 0 && k < 64 && rep == 0) p.prof[k * 16 + 8] = __builtin_amdgcn_s_memtime();
+        if (!ok && must) {  // blocking re-poll of body dj
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          while (!ok) {
+            __builtin_amdgcn_s_sleep(1);
+            load_parts(p, dj, lane, lv0);
+            ok = true;
+#pragma unroll
+            for (int q = 0; q < kPartPerLane; ++q) ok &= (lv0[q] != kSentinel);
+            ok = __all(ok);
+            if (p.prof && g == 0 && lane == 0 && k < 64) p.prof[k * 16 + 7] += 1;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > p.spin) {
+              if (lane == 0) {
+                atomicOr(p.timeout, 1);
+                sCtl[2] = 1;
+              }
+              break;
+            }
+          }
+          if (!ok) break;
+        }
+        if (!ok) {  // not published yet: re-issue, try next body
+          load_parts(p, dj, lane, lv0);
+          break;
+        }
+        const double loss = sum_parts(lv0);
+        if (p.prof && g == 0 && lane == 0 && k < 64 && rep == 0) p.prof[k * 16 + 9] = __builtin_amdgcn_s_memtime();
+        const int j = dj;
+        if (j == 0) {
+          loss0 = loss;
+          loss_prev = loss;
+        }
+        bool cont;
+        if (eval_only) {
+          cont = false;
+        } else {
+          const double rel = fabs(loss - loss_prev) / fmax(fabs(loss), 1e-8);
+          // tol < 0: no early stop (the speculative batches of the neuron-sharded M-step),
+          // also not on a NaN loss, whose rel compares false
+          cont = (j + 1 < maxiter - 1) && ((j + 1 < 5) || p.tol < 0.0 || (rel > p.tol));
+        }
+        loss_prev = loss;
+        ++dj;
+        if (!cont) {
+          fin_loss = loss;
+          if (lane == 0) sCtl[0] = 1, sCtl[1] = j;
+          break;
+        }
+#pragma unroll
+        for (int q = 0; q < kPartPerLane; ++q) lv0[q] = lv1[q];
+        issued0 = issued1;
+        issued1 = false;
+      }
+      if (p.prof && g == 0 && lane == 0 && k < 64) p.prof[k * 16 + 10] = __builtin_amdgcn_s_memtime();
+      if (!sCtl[0]) {  // keep bodies dj and dj+1 in flight (both <= last)
+        if (!issued0 && dj <= last) {
+          load_parts(p, dj, lane, lv0);
+          issued0 = true;
+        }
+        if (!issued1 && dj + 1 <= last) {
+          load_parts(p, dj + 1, lane, lv1);
+          issued1 = true;
+        }
+      }
+    }
+    if (p.prof && g == 0 && tid == kCtl * 64 && k < 64) p.prof[k * 16 + 6] = __builtin_amdgcn_s_memtime();
     PMG_ADAM_STAMP(k, 1)
     PMG_LDS_BARRIER();
     PMG_ADAM_STAMP(k, 2)
@@ -605,88 +692,6 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
       sSum[wid] = lpart;
       sSum[kNW + wid] = gsq;
     }
-    if (p.prof && g == 0 && tid == kThreads - 64 && k < 64) p.prof[k * 16 + 5] = __builtin_amdgcn_s_memtime();
-    if (ctl && k > 0) {
-      // ---- decision pipeline (control wave) over bodies dj .. k-1 ---------------
-      // Partials are pre-filled with a signalling-NaN sentinel (never produced by
-      // arithmetic) and each is written once by one 8-byte atomic store, so a load
-      // returns either the sentinel (not published yet) or the final value.  Loads
-      // for bodies dj and dj+1 are kept in flight across bodies; the wave blocks
-      // (bounded spin) only when the pipeline is kLag bodies behind.
-      const int last = k - 1;                // latest body this workgroup has published
-      for (int rep = 0; rep < 2; ++rep) {
-        const bool must = eval_only || (last - dj) >= kLag;
-        if (!issued0 || dj > last) break;
-        bool ok = true;
-#pragma unroll
-        for (int q = 0; q < kPartPerLane; ++q) ok &= (lv0[q] != kSentinel);
-        ok = __all(ok);
-        if (p.prof && g == 0 && lane == 0 && k < 64 && rep == 0) p.prof[k * 16 + 8] = __builtin_amdgcn_s_memtime();
-        if (!ok && must) {  // blocking re-poll of body dj
-          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-          while (!ok) {
-            __builtin_amdgcn_s_sleep(1);
-            load_parts(p, dj, lane, lv0);
-            ok = true;
-#pragma unroll
-            for (int q = 0; q < kPartPerLane; ++q) ok &= (lv0[q] != kSentinel);
-            ok = __all(ok);
-            if (p.prof && g == 0 && lane == 0 && k < 64) p.prof[k * 16 + 7] += 1;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > p.spin) {
-              if (lane == 0) {
-                atomicOr(p.timeout, 1);
-                sCtl[2] = 1;
-              }
-              break;
-            }
-          }
-          if (!ok) break;
-        }
-        if (!ok) {  // not published yet: re-issue, try next body
-          load_parts(p, dj, lane, lv0);
-          break;
-        }
-        const double loss = sum_parts(lv0);
-        if (p.prof && g == 0 && lane == 0 && k < 64 && rep == 0) p.prof[k * 16 + 9] = __builtin_amdgcn_s_memtime();
-        const int j = dj;
-        if (j == 0) {
-          loss0 = loss;
-          loss_prev = loss;
-        }
-        bool cont;
-        if (eval_only) {
-          cont = false;
-        } else {
-          const double rel = fabs(loss - loss_prev) / fmax(fabs(loss), 1e-8);
-          // tol < 0: no early stop (the speculative batches of the neuron-sharded M-step),
-          // also not on a NaN loss, whose rel compares false
-          cont = (j + 1 < maxiter - 1) && ((j + 1 < 5) || p.tol < 0.0 || (rel > p.tol));
-        }
-        loss_prev = loss;
-        ++dj;
-        if (!cont) {
-          fin_loss = loss;
-          if (lane == 0) sCtl[0] = 1, sCtl[1] = j;
-          break;
-        }
-#pragma unroll
-        for (int q = 0; q < kPartPerLane; ++q) lv0[q] = lv1[q];
-        issued0 = issued1;
-        issued1 = false;
-      }
-      if (p.prof && g == 0 && lane == 0 && k < 64) p.prof[k * 16 + 10] = __builtin_amdgcn_s_memtime();
-      if (!sCtl[0]) {  // keep bodies dj and dj+1 in flight (both <= last)
-        if (!issued0 && dj <= last) {
-          load_parts(p, dj, lane, lv0);
-          issued0 = true;
-        }
-        if (!issued1 && dj + 1 <= last) {
-          load_parts(p, dj + 1, lane, lv1);
-          issued1 = true;
-        }
-      }
-    }
-    if (p.prof && g == 0 && tid == kThreads - 64 && k < 64) p.prof[k * 16 + 6] = __builtin_amdgcn_s_memtime();
     PMG_ADAM_STAMP(k, 3)
     PMG_LDS_BARRIER();
     if (sCtl[0] || sCtl[2]) break;

@@ -196,6 +196,44 @@ __global__ void k_log(const float* __restrict__ x, int64_t n, float* __restrict_
   for (; i < n; i += stride) y[i] = logf(x[i]);
 }
 
+// The arrays a fit / decode returns from the posterior (T, 2, L) (core.py:696-712,
+// decoder.py:300-315), in one pass over it: its log (logf, as k_log), the latent marginal
+// plm (T, L) = g[t,0,l] + g[t,1,l] and the dynamics marginal pdm (T, 2) = sum_l g[t,d,l]
+// (f64 sums rounded once).  One workgroup per row t (grid-stride); any output may be null.
+__global__ void __launch_bounds__(256) k_posterior_outputs(const float* __restrict__ g, int64_t T, int L,
+                                                           float* __restrict__ lg, float* __restrict__ plm,
+                                                           float* __restrict__ pdm) {
+  __shared__ double red[2][4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int64_t t = blockIdx.x; t < T; t += gridDim.x) {
+    const float* r = g + t * 2 * L;
+    double s0 = 0.0, s1 = 0.0;
+    for (int l = threadIdx.x; l < L; l += 256) {
+      const float a = r[l], b = r[L + l];
+      s0 += a;
+      s1 += b;
+      if (plm) plm[t * L + l] = a + b;
+      if (lg) {
+        lg[t * 2 * L + l] = logf(a);
+        lg[t * 2 * L + L + l] = logf(b);
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      s0 += __shfl_xor(s0, o);
+      s1 += __shfl_xor(s1, o);
+    }
+    if (lane == 0) {
+      red[0][wv] = s0;
+      red[1][wv] = s1;
+    }
+    __syncthreads();
+    if (pdm && threadIdx.x < 2)
+      pdm[t * 2 + threadIdx.x] = (float)(red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] +
+                                         red[threadIdx.x][3]);
+    __syncthreads();
+  }
+}
+
 // out[t, n] = y[(t - shift[n]) mod T, n]: np.roll of every neuron's column by its own
 // shift (circular_shuffle_data, test.py:20-23).  A block walks rows t; its threads own
 // neuron columns, so each thread's shift is read once and every row write is coalesced.
@@ -288,8 +326,9 @@ int pmg_loglik_materialize(const float* delta, const double* rblk, int64_t T, in
 }
 
 int pmg_exp(const float* logp, int64_t n, float* p, void* stream) {
-  PMG_REQUIRE(n >= 0 && logp && p, "pmg_exp: bad args");
+  PMG_REQUIRE(n >= 0, "pmg_exp: bad args");
   if (n == 0) return PMG_OK;
+  PMG_REQUIRE(logp && p, "pmg_exp: null pointer");
   unsigned blocks = (unsigned)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
   hipLaunchKernelGGL(k_exp, dim3(blocks), dim3(256), 0, as_stream(stream), logp, n, p);
   PMG_LAUNCH_CHECK();
@@ -306,10 +345,22 @@ int pmg_roll_columns(const float* y, int64_t T, int32_t N, const int64_t* shift,
 }
 
 int pmg_log(const float* x, int64_t n, float* out, void* stream) {
-  PMG_REQUIRE(n >= 0 && x && out, "pmg_log: bad args");
+  PMG_REQUIRE(n >= 0, "pmg_log: bad args");
   if (n == 0) return PMG_OK;
+  PMG_REQUIRE(x && out, "pmg_log: null pointer");
   unsigned blocks = (unsigned)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
   hipLaunchKernelGGL(k_log, dim3(blocks), dim3(256), 0, as_stream(stream), x, n, out);
+  PMG_LAUNCH_CHECK();
+  return PMG_OK;
+}
+
+int pmg_posterior_outputs(const float* gamma, int64_t T, int32_t L, float* log_out, float* plm, float* pdm,
+                          void* stream) {
+  PMG_REQUIRE(T >= 0 && L > 0 && (T == 0 || gamma), "pmg_posterior_outputs: bad args (T=%lld, L=%d)", (long long)T, L);
+  if (T == 0 || (!log_out && !plm && !pdm)) return PMG_OK;
+  const unsigned blocks = (unsigned)(T < 4096 ? T : 4096);
+  hipLaunchKernelGGL(k_posterior_outputs, dim3(blocks), dim3(256), 0, as_stream(stream), gamma, T, L, log_out,
+                     plm, pdm);
   PMG_LAUNCH_CHECK();
   return PMG_OK;
 }

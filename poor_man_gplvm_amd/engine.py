@@ -893,6 +893,20 @@ def log_of(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def posterior_outputs(gamma: torch.Tensor, log: bool = True):
+    """(log gamma or None, posterior_latent_marg (T, L), posterior_dynamics_marg (T, 2)) of a
+    posterior (T, 2, L) f32, in one device pass (pmg_posterior_outputs)."""
+    if gamma.dim() != 3 or gamma.shape[1] != 2 or gamma.dtype != torch.float32:
+        raise ValueError("posterior_outputs: expected a (T, 2, L) float32 tensor")
+    T, _, L = gamma.shape
+    lg = torch.empty_like(gamma) if log else None
+    plm = torch.empty((T, L), dtype=torch.float32, device=gamma.device)
+    pdm = torch.empty((T, 2), dtype=torch.float32, device=gamma.device)
+    nat.check(nat.load().pmg_posterior_outputs(nat.ptr(gamma), T, L, nat.ptr(lg), nat.ptr(plm), nat.ptr(pdm),
+                                               nat.stream_handle()), "pmg_posterior_outputs")
+    return lg, plm, pdm
+
+
 class RestartBatchEM:
     """R independent EM restarts of one recording on one GPU (model_selection_helper.py:53-59:
     the restarts differ only in their posterior init; SURVEY 8(e): 8 restarts per GPU at C5).

@@ -50,3 +50,25 @@ def test_fit_and_decode_results_are_host_arrays():
     np.testing.assert_array_equal(dec['log_posterior_all'], lp)
     np.testing.assert_allclose(plm, dec['posterior_all'].sum(1), rtol=1e-6, atol=1e-7)
     np.testing.assert_allclose(dec['posterior_dynamics_marg'], dec['posterior_all'].sum(2), rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("T,L", [(1000, 96), (257, 300), (3, 1), (0, 16), (4100, 512)])
+def test_posterior_outputs_one_pass(T, L):
+    """pmg_posterior_outputs: log (bit-identical to pmg_log), latent marginal (the f32
+    sum of the two dynamics rows, exact) and dynamics marginal (f64 sum rounded once) of
+    a posterior with exact zeros (log -inf)."""
+    from poor_man_gplvm_amd.engine import log_of, posterior_outputs
+    rng = np.random.default_rng(T + L)
+    g = rng.random((T, 2, L)).astype(np.float32)
+    g[rng.random(g.shape) < 0.05] = 0.0
+    gd = torch.as_tensor(g, device='cuda')
+    lg, plm, pdm = posterior_outputs(gd)
+    ref_log = log_of(gd)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(lg.cpu().numpy(), ref_log.cpu().numpy())
+    np.testing.assert_array_equal(plm.cpu().numpy(), g[:, 0, :] + g[:, 1, :])
+    np.testing.assert_allclose(pdm.cpu().numpy(), g.astype(np.float64).sum(2).astype(np.float32), rtol=1.2e-7)
+    lg2, plm2, pdm2 = posterior_outputs(gd, log=False)
+    assert lg2 is None
+    np.testing.assert_array_equal(plm2.cpu().numpy(), plm.cpu().numpy())
+    np.testing.assert_array_equal(pdm2.cpu().numpy(), pdm.cpu().numpy())
