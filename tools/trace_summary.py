@@ -2,7 +2,9 @@
 `rocprofv3 --kernel-trace` (the last `steps` EM iterations' launches of each kernel),
 for comparison with bench.py's live HIP-event timings (its `rooflines[*].ms` and
 `kernels_ms`).  `iters` = every EM iteration the run executed (bench.py: 1 pre-warm +
-warmup + steps), so a kernel launched k times per iteration keeps its last k*steps.
+2 x (warmup + steps): the measured fit and the instrumented one, e.g. 51 for --warmup 5
+--steps 20), so a kernel launched k times per iteration keeps its last k*steps.  Per-fit
+kernels (spike preparation, the first M-step's exp) are listed with their own counts.
 usage: python tools/trace_summary.py gpurun_out/prof_X/run_kernel_trace.csv STEPS ITERS out.csv
 """
 import csv
