@@ -55,8 +55,10 @@ constexpr int kPfFwd = 4;
 constexpr int kPfBwdWarm = 4;
 constexpr int kPfBwdOut = 2;
 // the relaxation kernel runs <= 1 wave per CU: a deeper ring covers the latency alone,
-// as deep as the registers allow (a backward row is 3J floats)
-template <int J> constexpr int pf_relax_fwd() { return J >= 16 ? 4 : 8; }
+// as deep as the registers allow (a backward row is 3J floats).  J = 8 forward: 4, not 8
+// (with the EM relaxation's A1-free loop, the 4-deep ring was 7 % faster on the first
+// E-step of a fit, profiles/r05_ab_experiments.txt item 7)
+template <int J> constexpr int pf_relax_fwd() { return J >= 8 ? 4 : 8; }
 template <int J> constexpr int pf_relax_bwd() { return J >= 16 ? 2 : (J >= 8 ? 4 : 8); }
 
 // Control words at the start of the scan workspace (int32), one block per direction
@@ -851,7 +853,7 @@ __device__ __forceinline__ double wave_sum_fixed(const double* x, int n) {
 // flagged (flg, round 0 only), the chunks up to the next flagged boundary are
 // consistent: stop (*stop = c).  Returns true iff the segment's end state (chunk b-1)
 // moved.
-template <int J, int WP, bool VEC>
+template <int J, int WP, bool VEC, bool A1 = true>
 __device__ __forceinline__ bool fwd_segment(const FBParams& p, Fwd<J, WP>& st, int c0, int b, int j0, const float invz[J],
                             const int* flg, int& nrep, int* stop = nullptr) {
   const size_t SZ = (size_t)2 * p.Lpad;
@@ -859,7 +861,7 @@ __device__ __forceinline__ bool fwd_segment(const FBParams& p, Fwd<J, WP>& st, i
     const int64_t t_c = (int64_t)c * p.C;
     const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
     st.save_state(p, p.s_in + (size_t)c * SZ, j0);
-    const double lz = fwd_stream<J, WP, pf_relax_fwd<J>(), VEC, true>(p, st, j0, invz, t_c, t_e);
+    const double lz = fwd_stream<J, WP, pf_relax_fwd<J>(), VEC, true, A1>(p, st, j0, invz, t_c, t_e);
     if ((threadIdx.x & 63) == 0) p.chunk_logz[c] = lz;
     ++nrep;
     float* so = p.s_out + (size_t)c * SZ;
@@ -876,7 +878,7 @@ __device__ __forceinline__ bool fwd_segment(const FBParams& p, Fwd<J, WP>& st, i
   return true;
 }
 
-template <int J, int WP, bool VEC>
+template <int J, int WP, bool VEC, bool A1 = true>
 __device__ __forceinline__ void forward_relax(const FBParams& p, int j0, const float invz[J]) {
   const size_t SZ = (size_t)2 * p.Lpad;
   const int s = blockIdx.x;
@@ -894,7 +896,7 @@ __device__ __forceinline__ void forward_relax(const FBParams& p, int j0, const f
     while (c0 >= 0) {
       st.load_state(p, p.s_in + (size_t)c0 * SZ, j0);
       int stop = b;
-      changed = fwd_segment<J, WP, VEC>(p, st, c0, b, j0, invz, p.flags, nrep, &stop);
+      changed = fwd_segment<J, WP, VEC, A1>(p, st, c0, b, j0, invz, p.flags, nrep, &stop);
       if (changed) break;                                  // ran through to the segment end
       c0 = stop + 2 < b ? find_flag<1>(p.flags, stop + 2, b) : -1;
     }
@@ -911,7 +913,7 @@ __device__ __forceinline__ void forward_relax(const FBParams& p, int j0, const f
         const float d = hilbert_dist(X, p.s_in + (size_t)a * SZ, (int)SZ);
         if (!(d <= p.tol)) {
           st.load_state(p, X, j0);
-          changed = fwd_segment<J, WP, VEC>(p, st, a, b, j0, invz, nullptr, nrep);
+          changed = fwd_segment<J, WP, VEC, A1>(p, st, a, b, j0, invz, nullptr, nrep);
         }
       }
     }
@@ -935,7 +937,9 @@ __global__ void __launch_bounds__(64) k_forward_relax(FBParams p_arg) {
   (void)lane;
   if constexpr (J % 4 == 0) {
     if ((p.L & 3) == 0) {
-      forward_relax<J, WP, true>(p, j0, invz);
+      // the EM passes store no d = 1 rows of alpha (a1_bytes = 0): no a1 row formed either
+      if (p.a1_bytes == 0) forward_relax<J, WP, true, false>(p, j0, invz);
+      else forward_relax<J, WP, true>(p, j0, invz);
       return;
     }
   }
@@ -1249,7 +1253,7 @@ __global__ void __launch_bounds__(64) k_backward_full(FBParams p_arg) {
 // boundary metric of k_verify) and boundary c-1 is not flagged, stop.  Returns true
 // iff the segment's end state (b_first[a]) moved; otherwise *stop = the chunk it
 // settled at.
-template <int J, int WP, bool VEC>
+template <int J, int WP, bool VEC, int MODE = 1>
 __device__ __forceinline__ bool bwd_segment(const FBParams& p, Bwd<J, WP>& st, int c0, int a, int j0, const float invz[J],
                             const int* flg, int& nrep, int* stop = nullptr) {
   const size_t SZ = (size_t)2 * p.Lpad;
@@ -1259,7 +1263,7 @@ __device__ __forceinline__ bool bwd_segment(const FBParams& p, Bwd<J, WP>& st, i
     st.save_state(p, p.b_in + (size_t)c * SZ, j0);
     float vp0[J], vp1[J];
     bwd_plain(p, st, j0, invz, t_e, vp0, vp1);
-    bwd_stream_out<J, WP, pf_relax_bwd<J>(), VEC, 1>(p, st, j0, invz, t_c, t_e, vp0, vp1, true);
+    bwd_stream_out<J, WP, pf_relax_bwd<J>(), VEC, MODE>(p, st, j0, invz, t_c, t_e, vp0, vp1, true);
     ++nrep;
     float* bf = p.b_first + (size_t)c * SZ;
     const float d = hilbert_reg<J>(st.b0, st.b1, bf, p.Lpad, j0, p.w_first + (size_t)c * SZ, p.Lpad);
@@ -1272,7 +1276,7 @@ __device__ __forceinline__ bool bwd_segment(const FBParams& p, Bwd<J, WP>& st, i
   return true;
 }
 
-template <int J, int WP, bool VEC>
+template <int J, int WP, bool VEC, int MODE = 1>
 __device__ __forceinline__ void backward_relax(const FBParams& p, int j0, const float invz[J]) {
   const size_t SZ = (size_t)2 * p.Lpad;
   const int s = blockIdx.x;
@@ -1290,7 +1294,7 @@ __device__ __forceinline__ void backward_relax(const FBParams& p, int j0, const 
     while (c0 >= 0) {
       st.load_state(p, p.b_in + (size_t)c0 * SZ, j0);
       int stop = a;
-      changed = bwd_segment<J, WP, VEC>(p, st, c0, a, j0, invz, p.flags, nrep, &stop);
+      changed = bwd_segment<J, WP, VEC, MODE>(p, st, c0, a, j0, invz, p.flags, nrep, &stop);
       if (changed) break;
       c0 = stop - 1 > a ? find_flag<-1>(p.flags, a, stop - 1) : -1;
     }
@@ -1307,7 +1311,7 @@ __device__ __forceinline__ void backward_relax(const FBParams& p, int j0, const 
         const float d = hilbert_dist(p.b_in + (size_t)(b - 1) * SZ, X, (int)SZ, w);
         if (!(d <= p.tol)) {
           st.load_state(p, X, j0);
-          changed = bwd_segment<J, WP, VEC>(p, st, b - 1, a, j0, invz, nullptr, nrep);
+          changed = bwd_segment<J, WP, VEC, MODE>(p, st, b - 1, a, j0, invz, nullptr, nrep);
         }
       }
     }
@@ -1329,7 +1333,10 @@ __global__ void __launch_bounds__(64) k_backward_relax(FBParams p_arg) {
   (void)lane;
   if constexpr (J % 4 == 0) {
     if ((p.L & 3) == 0) {
-      backward_relax<J, WP, true>(p, j0, invz);
+      // EM passes (P only): the main pass's P arithmetic (MODE 0: P bit-identical to a
+      // main pass from the same beta), no gamma / rho rows, no v kept
+      if (!p.gamma && !p.rho) backward_relax<J, WP, true, 0>(p, j0, invz);
+      else backward_relax<J, WP, true>(p, j0, invz);
       return;
     }
   }
