@@ -641,10 +641,11 @@ __device__ __forceinline__ void bem_load(const FBParams& p, int64_t t, int j0, E
 }
 
 // forward steps t in [t_a, t_b): OUT writes alpha / logc and returns sum logc; A1: also
-// alpha's d = 1 rows (p.a1_bytes of them; the EM passes omit them)
-template <int J, int WP, int PF, bool VEC, bool OUT, bool A1 = true>
-__device__ __forceinline__ double fwd_stream(const FBParams& p, Fwd<J, WP>& st, int j0, const float invz[J],
-                                             int64_t t_a, int64_t t_b) {
+// alpha's d = 1 rows (p.a1_bytes of them; the EM passes omit them).  MLDS: the row
+// references m_t come from sm (LDS, indexed t - t_a), else from a register ring
+template <int J, int WP, int PF, bool VEC, bool OUT, bool A1, bool MLDS>
+__device__ __forceinline__ double fwd_stream_piece(const FBParams& p, Fwd<J, WP>& st, int j0, const float invz[J],
+                                                   int64_t t_a, int64_t t_b, const double* sm) {
   double logz = 0.0;
   if (t_a >= t_b) return 0.0;
   const int64_t last = t_b - 1;
@@ -654,17 +655,18 @@ __device__ __forceinline__ double fwd_stream(const FBParams& p, Fwd<J, WP>& st, 
   for (int q = 0; q < PF; ++q) {
     const int64_t tl = t_a + q < last ? t_a + q : last;
     bem_load<J, VEC>(p, tl, j0, ring[q]);
-    if constexpr (OUT) mr[q] = p.m[tl * p.ldm];
+    if constexpr (OUT && !MLDS) mr[q] = p.m[tl * p.ldm];
   }
   auto body = [&](int q, int64_t t, bool refill) {
     float e[J];
     em_exp<J>(p, j0, ring[q], e);
     double mt = 0.0;
-    if constexpr (OUT) mt = mr[q];
+    if constexpr (OUT && MLDS) mt = sm[t - t_a];
+    if constexpr (OUT && !MLDS) mt = mr[q];
     if (refill) {
       const int64_t tl = t + PF < last ? t + PF : last;
       bem_load<J, VEC>(p, tl, j0, ring[q]);
-      if constexpr (OUT) mr[q] = p.m[tl * p.ldm];
+      if constexpr (OUT && !MLDS) mr[q] = p.m[tl * p.ldm];
     }
     const float S = st.step(p, j0, invz, e);
     if constexpr (OUT) {
@@ -694,6 +696,34 @@ __device__ __forceinline__ double fwd_stream(const FBParams& p, Fwd<J, WP>& st, 
   for (int q = 0; q < PF; ++q)
     if (tb + q < t_b) body(q, tb + q, false);
   return logz;
+}
+
+// The relaxation's output steps take the row references m_t from wave-local LDS, filled
+// per piece of <= kMPiece steps before the piece's step loop: there a plain global load of
+// m in the loop rotated through registers that the back-edge copied into the ring after a
+// vmcnt(0), i.e. behind every store of the ring cycle (profiles/r05_ab_experiments.txt
+// item 11).  The main passes keep the register ring, whose loops have no such drain and
+// whose waits the LDS form would tighten.
+#ifndef PMG_RELAX_MLDS
+#define PMG_RELAX_MLDS true
+#endif
+constexpr int kMPiece = 512;
+template <int J, int WP, int PF, bool VEC, bool OUT, bool A1 = true, bool MLDS = false>
+__device__ __forceinline__ double fwd_stream(const FBParams& p, Fwd<J, WP>& st, int j0, const float invz[J],
+                                             int64_t t_a, int64_t t_b) {
+  if constexpr (OUT && MLDS) {
+    __shared__ double sm[kMPiece];   // one wave per workgroup: no barrier, only the waits
+    const int lane = threadIdx.x & 63;
+    double logz = 0.0;
+    for (int64_t ta = t_a; ta < t_b; ta += kMPiece) {
+      const int64_t tz = ta + kMPiece < t_b ? ta + kMPiece : t_b;
+      for (int64_t t = ta + lane; t < tz; t += 64) sm[t - ta] = p.m[t * p.ldm];
+      __builtin_amdgcn_s_waitcnt(0);   // vmcnt(0) lgkmcnt(0): the piece's m is in LDS
+      logz += fwd_stream_piece<J, WP, PF, VEC, OUT, A1, true>(p, st, j0, invz, ta, tz, sm);
+    }
+    return logz;
+  }
+  return fwd_stream_piece<J, WP, PF, VEC, OUT, A1, false>(p, st, j0, invz, t_a, t_b, nullptr);
 }
 
 #define PMG_FB_LANE_SETUP                                               \
@@ -861,7 +891,7 @@ __device__ __forceinline__ bool fwd_segment(const FBParams& p, Fwd<J, WP>& st, i
     const int64_t t_c = (int64_t)c * p.C;
     const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
     st.save_state(p, p.s_in + (size_t)c * SZ, j0);
-    const double lz = fwd_stream<J, WP, pf_relax_fwd<J>(), VEC, true, A1>(p, st, j0, invz, t_c, t_e);
+    const double lz = fwd_stream<J, WP, pf_relax_fwd<J>(), VEC, true, A1, PMG_RELAX_MLDS>(p, st, j0, invz, t_c, t_e);
     if ((threadIdx.x & 63) == 0) p.chunk_logz[c] = lz;
     ++nrep;
     float* so = p.s_out + (size_t)c * SZ;
