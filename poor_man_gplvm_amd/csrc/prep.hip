@@ -104,33 +104,67 @@ __global__ void __launch_bounds__(256) k_spikes_prepare(
   }
 }
 
-__global__ void k_tuning_softplus(const float* __restrict__ basis, const double* __restrict__ W,
-                                  int L, int NB, int N, double* __restrict__ t64,
-                                  float* __restrict__ t32) {
-  // blockIdx.z = restart r of a batched fit: W (R, NB, N) -> rows r L + l of the stacked
-  // (R L, N) tuning
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  const int l = blockIdx.y;
-  if (n >= N) return;
+// tuning[l, n] = softplus(sum_k B[l, k] W[k, n]) (fit_tuning_helper.py:19-25) in f64.
+// A 64-thread workgroup owns 64 neurons x kTunRows latent rows: each W element is loaded
+// once per row tile (the per-row form re-read W's 323 KB 512 times at C3, 165 MB of L2
+// traffic for 2 MB of output), the tile's basis rows sit in LDS.  Larger tiles leave too
+// few waves to hide the f64 softplus latency (tools/tuning_bench.py).  Every
+// output keeps the round-4 summation order (four interleaved partial sums over k % 4,
+// combined (a0 + a1) + (a2 + a3), the tail into a0), so the tuning is bit-identical.
+// blockIdx.z = restart r of a batched fit: W (R, NB, N) -> rows r L + l of the stacked
+// (R L, N) tuning.
+constexpr int kTunRows = 2;   // C3: 12.6 (one row per workgroup) -> 9.1 us; 4 rows 10.9, 8 rows 16.6 (fewer waves)
+constexpr int kTunKC = 256;   // basis columns staged in LDS per pass (a multiple of 4)
+__global__ void __launch_bounds__(64) k_tuning_softplus(const float* __restrict__ basis, const double* __restrict__ W,
+                                                        int L, int NB, int N, double* __restrict__ t64,
+                                                        float* __restrict__ t32) {
+  __shared__ float sB[kTunRows * kTunKC];
+  const int n = blockIdx.x * 64 + threadIdx.x;
+  const bool live = n < N;
+  const int l0 = blockIdx.y * kTunRows;
   const int64_t r = blockIdx.z;
   W += r * NB * (int64_t)N;
-  const int64_t row = r * L + l;
-  const float* br = basis + (int64_t)l * NB;
-  // four interleaved partial sums (the f64 FMA chain, not the loads, bounded the single
-  // accumulator), combined in a fixed order
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-  int k = 0;
-  for (; k + 4 <= NB; k += 4) {
-    a0 = fma((double)br[k], W[(int64_t)k * N + n], a0);
-    a1 = fma((double)br[k + 1], W[(int64_t)(k + 1) * N + n], a1);
-    a2 = fma((double)br[k + 2], W[(int64_t)(k + 2) * N + n], a2);
-    a3 = fma((double)br[k + 3], W[(int64_t)(k + 3) * N + n], a3);
+  const int nr = L - l0 < kTunRows ? L - l0 : kTunRows;
+  const int NB4 = NB & ~3;
+  double a[kTunRows][4];
+#pragma unroll
+  for (int rr = 0; rr < kTunRows; ++rr) a[rr][0] = a[rr][1] = a[rr][2] = a[rr][3] = 0.0;
+  for (int kc = 0; kc < NB; kc += kTunKC) {
+    const int kw = NB - kc < kTunKC ? NB - kc : kTunKC;
+    __syncthreads();   // the previous pass's reads are done
+    for (int i = threadIdx.x; i < kTunRows * kw; i += 64) {
+      const int rr = i / kw, k = i - rr * kw;
+      sB[rr * kTunKC + k] = rr < nr ? basis[(int64_t)(l0 + rr) * NB + kc + k] : 0.f;
+    }
+    __syncthreads();
+    if (live) {
+      const int k4 = (NB4 - kc) < kw ? (NB4 - kc) : kw;   // this pass's columns of the k % 4 sums
+      int k = 0;
+      for (; k + 4 <= k4; k += 4) {
+        double w[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = W[(int64_t)(kc + k + j) * N + n];
+#pragma unroll
+        for (int rr = 0; rr < kTunRows; ++rr)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) a[rr][j] = fma((double)sB[rr * kTunKC + k + j], w[j], a[rr][j]);
+      }
+      for (k = k4 > 0 ? k4 : 0; k < kw; ++k) {   // the NB % 4 tail (last pass only)
+        const double w = W[(int64_t)(kc + k) * N + n];
+#pragma unroll
+        for (int rr = 0; rr < kTunRows; ++rr) a[rr][0] = fma((double)sB[rr * kTunKC + k], w, a[rr][0]);
+      }
+    }
   }
-  for (; k < NB; ++k) a0 = fma((double)br[k], W[(int64_t)k * N + n], a0);
-  const double acc = (a0 + a1) + (a2 + a3);
-  double f = softplus_d(acc);
-  if (t64) t64[row * N + n] = f;
-  if (t32) t32[row * N + n] = (float)f;
+  if (!live) return;
+#pragma unroll
+  for (int rr = 0; rr < kTunRows; ++rr) {
+    if (rr >= nr) break;
+    const int64_t row = r * L + l0 + rr;
+    const double f = softplus_d((a[rr][0] + a[rr][1]) + (a[rr][2] + a[rr][3]));
+    if (t64) t64[row * N + n] = f;
+    if (t32) t32[row * N + n] = (float)f;
+  }
 }
 
 // Row references: per (t, group) the max over the group's nb = nblk / R blocks (R groups
@@ -288,8 +322,8 @@ int pmg_tuning_softplus(const float* basis, const double* W, int32_t L, int32_t 
 int pmg_tuning_softplus_batched(const float* basis, const double* W, int32_t L, int32_t NB, int32_t N, int32_t R,
                                 double* tuning64, float* tuning32, void* stream) {
   PMG_REQUIRE(L > 0 && NB > 0 && N > 0 && R > 0 && R <= 65535 && basis && W, "pmg_tuning_softplus: bad args");
-  dim3 grid((N + 127) / 128, L, R);
-  hipLaunchKernelGGL(k_tuning_softplus, grid, dim3(128), 0, as_stream(stream), basis, W, L, NB,
+  dim3 grid((N + 63) / 64, (L + kTunRows - 1) / kTunRows, R);
+  hipLaunchKernelGGL(k_tuning_softplus, grid, dim3(64), 0, as_stream(stream), basis, W, L, NB,
                      N, tuning64, tuning32);
   PMG_LAUNCH_CHECK();
   return PMG_OK;
