@@ -545,6 +545,9 @@ __global__ void __launch_bounds__(1024) k_emission_pipe(
 //   maxima and one half-wave swap per row (it was a 5-step cross-lane reduction per output
 //   row), and delta leaves as 16-B stores: emission 164 -> 140 us at C3.
 // Bit-identical to k_emission_i8 (same int32 digit sums, same f64 epilogue).
+#ifndef PMG_RBLK_PAIRS
+#define PMG_RBLK_PAIRS 1   // 0: one 8-byte rblk store per item (round 4; A/B builds)
+#endif
 constexpr int RT = 256, RLW = 32;                       // time bins, latents per work item
 constexpr int RLC_MAX = 4096;                            // latents of the LDS lconst table
 // chunk of CK neurons (128 or 256 B digit rows): ring slots and DMA pieces
@@ -623,9 +626,12 @@ __global__ void __launch_bounds__(512) k_emission_yreg(
   // VMEM stores per epilogue, a lower bound over both store forms (4 x 16 B delta + 1 rblk
   // (+ 8 x 16 B ll) when L % 4 == 0, 16 + 1 (+ 16) otherwise): the counted waits below
   // must never assume more younger stores than were issued
-  constexpr int NST = LL ? 13 : 5;
+  constexpr int NST = (LL ? 13 : 5) - (PMG_RBLK_PAIRS ? 1 : 0);   // a held rblk block stores nothing
   v16i acc[kDig];
   int cur_tt = -1;
+#if PMG_RBLK_PAIRS
+  unsigned long long rb_hold = 0;   // the held even block maximum (h == 0 lanes)
+#endif
   for (int xi = 0; xi < mine; ++xi) {
     const int it = i0 + xi;
     const int tt = it / nLT;
@@ -768,9 +774,23 @@ __global__ void __launch_bounds__(512) k_emission_yreg(
           }
         }
       }
-      const uint32_t ob = (h == 0 && tvalid) ? (uint32_t)(tr * nblk + blk) * 8u : 0x80000000u;
       const unsigned long long mu = (unsigned long long)__double_as_longlong(mx);
-      __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)mu, (uint32_t)(mu >> 32)}, rr, ob, 0, 0);
+#if PMG_RBLK_PAIRS
+      // rblk in 16-byte pairs: an even block whose odd partner is this workgroup's next item
+      // (same time tile) is held in a register and written with it, so each row's 8-byte
+      // block maxima reach memory in half as many (and twice as wide) partial-line writes
+      if ((blk & 1) == 0 && blk + 1 < nLT && xi + 1 < mine) {
+        rb_hold = mu;
+      } else if ((blk & 1) == 1 && xi > 0) {
+        const uint32_t ob = (h == 0 && tvalid) ? (uint32_t)(tr * nblk + blk - 1) * 8u : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128((v4u){(uint32_t)rb_hold, (uint32_t)(rb_hold >> 32), (uint32_t)mu,
+                                                     (uint32_t)(mu >> 32)}, rr, ob, 0, 0);
+      } else
+#endif
+      {
+        const uint32_t ob = (h == 0 && tvalid) ? (uint32_t)(tr * nblk + blk) * 8u : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)mu, (uint32_t)(mu >> 32)}, rr, ob, 0, 0);
+      }
     }
   }
 #undef PMG_YR_ISSUE
