@@ -548,6 +548,10 @@ __global__ void __launch_bounds__(1024) k_emission_pipe(
 #ifndef PMG_RBLK_PAIRS
 #define PMG_RBLK_PAIRS 1   // 0: one 8-byte rblk store per item (round 4; A/B builds)
 #endif
+#ifndef PMG_RBLK_RUN
+#define PMG_RBLK_RUN 4
+#endif
+constexpr int kRbRun = PMG_RBLK_RUN;   // 2 or 4 blocks per rblk run
 constexpr int RT = 256, RLW = 32;                       // time bins, latents per work item
 constexpr int RLC_MAX = 4096;                            // latents of the LDS lconst table
 // chunk of CK neurons (128 or 256 B digit rows): ring slots and DMA pieces
@@ -630,7 +634,8 @@ __global__ void __launch_bounds__(512) k_emission_yreg(
   v16i acc[kDig];
   int cur_tt = -1;
 #if PMG_RBLK_PAIRS
-  unsigned long long rb_hold = 0;   // the held even block maximum (h == 0 lanes)
+  unsigned long long rb_h0 = 0, rb_h1 = 0, rb_h2 = 0;   // held block maxima of the open run
+  int rb_n = 0;                                          // (uniform) blocks held
 #endif
   for (int xi = 0; xi < mine; ++xi) {
     const int it = i0 + xi;
@@ -776,15 +781,31 @@ __global__ void __launch_bounds__(512) k_emission_yreg(
       }
       const unsigned long long mu = (unsigned long long)__double_as_longlong(mx);
 #if PMG_RBLK_PAIRS
-      // rblk in 16-byte pairs: an even block whose odd partner is this workgroup's next item
-      // (same time tile) is held in a register and written with it, so each row's 8-byte
-      // block maxima reach memory in half as many (and twice as wide) partial-line writes
-      if ((blk & 1) == 0 && blk + 1 < nLT && xi + 1 < mine) {
-        rb_hold = mu;
-      } else if ((blk & 1) == 1 && xi > 0) {
-        const uint32_t ob = (h == 0 && tvalid) ? (uint32_t)(tr * nblk + blk - 1) * 8u : 0x80000000u;
-        __builtin_amdgcn_raw_buffer_store_b128((v4u){(uint32_t)rb_hold, (uint32_t)(rb_hold >> 32), (uint32_t)mu,
-                                                     (uint32_t)(mu >> 32)}, rr, ob, 0, 0);
+      // rblk in runs of up to kRbRun blocks: a block whose successor is this workgroup's next
+      // item (same time tile) and does not end a run is held in registers and written with
+      // the run, so each row's 8-byte block maxima reach memory in fewer, wider partial-line
+      // writes (one 8-byte store per item before)
+      if ((blk % kRbRun) != kRbRun - 1 && blk + 1 < nLT && xi + 1 < mine) {
+        if (rb_n == 0) rb_h0 = mu;
+        else if (rb_n == 1) rb_h1 = mu;
+        else rb_h2 = mu;
+        ++rb_n;
+      } else if (rb_n > 0) {
+        const uint32_t ob = (h == 0 && tvalid) ? (uint32_t)(tr * nblk + blk - rb_n) * 8u : 0x80000000u;
+        if (rb_n == 1) {
+          __builtin_amdgcn_raw_buffer_store_b128((v4u){(uint32_t)rb_h0, (uint32_t)(rb_h0 >> 32), (uint32_t)mu,
+                                                       (uint32_t)(mu >> 32)}, rr, ob, 0, 0);
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b128((v4u){(uint32_t)rb_h0, (uint32_t)(rb_h0 >> 32), (uint32_t)rb_h1,
+                                                       (uint32_t)(rb_h1 >> 32)}, rr, ob, 0, 0);
+          const uint32_t ob2 = ob == 0x80000000u ? ob : ob + 16u;
+          if (rb_n == 2)
+            __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)mu, (uint32_t)(mu >> 32)}, rr, ob2, 0, 0);
+          else
+            __builtin_amdgcn_raw_buffer_store_b128((v4u){(uint32_t)rb_h2, (uint32_t)(rb_h2 >> 32), (uint32_t)mu,
+                                                         (uint32_t)(mu >> 32)}, rr, ob2, 0, 0);
+        }
+        rb_n = 0;
       } else
 #endif
       {
