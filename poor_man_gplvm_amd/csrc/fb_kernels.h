@@ -51,6 +51,12 @@ constexpr int kMaxBand = 32;
 // Emission / alpha rows are prefetched this many steps ahead on the chunk-parallel
 // kernels: with ~2 waves per SIMD the step's VALU work (~0.3 us) cannot cover an HBM
 // round trip (~2 us), so the row ring, not other waves, hides the latency.
+// The forward's alpha (d = 0) rows are stored non-temporally (nt): with them out of the
+// caches the backward pass, which reads delta + alpha, ran 11-16 us faster and the forward
+// 2-5 us slower (profiles/r05_ab_experiments.txt item 18).  0 = the default policy (A/B).
+#ifndef PMG_ALPHA_AUX
+#define PMG_ALPHA_AUX 2
+#endif
 constexpr int kPfFwd = 4;
 constexpr int kPfBwdWarm = 4;
 constexpr int kPfBwdOut = 2;
@@ -555,7 +561,7 @@ __device__ __forceinline__ void bload_row(const float* row, int L, int j0, float
 }
 
 // bytes: the row's extent (lanes past it drop their stores; 0 = the row is not written)
-template <int J, bool VEC>
+template <int J, bool VEC, int AUX = 0>
 __device__ __forceinline__ void bstore_row_n(float* row, uint32_t bytes, int j0, const float v[J]) {
   const __amdgpu_buffer_rsrc_t rs = rsrc_of(row, bytes);
   if constexpr (VEC) {
@@ -566,11 +572,11 @@ __device__ __forceinline__ void bstore_row_n(float* row, uint32_t bytes, int j0,
       q.y = __float_as_uint(v[j + 1]);
       q.z = __float_as_uint(v[j + 2]);
       q.w = __float_as_uint(v[j + 3]);
-      __builtin_amdgcn_raw_buffer_store_b128(q, rs, (j0 + j) * 4, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(q, rs, (j0 + j) * 4, 0, AUX);
     }
   } else {
 #pragma unroll
-    for (int j = 0; j < J; ++j) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[j]), rs, (j0 + j) * 4, 0, 0);
+    for (int j = 0; j < J; ++j) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[j]), rs, (j0 + j) * 4, 0, AUX);
   }
 }
 
@@ -674,7 +680,7 @@ __device__ __forceinline__ double fwd_stream_piece(const FBParams& p, Fwd<J, WP>
       float a0[J];
 #pragma unroll
       for (int j = 0; j < J; ++j) a0[j] = st.q0[j] * st.iS;
-      bstore_row_n<J, VEC>(arow, p.a0_bytes, j0, a0);
+      bstore_row_n<J, VEC, PMG_ALPHA_AUX>(arow, p.a0_bytes, j0, a0);
       if constexpr (A1) {   // alpha's d = 1 row, as the backward rebuilds it
         float a1[J];
 #pragma unroll
