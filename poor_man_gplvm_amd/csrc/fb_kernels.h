@@ -51,9 +51,11 @@ constexpr int kMaxBand = 32;
 // Emission / alpha rows are prefetched this many steps ahead on the chunk-parallel
 // kernels: with ~2 waves per SIMD the step's VALU work (~0.3 us) cannot cover an HBM
 // round trip (~2 us), so the row ring, not other waves, hides the latency.
-// The forward's alpha (d = 0) rows are stored non-temporally (nt): with them out of the
-// caches the backward pass, which reads delta + alpha, ran 11-16 us faster and the forward
-// 2-5 us slower (profiles/r05_ab_experiments.txt item 18).  0 = the default policy (A/B).
+// The forward's alpha (d = 0) rows are stored non-temporally (nt) for L <= 512 (J <= 8):
+// with them out of the caches the C3 backward pass, which reads delta + alpha, ran 11-16 us
+// faster and the forward 2-5 us slower; at L = 1024 (J = 16, the C4 shard) the forward ran
+// 25 % slower with them, so J = 16 keeps the default policy (profiles/r05_ab_experiments.txt
+// item 18).  0 = the default policy everywhere (A/B builds).
 #ifndef PMG_ALPHA_AUX
 #define PMG_ALPHA_AUX 2
 #endif
@@ -680,7 +682,7 @@ __device__ __forceinline__ double fwd_stream_piece(const FBParams& p, Fwd<J, WP>
       float a0[J];
 #pragma unroll
       for (int j = 0; j < J; ++j) a0[j] = st.q0[j] * st.iS;
-      bstore_row_n<J, VEC, PMG_ALPHA_AUX>(arow, p.a0_bytes, j0, a0);
+      bstore_row_n<J, VEC, (J <= 8 ? PMG_ALPHA_AUX : 0)>(arow, p.a0_bytes, j0, a0);
       if constexpr (A1) {   // alpha's d = 1 row, as the backward rebuilds it
         float a1[J];
 #pragma unroll
