@@ -376,7 +376,8 @@ int pmg_joint_log_accumulate(const double* log_alpha, const double* log_rho, int
                              void* stream);
 /* The same with a caller-owned workspace of pmg_joint_log_workspace_size bytes, which  */
 /* lets the time axis split over more workgroups (their (max, sum) partials are folded  */
-/* in split order).  Per block of 64 steps the logs are shifted by their row / column  */
+/* in split order).  The size is 0 when the 64 x 64 output tiles alone fill the chip   */
+/* (e.g. L >= 1024): the joint then runs unsplit and needs no workspace (pass NULL).  Per block of 64 steps the logs are shifted by their row / column  */
 /* maxima and exponentiated once per (row, step), the block sum is an f64 contraction, */
 /* and an entry whose block sum leaves f64's range is summed term by term in log space. */
 size_t pmg_joint_log_workspace_size(int64_t T, int32_t L);

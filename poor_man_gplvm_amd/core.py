@@ -107,8 +107,9 @@ class _PinnedCopies:
         host = q.pop(0).result() if q else nat.host_array(tuple(t.shape), _NP_DTYPE[t.dtype])
         if host.shape != tuple(t.shape) or host.dtype != _NP_DTYPE[t.dtype]:
             raise ValueError("reserved host buffer does not match the tensor")
-        nat.check(nat.load().pmg_copy_d2h(host.ctypes.data, t.data_ptr(), nbytes, st.cuda_stream),
-                  "pmg_copy_d2h")
+        if nbytes:   # an empty tensor (e.g. run_em(n_iter=0)'s histories) has nothing to copy
+            nat.check(nat.load().pmg_copy_d2h(host.ctypes.data, t.data_ptr(), nbytes, st.cuda_stream),
+                      "pmg_copy_d2h")
         self.items.append(host)
         return host
 
@@ -778,6 +779,10 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
     noise_std: Gaussian observation model (analytic M-step, linear tuning; adam.prior_std
     is the parameter prior) instead of the Poisson one.
     `timing`, if a list, receives per-iteration wall-clock seconds (bench)."""
+    if int(n_iter) < 1:
+        # the reference's fit_em defines tuning / log_posterior_all inside its loop and
+        # fails after a 0-iteration loop (core.py:650-681); never return an unset posterior
+        raise ValueError(f"n_iter must be >= 1 (got {n_iter})")
     adam = adam or AdamConfig()
     y = np.asarray(y)
     T = y.shape[0]
@@ -872,7 +877,7 @@ def run_em(y, params, basis, log_posterior_init, n_iter, transition, ma_neuron=N
            'params': h_W.astype(np.float32),
            'tuning': h_tun,
            'log_posterior_final': _masked_log(h_lpf, mlat),
-           'log_marginal': float(lz[n_iter - 1]) if n_iter else float('nan'),
+           'log_marginal': float(lz[n_iter - 1]),
            'log_marginal_l': [float(v) for v in lz[:n_iter]],
            'log_marginal_saved': saved['log_marginal_saved'],
            'posterior': posterior,

@@ -1294,10 +1294,23 @@ int pmg_dense_backward_phase(const float* delta, const float* phi, const double*
                              log_gamma, rho, log_rho, workspace, workspace_bytes, stream, phase);
 }
 
+// time splits of the joint: enough workgroups to fill the chip (one 64 x 64 tile each),
+// each split at least a few blocks long; 1 (no workspace partials) when the tiles alone fill it
+static int joint_log_splits(int64_t T, int32_t L) {
+  const int L2 = 2 * L;
+  const int64_t tiles = (int64_t)((L2 + kJT - 1) / kJT) * ((L2 + kJT - 1) / kJT);
+  int nsplit = 1;
+  while (nsplit < kJointSplits && tiles * nsplit < 1024 && (T - 1) / (2 * nsplit) >= 4 * kJB) nsplit *= 2;
+  return nsplit;
+}
+
+// the partials of the splits (two f64 per entry and split), or 0 when the joint runs unsplit
 size_t pmg_joint_log_workspace_size(int64_t T, int32_t L) {
   if (T <= 0 || L <= 0) return 0;
+  const int nsplit = joint_log_splits(T, L);
+  if (nsplit == 1) return 0;
   const int64_t n = (int64_t)(2 * L) * (2 * L);
-  return (size_t)kJointSplits * (size_t)n * 2 * sizeof(double) + 256;
+  return (size_t)nsplit * (size_t)n * 2 * sizeof(double) + 256;
 }
 
 int pmg_joint_log_accumulate_ws(const double* log_alpha, const double* log_rho, int64_t T, int32_t L, double* logS,
@@ -1305,13 +1318,11 @@ int pmg_joint_log_accumulate_ws(const double* log_alpha, const double* log_rho, 
   PMG_REQUIRE(log_alpha && log_rho && logS && T > 0 && L > 0, "pmg_joint_log_accumulate: bad argument");
   const int L2 = 2 * L;
   const int64_t n = (int64_t)L2 * L2;
-  // time splits: enough workgroups to fill the chip (one 64 x 64 tile each), each split
-  // at least a few blocks long
+  // split in time only with a workspace of the size pmg_joint_log_workspace_size asks for
   int nsplit = 1;
   if (workspace) {
     PMG_REQUIRE(workspace_bytes >= pmg_joint_log_workspace_size(T, L), "pmg_joint_log_accumulate: workspace too small");
-    const int64_t tiles = (int64_t)((L2 + kJT - 1) / kJT) * ((L2 + kJT - 1) / kJT);
-    while (nsplit < kJointSplits && tiles * nsplit < 1024 && (T - 1) / (2 * nsplit) >= 4 * kJB) nsplit *= 2;
+    nsplit = joint_log_splits(T, L);
   }
   const int64_t per = ((T - 1 + nsplit - 1) / nsplit + kJB - 1) / kJB * kJB;
   dim3 grid((L2 + kJT - 1) / kJT, (L2 + kJT - 1) / kJT, nsplit);

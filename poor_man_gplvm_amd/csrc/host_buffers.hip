@@ -64,8 +64,8 @@ extern "C" int pmg_host_free(void* p, size_t bytes) {
 // device -> host copy of `bytes` into a pmg_host_alloc buffer, enqueued on `stream`
 // (the caller synchronises the stream before reading dst)
 extern "C" int pmg_copy_d2h(void* dst, const void* src, size_t bytes, void* stream) {
+  if (bytes == 0) return PMG_OK;   // nothing to copy (an empty tensor's data pointer is NULL)
   PMG_REQUIRE(dst != nullptr && src != nullptr, "pmg_copy_d2h: null pointer");
-  if (bytes == 0) return PMG_OK;
   PMG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ::pmg::as_stream(stream)));
   return PMG_OK;
 }

@@ -810,10 +810,13 @@ class DeviceEM:
     def joint_log(self, log_rho):
         """Dense scans: log S[x,x'] = LSE_t log alpha_t[x] + log rho_{t+1}[x'] (2L x 2L, f64)."""
         S = torch.empty((2 * self.L, 2 * self.L), dtype=torch.float64, device=self.dev)
-        ws = torch.empty(int(self.lib.pmg_joint_log_workspace_size(self.T, self.L)), dtype=torch.uint8, device=self.dev)
+        # split partials only when the tiles alone leave the chip idle (size 0 otherwise, e.g. L >= 1024)
+        nws = int(self.lib.pmg_joint_log_workspace_size(self.T, self.L))
+        ws = torch.empty(nws, dtype=torch.uint8, device=self.dev) if nws else None
         with self._t('joint_log'):
             nat.check(self.lib.pmg_joint_log_accumulate_ws(nat.ptr(self.log_alpha), nat.ptr(log_rho), self.T, self.L,
-                                                           nat.ptr(S), nat.ptr(ws), ws.numel(), nat.stream_handle()),
+                                                           nat.ptr(S), nat.ptr(ws) if nws else None, nws,
+                                                           nat.stream_handle()),
                       "pmg_joint_log_accumulate")
         return S
 
@@ -958,9 +961,14 @@ class RestartBatchEM:
         self.alpha = torch.empty((R, T, 2, L), dtype=f32, device=dev)
         self.logc = torch.empty((R, T), dtype=f64, device=dev)
         self._P = torch.empty((T, LA), dtype=f32, device=dev)
-        # as DeviceEM: P as its exact bf16 planes between the backward and the statistics
-        # (both the batched and the one-restart fit take the same statistics kernel, so a
-        # restart alone on the batch's grid reproduces its batched fit)
+        # as DeviceEM: P as its exact bf16 planes between the backward and the statistics.
+        # The gate here is the stacked width R L, a lone restart's is L, so near the 2 GiB
+        # plane bound a batch can take the f32-P path where the lone restart takes the
+        # planes.  The two paths give y_w bit for bit (the planes are the exact split of
+        # the same f32 P that k_ptb3 splits in-kernel) and t_w to ~1e-8 (f32 group sums over
+        # different time groupings; test_backward_planes_bit_identical,
+        # test_suffstats_vs_numpy), inside the restart-equivalence bar of 1e-6
+        # (tests/test_gpu_restarts.py).  PLANES is off by default in both engines.
         self.use_planes = bool(self.PLANES and spikes.ybt is not None and planes_ok(T, LA))
         self.Pq = torch.empty((3, T, LA), dtype=torch.int16, device=dev) if self.use_planes else None
         self._p_fresh = 'f32'

@@ -1,5 +1,5 @@
 """Rounding-ensemble fixtures for the long M-step tests (run from the repo root:
-`python tests/golden/make_ensemble.py [adam|c1|c3|c4] [workers]`).
+`python tests/golden/make_ensemble.py [adam|c1|c2m|c3|c4] [workers]`).
 
 A long Adam loop at the C3 shape is chaotic at the f64 ulp: after ~650 bodies, elements
 with gradients near zero take +-lr steps whose sign is decided by rounding, so two f64
@@ -18,6 +18,9 @@ Fixtures:
                         fit_em n_iter=20, maxiter 1000, tol 1e-6), base run + ensemble
   c3_em_ensemble.npz    the one-EM-iteration C3 case of c3_sample.npz (864 Adam bodies,
                         then the E-step at T=5000): ensemble spread of tuning and posterior
+  em_c2_multi.npz       a 4-iteration fit at the C2 shape (N = 128, L = 256, T = 1e4,
+                        tests.synth.make; maxiter 1000, tol 1e-6 in every M-step): the
+                        base run's outputs and the ensemble spread of every iteration
   adam_c4_ensemble.npz  the first M-step of the C4 shape (N = L = 1024, 154 basis columns,
                         T = 1e6: bench.synth_long), the 1000-body loop under tol 1e-6, on
                         the statistics of the posterior init (P = f32(exp(lp0)), as the
@@ -157,6 +160,49 @@ def c3_case(pool):
           % (max(tun_dev), np.median(tun_dev), max(post_dev), max(tw_dev), max(lml_dev), flips))
 
 
+# ----------------------------------------------------------------------------- C2 multi-iteration fit
+C2M = dict(N=128, L=256, T=10000, n_iter=4, maxiter=1000, tol=1e-6, n_rows=512)
+
+
+def _c2m_member(k):
+    d = make(C2M['N'], C2M['L'], C2M['T'])
+    kw = dict(n_iter=C2M['n_iter'], m_step_maxiter=C2M['maxiter'], m_step_tol=C2M['tol'])
+    if k >= 0:
+        kw['stats_perturb'] = (np.random.default_rng(5000 + k), EPS)
+    r = O.fit_em(d['y'], d['W0'].astype(np.float64), d['B'].astype(np.float64), d['lp0'].astype(np.float64), **kw)
+    plm = r['posterior_latent_marg']
+    rows = np.random.default_rng(11).choice(C2M['T'], C2M['n_rows'], replace=False)
+    m = r['m_step_res_l']
+    return k, dict(tuning=r['tuning'], params=r['params'], rows=plm[rows], argmax=plm.argmax(1), tw=plm.sum(0),
+                   lml=np.array(r['log_marginal_l']), n_iter=np.array(m['n_iter']),
+                   final_loss=np.array(m['final_loss']), row_idx=rows)
+
+
+def c2m_case(pool):
+    res = dict(pool.map(_c2m_member, range(-1, K)))
+    b = res[-1]
+    ens = [res[k] for k in range(K)]
+    tun_dev = [_rel(e['tuning'], b['tuning']) for e in ens]
+    post_dev = [float(np.abs(e['rows'] - b['rows']).max()) for e in ens]
+    tw_dev = [float(np.abs(e['tw'] - b['tw']).sum() / C2M['T']) for e in ens]
+    lml_dev = [_rel(e['lml'], b['lml']) for e in ens]
+    loss_dev = [_rel(e['final_loss'], b['final_loss']) for e in ens]
+    flips = [int((e['argmax'] != b['argmax']).sum()) for e in ens]
+    n_iter = np.array([e['n_iter'] for e in ens])
+    np.savez_compressed(
+        os.path.join(HERE, 'em_c2_multi.npz'), N=C2M['N'], L=C2M['L'], T=C2M['T'], n_iter=C2M['n_iter'],
+        maxiter=C2M['maxiter'], tol=C2M['tol'], rows=b['row_idx'], params=b['params'], tuning=b['tuning'],
+        posterior_latent_rows=b['rows'].astype(np.float64), argmax=b['argmax'].astype(np.int16), tw=b['tw'],
+        log_marginal_l=b['lml'], m_n_iter=b['n_iter'], m_final_loss=b['final_loss'],
+        ens_tuning_dev=np.array(tun_dev), ens_posterior_dev=np.array(post_dev), ens_tw_dev=np.array(tw_dev),
+        ens_log_marginal_dev=np.array(lml_dev), ens_final_loss_dev=np.array(loss_dev),
+        ens_argmax_flips=np.array(flips), ens_m_n_iter=n_iter, eps=EPS, seed0=5000)
+    print('C2 4-iteration fit: n_iter', list(b['n_iter']))
+    print('  ensemble n_iter rows differing from base:', int((n_iter != b['n_iter'][None]).any(1).sum()))
+    print('  tuning dev max %.3e median %.3e; posterior rows %.3e; tw %.3e; lml %.2e; loss %.2e; flips %s'
+          % (max(tun_dev), np.median(tun_dev), max(post_dev), max(tw_dev), max(lml_dev), max(loss_dev), flips))
+
+
 # ----------------------------------------------------------------------------- C4 first M-step
 C4 = dict(N=1024, T=1000000, L=1024)
 C4_STATS = os.path.join(os.environ.get('TMPDIR', '/tmp'), 'pmg_c4_first_mstep_stats.npz')
@@ -215,7 +261,7 @@ def main():
     os.environ.setdefault('OMP_NUM_THREADS', '1')
     with get_context('spawn').Pool(workers) as pool:
         for w in which:
-            {'adam': adam_case, 'c1': c1_case, 'c3': c3_case, 'c4': c4_case}[w](pool)
+            {'adam': adam_case, 'c1': c1_case, 'c2m': c2m_case, 'c3': c3_case, 'c4': c4_case}[w](pool)
 
 
 if __name__ == '__main__':

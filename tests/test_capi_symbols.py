@@ -34,6 +34,13 @@ def test_abi_version_and_workspace_queries():
     assert lib.pmg_suffstats_workspace_size(1000, 100, 64) > 0
     assert lib.pmg_joint_workspace_size(1000, 100) > 0
     assert lib.pmg_mstep_workspace_size(512, 1000) > 0
+    # the log-domain joint's split partials: only where the joint splits in time
+    # (the workspace was sized for 8 splits even where none runs)
+    assert lib.pmg_joint_log_workspace_size(100000, 1024) == 0      # 32 x 32 tiles fill the chip
+    assert lib.pmg_joint_log_workspace_size(100000, 2048) == 0
+    assert lib.pmg_joint_log_workspace_size(100000, 512) == 4 * 1024 * 1024 * 16 + 256
+    assert lib.pmg_joint_log_workspace_size(100000, 64) == 8 * 128 * 128 * 16 + 256
+    assert lib.pmg_joint_log_workspace_size(200, 64) == 0            # too short to split
 
 
 def test_invalid_arguments_are_rejected_without_gpu():
@@ -41,3 +48,11 @@ def test_invalid_arguments_are_rejected_without_gpu():
     rc = lib.pmg_spikes_prepare(None, 0, 0, None, 0, None, 0, None, None, 0, None, None)
     assert rc == -1
     assert b'T=0' in lib.pmg_last_error()
+
+
+def test_zero_byte_copy_is_a_no_op():
+    """pmg_copy_d2h of 0 bytes succeeds whatever the pointers (an empty tensor's data
+    pointer is NULL) and touches no device."""
+    lib = _native.load()
+    assert lib.pmg_copy_d2h(None, None, 0, None) == 0
+    assert lib.pmg_copy_d2h(None, None, 8, None) == -1

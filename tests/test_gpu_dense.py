@@ -215,7 +215,9 @@ def test_joint_log_accumulate_vs_logsumexp(T, L, spread, ws):
     r = torch.as_tensor(lr, device='cuda')
     S = torch.empty((L2, L2), dtype=torch.float64, device='cuda')
     if ws:
-        w = torch.empty(int(lib.pmg_joint_log_workspace_size(T, L)), dtype=torch.uint8, device='cuda')
+        nws = int(lib.pmg_joint_log_workspace_size(T, L))
+        assert nws > 0          # these shapes split in time: the combine path runs
+        w = torch.empty(nws, dtype=torch.uint8, device='cuda')
         nat.check(lib.pmg_joint_log_accumulate_ws(nat.ptr(a), nat.ptr(r), T, L, nat.ptr(S), nat.ptr(w), w.numel(),
                                                   nat.stream_handle()), "joint")
     else:
@@ -227,3 +229,36 @@ def test_joint_log_accumulate_vs_logsumexp(T, L, spread, ws):
     assert np.array_equal(np.isfinite(got), fin)
     assert np.all(np.isneginf(got[~fin]))
     np.testing.assert_allclose(got[fin], ref[fin], rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.parametrize("T,L", [(200, 40), (4000, 16)])
+def test_joint_log_block_fallback_deterministic(T, L):
+    """The blocked joint's term-by-term fallback, forced: latent 1 of log
+    alpha sits 900 nats below latent 0 at every step, so inside every 64 x 64 tile and
+    64-step block its shifted terms underflow to 0 and the block sum of every entry of
+    row 1 is 0; the right answer, -900 + lr + log(T - 1), is finite only if the fallback
+    ran.  (4000, 16): a shape whose workspace size is nonzero, so the time splits and their
+    combine run as well; (200, 40) runs unsplit."""
+    from poor_man_gplvm_amd import _native as nat
+    from scipy.special import logsumexp
+    L2 = 2 * L
+    la = np.zeros((T, L2))
+    la[:, 1] = -900.0
+    la[:, 5] = -1600.0
+    rng = np.random.default_rng(T + L)
+    lr = rng.standard_normal((T, L2)) * 0.1
+    lr[:, 2] -= 850.0                      # a column 850 nats down: entry (1, 2) is ~1750 below the tile max
+    lib = nat.load()
+    nws = int(lib.pmg_joint_log_workspace_size(T, L))
+    assert (nws > 0) == (T >= 2048)
+    a = torch.as_tensor(la, device='cuda')
+    r = torch.as_tensor(lr, device='cuda')
+    S = torch.empty((L2, L2), dtype=torch.float64, device='cuda')
+    w = torch.empty(nws, dtype=torch.uint8, device='cuda') if nws else None
+    nat.check(lib.pmg_joint_log_accumulate_ws(nat.ptr(a), nat.ptr(r), T, L, nat.ptr(S), nat.ptr(w), nws,
+                                              nat.stream_handle()), "joint")
+    got = S.cpu().numpy()
+    ref = logsumexp(la[:-1, :, None] + lr[1:, None, :], axis=0)
+    assert np.all(np.isfinite(got))
+    np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-9)
+    assert got[1, 2] < -1700 and got[5, 2] < -2400

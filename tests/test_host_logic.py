@@ -119,6 +119,15 @@ def test_product_fails_loudly_without_gpu():
         m.fit_em(np.zeros((10, 5)), n_iter=1)
 
 
+def test_run_em_rejects_zero_iterations():
+    """n_iter = 0: the reference's loop leaves tuning / log_posterior_all unset and fails
+    (core.py:650-681); run_em raises before any device work instead of returning an unset
+    posterior."""
+    with pytest.raises(ValueError, match="n_iter"):
+        P.run_em(np.zeros((10, 5), np.float32), np.zeros((3, 5)), np.ones((16, 3), np.float32),
+                 np.zeros((10, 16), np.float32), n_iter=0, transition=None)
+
+
 def test_transition_posterior_key_order_matches_notebook():
     lj = np.log(np.random.default_rng(0).random((2, 2, 5, 5)))
     r = P.compute_transition_posterior_prob(lj)
