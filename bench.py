@@ -364,6 +364,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--chunk-bwd", type=int, default=0, help="backward chunk (0: ScanConfig default, 2x forward)")
     ap.add_argument("--warm-steps", type=int, default=48)
+    ap.add_argument("--two-waves", action="store_true", help="main-pass chains on two waves (PMG_PHASE_TWO_WAVES)")
     ap.add_argument("--scan-tol", type=float, default=0.0, help="boundary tolerance (0: ScanConfig default)")
     ap.add_argument("--warm-fb", type=str, default="", help="fixed forward,backward warm-up (no adaptation)")
     ap.add_argument("--verbose", action="store_true")
@@ -408,7 +409,8 @@ def main():
     N, T, L = CONFIGS[args.config]
     y, B, W0, lp0 = synth(N, T, L, rank=rank)
     dev = torch.device("cuda", local)
-    scan = ScanConfig(chunk=args.chunk or None, warmup=args.warm_steps, chunk_bwd=args.chunk_bwd or None)
+    scan = ScanConfig(chunk=args.chunk or None, warmup=args.warm_steps, chunk_bwd=args.chunk_bwd or None,
+                      two_waves=args.two_waves)
     if args.scan_tol > 0:
         scan.tol = args.scan_tol
     sp = SpikeData(y)

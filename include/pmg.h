@@ -258,7 +258,13 @@ int pmg_backward_smoother(const float* delta, const float* phi, const float* alp
 /* f32.  They are the exact-product operands of pmg_suffstats_bf16x3 (the split  */
 /* runs once per value here instead of once per neuron tile in the statistics).  */
 #define PMG_PHASE_P_BF16X3 32
-#define PMG_PHASE_FLAG_BITS (7 | PMG_PHASE_ADAPTIVE_WARMUP | PMG_PHASE_NO_ALPHA | PMG_PHASE_P_BF16X3 | (0xfff << 16))
+/* Either direction, phase-1 calls: PMG_PHASE_TWO_WAVES runs each chain of the main  */
+/* pass on two waves (half the latents per lane, the band halo and the per-step sums */
+/* exchanged through LDS) where that form is compiled (Lpad 512 / 1024, i.e. L in    */
+/* (256, 1024]); elsewhere it is ignored.  Same outputs up to f32 summation order.   */
+#define PMG_PHASE_TWO_WAVES 64
+#define PMG_PHASE_FLAG_BITS \
+  (7 | PMG_PHASE_ADAPTIVE_WARMUP | PMG_PHASE_NO_ALPHA | PMG_PHASE_P_BF16X3 | PMG_PHASE_TWO_WAVES | (0xfff << 16))
 int pmg_forward_filter_phase(const float* delta, const float* phi, const double* m, int64_t T,
                              const pmg_transition* tr, double likelihood_scale, int32_t chunk,
                              int32_t warmup, double tol, float* alpha, double* logc, double* logz,

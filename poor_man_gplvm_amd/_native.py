@@ -35,6 +35,8 @@ PHASE_ADAPTIVE_WARMUP = 8
 PHASE_NO_ALPHA = 16
 # backward, both phase calls: P written as three bf16 planes [3][T][ldd] (PMG_PHASE_P_BF16X3)
 PHASE_P_BF16X3 = 32
+# phase-1 calls: each main-pass chain on two waves where compiled (PMG_PHASE_TWO_WAVES)
+PHASE_TWO_WAVES = 64
 ABI_VERSION = 2
 
 

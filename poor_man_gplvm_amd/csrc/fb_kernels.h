@@ -228,10 +228,11 @@ __device__ __forceinline__ void em_load(const FBParams& p, int64_t t, int j0, Em
   r.ph = (b < p.nblk) ? p.phi[t * p.ldphi + b] : 0.f;
 }
 
-template <int J>
+// FULL: every lane's latents are < L (L == Lpad), so no lane-validity select
+template <int J, bool FULL = false>
 __device__ __forceinline__ void em_exp(const FBParams& p, int j0, const EmRaw<J>& r, float e[J]) {
 #pragma unroll
-  for (int j = 0; j < J; ++j) e[j] = (j0 + j < p.L) ? exp_acc(fmaf(p.s, r.d[j], r.ph)) : 0.f;
+  for (int j = 0; j < J; ++j) e[j] = (FULL || j0 + j < p.L) ? exp_acc(fmaf(p.s, r.d[j], r.ph)) : 0.f;
 }
 
 // One wave holds the whole line (lane l owns latents lJ .. lJ+J-1): the halo comes
@@ -248,9 +249,103 @@ __device__ __forceinline__ float wave_shl1(float v) {  // lane i <- lane i+1 (la
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, true));
 }
 
-// out[j] = sum_{k=-WP..WP} g[|k|] * in[j+k]  over the whole latent line (zero halo)
-template <int J, int WP>
-__device__ __forceinline__ void band_conv(const FBParams& p, const float in[J], float out[J]) {
+// the same shifts with the incoming lane (lane 0 / lane 63) taking `in0` instead of 0:
+// DPP with bound_ctrl off leaves a lane whose source is out of range at its old value
+__device__ __forceinline__ float wave_shr1_in(float v, float in0) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(in0), __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float wave_shl1_in(float v, float in63) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(in63), __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
+
+// ---------------------------------------------------------------------------
+// Several waves per chain (NW > 1): wave w of the chain's workgroup owns latents
+// (64 w + lane) J .. + J - 1, so the (2, Lpad) state layout is the one-wave layout at
+// J' = NW J.  Per exchange each wave writes its line (the band convolution's input) and
+// its wave-reduced partial sums to LDS, one s_barrier, then reads its neighbours' edge
+// latents (the halo of the DPP shifts) and every wave's partials, summed in wave order so
+// all waves hold bit-identical totals.  Two LDS slots alternate between exchanges: a
+// wave writes slot s again only after the barrier of the next exchange, which its
+// neighbours pass only once their reads of slot s have returned (the LDS-only release
+// before each barrier waits lgkmcnt(0), nothing else: the row rings stay in flight).
+// Line slots 0 and NW + 1 of each LDS slot stay zero: the halo past the line's ends.
+// ---------------------------------------------------------------------------
+template <int NW, int J>
+struct ChainX {
+  static constexpr int kLine = 64 * J;
+  static constexpr int kSlot = (NW + 2) * kLine + NW * 4;   // lines + [NW][4] partial sums
+  int w;      // this wave's index in the chain (wave-uniform)
+  int par;    // LDS slot of the next exchange
+  float* lds;
+
+  __device__ __forceinline__ void init() {
+    lds = nullptr;
+    w = 0;
+    par = 0;
+    if constexpr (NW > 1) {
+      __shared__ float buf[2 * kSlot];
+      lds = buf;
+      w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+      for (int s = 0; s < 2; ++s)
+        for (int i = threadIdx.x; i < kLine; i += 64 * NW) {
+          buf[s * kSlot + i] = 0.f;
+          buf[s * kSlot + (NW + 1) * kLine + i] = 0.f;
+        }
+      barrier();
+    }
+  }
+  __device__ __forceinline__ static void barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  }
+  // one exchange: `line` (this lane's J values, may be null) and NS wave-uniform partial
+  // sums in; the neighbours' edge values (NL lanes x J each side, lin: left neighbour's
+  // lanes 64-NL..63, rin: right neighbour's lanes 0..NL-1; zero past the line) and the
+  // chain's totals out
+  template <int NL, int NS>
+  __device__ __forceinline__ void exchange(const float* line, float* lin, float* rin, float* sums) {
+    static_assert(NW > 1 && NS <= 4 && NL <= 64, "chain exchange");
+    float* s = lds + par * kSlot;
+    const int lane = threadIdx.x & 63;
+    if (line) {
+      float* my = s + (w + 1) * kLine + lane * J;
+#pragma unroll
+      for (int j = 0; j < J; ++j) my[j] = line[j];
+    }
+    if (NS > 0 && lane == 0) {
+#pragma unroll
+      for (int k = 0; k < NS; ++k) s[(NW + 2) * kLine + w * 4 + k] = sums[k];
+    }
+    barrier();
+    if (line) {
+      const float* ln = s + w * kLine + kLine - NL * J;    // wave w-1 (or the zero slot)
+      const float* rn = s + (w + 2) * kLine;               // wave w+1 (or the zero slot)
+#pragma unroll
+      for (int q = 0; q < NL * J; ++q) {
+        lin[q] = ln[q];
+        rin[q] = rn[q];
+      }
+    }
+    if constexpr (NS > 0) {
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        float t = 0.f;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) t += s[(NW + 2) * kLine + v * 4 + k];
+        sums[k] = t;
+      }
+    }
+    par ^= 1;
+  }
+};
+
+// out[j] = sum_{k=-WP..WP} g[|k|] * in[j+k]  over the whole latent line (zero halo).
+// NW > 1: the lanes at the wave's ends take their neighbours' values from lin / rin
+// (ChainX::exchange), so the line spans the chain's NW waves.
+template <int J, int WP, int NW = 1>
+__device__ __forceinline__ void band_conv(const FBParams& p, const float in[J], float out[J],
+                                          const float* lin = nullptr, const float* rin = nullptr) {
   constexpr int NL = (WP + J - 1) / J;  // neighbour lanes on each side
   constexpr int C = NL * J;             // window index of this lane's first latent
   float win[J + 2 * C];
@@ -261,16 +356,18 @@ __device__ __forceinline__ void band_conv(const FBParams& p, const float in[J], 
   for (int k = 1; k <= NL; ++k)
 #pragma unroll
     for (int i = 0; i < J; ++i) {
-      if (k * J - i <= WP) win[C - k * J + i] = wave_shr1(win[C - (k - 1) * J + i]);
-      else win[C - k * J + i] = 0.f;
+      if (k * J - i > WP) win[C - k * J + i] = 0.f;
+      else if constexpr (NW > 1) win[C - k * J + i] = wave_shr1_in(win[C - (k - 1) * J + i], lin[(NL - k) * J + i]);
+      else win[C - k * J + i] = wave_shr1(win[C - (k - 1) * J + i]);
     }
   // right: block k (lane l+k) local i at window C + kJ + i; needed iff kJ + i - (J-1) <= WP
 #pragma unroll
   for (int k = 1; k <= NL; ++k)
 #pragma unroll
     for (int i = 0; i < J; ++i) {
-      if (k * J + i - (J - 1) <= WP) win[C + k * J + i] = wave_shl1(win[C + (k - 1) * J + i]);
-      else win[C + k * J + i] = 0.f;
+      if (k * J + i - (J - 1) > WP) win[C + k * J + i] = 0.f;
+      else if constexpr (NW > 1) win[C + k * J + i] = wave_shl1_in(win[C + (k - 1) * J + i], rin[(k - 1) * J + i]);
+      else win[C + k * J + i] = wave_shl1(win[C + (k - 1) * J + i]);
     }
   if constexpr ((J & 1) == 0) {
     // output pairs (j, j+1) on packed math (v_pk_fma_f32 / v_pk_add_f32): per lane the
@@ -317,9 +414,18 @@ __device__ __forceinline__ void band_conv(const FBParams& p, const float in[J], 
   }
 }
 
-// wave-wide reductions of one chain (one wave carries it)
-__device__ __forceinline__ void chain_sum2(float& a, float& b) { wave_sum2(a, b); }
-__device__ __forceinline__ float chain_sum(float a) { return wave_sum(a); }
+// reductions over one chain: the wave's sum, then (NW > 1) the waves' partials in wave
+// order through the chain's LDS exchange
+template <int NW, int J>
+__device__ __forceinline__ void chain_sum2(ChainX<NW, J>& x, float& a, float& b) {
+  wave_sum2(a, b);
+  if constexpr (NW > 1) {
+    float s[2] = {a, b};
+    x.template exchange<0, 2>(nullptr, nullptr, nullptr, s);
+    a = s[0];
+    b = s[1];
+  }
+}
 
 // ---------------------------------------------------------------------------
 // Hilbert projective distance between two non-negative (2, Lpad) states.
@@ -455,13 +561,16 @@ __device__ __forceinline__ float hilbert_reg(const float x0[J], const float x1[J
 // its scalar coefficients, so no per-element normalisation or d = 1 row is formed on
 // the recursion (only where alpha is stored); the backward rebuilds alpha's d = 1 row
 // from (e, jmp, iS) exactly as written here.
-template <int J, int WP>
+template <int J, int WP, int NW = 1>
 struct Fwd {
+  static constexpr int NL = (WP + J - 1) / J;
   float q0[J], ep[J];
   float P0, P1;  // normalised sums of the d = 0 / d = 1 parts (wave-uniform)
   float jmp, iS; // the last step's jump mass and 1/S
+  ChainX<NW, J> x;
 
   __device__ void init_uniform(const FBParams& p, int j0) {
+    x.init();
     const float u = 0.5f * p.invL;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
@@ -485,7 +594,7 @@ struct Fwd {
       a += q0[j];
       b += ep[j];
     }
-    chain_sum2(a, b);
+    chain_sum2(x, a, b);
     const float inv = rcp_nr(a + b);
     jmp = 1.f;
     iS = inv;
@@ -508,7 +617,13 @@ struct Fwd {
     for (int j = 0; j < J; ++j) a0[j] = fmaf(q0[j], c0, ep[j] * c1) * invz[j];
     const float jump = fmaf(p.A01, P0, p.A11 * P1) * p.invL;
     float pr0[J];
-    band_conv<J, WP>(p, a0, pr0);
+    if constexpr (NW > 1) {
+      float lin[NL * J], rin[NL * J];
+      x.template exchange<NL, 0>(a0, lin, rin, nullptr);
+      band_conv<J, WP, NW>(p, a0, pr0, lin, rin);
+    } else {
+      band_conv<J, WP>(p, a0, pr0);
+    }
     float U0 = 0.f, E = 0.f;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
@@ -517,7 +632,7 @@ struct Fwd {
       U0 += q0[j];
       E += e[j];
     }
-    chain_sum2(U0, E);
+    chain_sum2(x, U0, E);
     const float U1 = jump * E;
     const float S = U0 + U1;
     const float inv = rcp_nr(S);
@@ -544,7 +659,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base, uint
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
-template <int J, bool VEC>
+template <int J, int VEC>
 __device__ __forceinline__ void bload_row(const float* row, int L, int j0, float v[J]) {
   const __amdgpu_buffer_rsrc_t rs = rsrc_of(row, (uint32_t)L * 4u);
   if constexpr (VEC) {
@@ -563,7 +678,7 @@ __device__ __forceinline__ void bload_row(const float* row, int L, int j0, float
 }
 
 // bytes: the row's extent (lanes past it drop their stores; 0 = the row is not written)
-template <int J, bool VEC, int AUX = 0>
+template <int J, int VEC, int AUX = 0>
 __device__ __forceinline__ void bstore_row_n(float* row, uint32_t bytes, int j0, const float v[J]) {
   const __amdgpu_buffer_rsrc_t rs = rsrc_of(row, bytes);
   if constexpr (VEC) {
@@ -582,14 +697,14 @@ __device__ __forceinline__ void bstore_row_n(float* row, uint32_t bytes, int j0,
   }
 }
 
-template <int J, bool VEC>
+template <int J, int VEC>
 __device__ __forceinline__ void bstore_row(float* row, int L, int j0, const float v[J]) {
   bstore_row_n<J, VEC>(row, (uint32_t)L * 4u, j0, v);
 }
 
 // row t of P as three bf16 planes (PMG_PHASE_P_BF16X3): the exact split of each value
 // (split3_pair), the lane's J values as J / 2 dwords per plane
-template <int J, bool VEC>
+template <int J, int VEC>
 __device__ __forceinline__ void bstore_planes(const FBParams& p, int64_t t, int j0, const float v[J]) {
   const uint32_t bytes = (uint32_t)p.L * 2u;
   if constexpr (VEC) {   // J % 4 == 0, L % 4 == 0: 8-byte aligned runs
@@ -627,7 +742,7 @@ __device__ __forceinline__ void bstore_planes(const FBParams& p, int64_t t, int 
 // two f32 per step (x at 2t, y at 2t + 1) written by lane 0 only
 __device__ __forceinline__ void bstore_pair_lane0(float* base, int64_t t, float x, float y) {
   const __amdgpu_buffer_rsrc_t rs = rsrc_of(base + 2 * t, 8u);
-  const int off = (threadIdx.x & 63) == 0 ? 0 : 64;
+  const int off = threadIdx.x == 0 ? 0 : 64;   // one store per chain (every wave of it holds the value)
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), rs, off, 0, 0);
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y), rs, off + 4, 0, 0);
 }
@@ -635,13 +750,20 @@ __device__ __forceinline__ void bstore_pair_lane0(float* base, int64_t t, float 
 // one f64 per step written by lane 0 only (the other lanes' offsets are out of range)
 __device__ __forceinline__ void bstore_f64_lane0(double* base, int64_t t, double v) {
   const __amdgpu_buffer_rsrc_t rs = rsrc_of(base + t, 8u);
-  const int off = (threadIdx.x & 63) == 0 ? 0 : 64;
+  const int off = threadIdx.x == 0 ? 0 : 64;
   const unsigned long long u = (unsigned long long)__double_as_longlong(v);
   __builtin_amdgcn_raw_buffer_store_b32((unsigned)u, rs, off, 0, 0);
   __builtin_amdgcn_raw_buffer_store_b32((unsigned)(u >> 32), rs, off + 4, 0, 0);
 }
 
-template <int J, bool VEC>
+// Ordering point without instructions: `v` counts as rewritten once `dep` (a value of the
+// step before) exists, so the emission arithmetic of a ring slot is not hoisted above the
+// previous step.  Without it hipcc evaluates the exp arguments of every slot of the ring
+// at the loop head, which makes it wait for all of them -- and for every store issued
+// since (s_waitcnt vmcnt(0) once per ring cycle).
+__device__ __forceinline__ void order_after(float& v, float dep) { asm volatile("" : "+v"(v) : "v"(dep)); }
+
+template <int J, int VEC>
 __device__ __forceinline__ void bem_load(const FBParams& p, int64_t t, int j0, EmRaw<J>& r) {
   bload_row<J, VEC>(p.delta + t * p.ldd, p.L, j0, r.d);
   const __amdgpu_buffer_rsrc_t rs = rsrc_of(p.phi + t * p.ldphi, (uint32_t)p.nblk * 4u);
@@ -651,8 +773,8 @@ __device__ __forceinline__ void bem_load(const FBParams& p, int64_t t, int j0, E
 // forward steps t in [t_a, t_b): OUT writes alpha / logc and returns sum logc; A1: also
 // alpha's d = 1 rows (p.a1_bytes of them; the EM passes omit them).  MLDS: the row
 // references m_t come from sm (LDS, indexed t - t_a), else from a register ring
-template <int J, int WP, int PF, bool VEC, bool OUT, bool A1, bool MLDS>
-__device__ __forceinline__ double fwd_stream_piece(const FBParams& p, Fwd<J, WP>& st, int j0, const float invz[J],
+template <int J, int WP, int PF, int VEC, bool OUT, bool A1, bool MLDS, int NW>
+__device__ __forceinline__ double fwd_stream_piece(const FBParams& p, Fwd<J, WP, NW>& st, int j0, const float invz[J],
                                                    int64_t t_a, int64_t t_b, const double* sm) {
   double logz = 0.0;
   if (t_a >= t_b) return 0.0;
@@ -667,7 +789,8 @@ __device__ __forceinline__ double fwd_stream_piece(const FBParams& p, Fwd<J, WP>
   }
   auto body = [&](int q, int64_t t, bool refill) {
     float e[J];
-    em_exp<J>(p, j0, ring[q], e);
+    order_after(ring[q].ph, st.q0[0]);
+    em_exp<J, VEC == 2>(p, j0, ring[q], e);
     double mt = 0.0;
     if constexpr (OUT && MLDS) mt = sm[t - t_a];
     if constexpr (OUT && !MLDS) mt = mr[q];
@@ -716,57 +839,62 @@ __device__ __forceinline__ double fwd_stream_piece(const FBParams& p, Fwd<J, WP>
 #define PMG_RELAX_MLDS true
 #endif
 constexpr int kMPiece = 512;
-template <int J, int WP, int PF, bool VEC, bool OUT, bool A1 = true, bool MLDS = false>
-__device__ __forceinline__ double fwd_stream(const FBParams& p, Fwd<J, WP>& st, int j0, const float invz[J],
+template <int J, int WP, int PF, int VEC, bool OUT, bool A1 = true, bool MLDS = false, int NW>
+__device__ __forceinline__ double fwd_stream(const FBParams& p, Fwd<J, WP, NW>& st, int j0, const float invz[J],
                                              int64_t t_a, int64_t t_b) {
   if constexpr (OUT && MLDS) {
-    __shared__ double sm[kMPiece];   // one wave per workgroup: no barrier, only the waits
+    // one copy per wave (each wave of a chain fills its own): no barrier, only the waits
+    __shared__ double sm_all[NW * kMPiece];
+    double* sm = sm_all + (threadIdx.x >> 6) * kMPiece;
     const int lane = threadIdx.x & 63;
     double logz = 0.0;
     for (int64_t ta = t_a; ta < t_b; ta += kMPiece) {
       const int64_t tz = ta + kMPiece < t_b ? ta + kMPiece : t_b;
       for (int64_t t = ta + lane; t < tz; t += 64) sm[t - ta] = p.m[t * p.ldm];
       __builtin_amdgcn_s_waitcnt(0);   // vmcnt(0) lgkmcnt(0): the piece's m is in LDS
-      logz += fwd_stream_piece<J, WP, PF, VEC, OUT, A1, true>(p, st, j0, invz, ta, tz, sm);
+      logz += fwd_stream_piece<J, WP, PF, VEC, OUT, A1, true, NW>(p, st, j0, invz, ta, tz, sm);
     }
     return logz;
   }
-  return fwd_stream_piece<J, WP, PF, VEC, OUT, A1, false>(p, st, j0, invz, t_a, t_b, nullptr);
+  return fwd_stream_piece<J, WP, PF, VEC, OUT, A1, false, NW>(p, st, j0, invz, t_a, t_b, nullptr);
 }
 
 #define PMG_FB_LANE_SETUP                                               \
   const int lane = threadIdx.x & 63;                                    \
-  const int j0 = lane * J;                                              \
+  const int j0 = (int)threadIdx.x * J;  /* wave w of a chain: lanes 64 w .. */ \
   float invz[J];                                                        \
   _Pragma("unroll") for (int j = 0; j < J; ++j) invz[j] = (j0 + j < p.L) ? p.invz[j0 + j] : 0.f;
 
 // speculative pass: chunk c starts `B` steps early from a uniform guess
-template <int J, int WP, bool VEC, bool A1>
+template <int J, int WP, int VEC, bool A1, int NW = 1>
 __device__ __forceinline__ void forward_chunk(const FBParams& p, int c, int j0, const float invz[J]) {
   const size_t SZ = (size_t)2 * p.Lpad;
   const int64_t t_c = (int64_t)c * p.C;
   const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
-  Fwd<J, WP> st;
+  Fwd<J, WP, NW> st;
   int64_t t0 = (c == 0) ? 0 : t_c - main_warmup(p);
   if (t0 < 0) t0 = 0;
   st.init_uniform(p, j0);
   fwd_stream<J, WP, kPfFwd, VEC, false>(p, st, j0, invz, t0, t_c);
   if (c > 0) st.save_state(p, p.s_in + (size_t)c * SZ, j0);  // the start k_verify checks
-  const double lz = fwd_stream<J, WP, kPfFwd, VEC, true, A1>(p, st, j0, invz, t_c, t_e);
+  // the row references m_t from LDS (filled once per chunk), as in the relaxation: a
+  // register ring of them makes hipcc rotate it on the loop's back edge behind a vmcnt(0)
+  const double lz = fwd_stream<J, WP, kPfFwd, VEC, true, A1, true>(p, st, j0, invz, t_c, t_e);
   st.save_state(p, p.s_out + (size_t)c * SZ, j0);
-  if ((threadIdx.x & 63) == 0) p.chunk_logz[c] = lz;
+  if (threadIdx.x == 0) p.chunk_logz[c] = lz;
 }
 
 // the main pass clears the per-call words (the relaxation kernels run after it)
 __device__ __forceinline__ void main_pass_reset(const FBParams& p) {
-  if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     p.ctl[kCtlRepairs] = 0;
     p.ctl[kCtlRounds] = 0;
   }
 }
 
-template <int J, int WP>
-__global__ void __launch_bounds__(64) k_forward(FBParams p_arg) {
+// NW waves per chain (workgroup of 64 NW threads): J latents per lane, Lpad = 64 NW J
+template <int J, int WP, int NW = 1>
+__global__ void __launch_bounds__(64 * NW) k_forward(FBParams p_arg) {
   const FBParams p = batch_view(p_arg);
   const int c = blockIdx.x;
   if (c >= p.M) return;
@@ -776,13 +904,15 @@ __global__ void __launch_bounds__(64) k_forward(FBParams p_arg) {
   const bool a1 = p.a1_bytes != 0;   // decode passes store alpha's d = 1 rows, EM passes do not
   if constexpr (J % 4 == 0) {
     if ((p.L & 3) == 0) {
-      if (a1) forward_chunk<J, WP, true, true>(p, c, j0, invz);
-      else forward_chunk<J, WP, true, false>(p, c, j0, invz);
+      // VEC 2: L == Lpad, no lane-validity selects in the step loops (the EM shapes)
+      if (a1) forward_chunk<J, WP, 1, true, NW>(p, c, j0, invz);
+      else if (p.L == p.Lpad) forward_chunk<J, WP, 2, false, NW>(p, c, j0, invz);
+      else forward_chunk<J, WP, 1, false, NW>(p, c, j0, invz);
       return;
     }
   }
-  if (a1) forward_chunk<J, WP, false, true>(p, c, j0, invz);
-  else forward_chunk<J, WP, false, false>(p, c, j0, invz);
+  if (a1) forward_chunk<J, WP, false, true, NW>(p, c, j0, invz);
+  else forward_chunk<J, WP, false, false, NW>(p, c, j0, invz);
 }
 
 // ---------------------------------------------------------------------------
@@ -891,7 +1021,7 @@ __device__ __forceinline__ double wave_sum_fixed(const double* x, int n) {
 // flagged (flg, round 0 only), the chunks up to the next flagged boundary are
 // consistent: stop (*stop = c).  Returns true iff the segment's end state (chunk b-1)
 // moved.
-template <int J, int WP, bool VEC, bool A1 = true>
+template <int J, int WP, int VEC, bool A1 = true>
 __device__ __forceinline__ bool fwd_segment(const FBParams& p, Fwd<J, WP>& st, int c0, int b, int j0, const float invz[J],
                             const int* flg, int& nrep, int* stop = nullptr) {
   const size_t SZ = (size_t)2 * p.Lpad;
@@ -916,7 +1046,7 @@ __device__ __forceinline__ bool fwd_segment(const FBParams& p, Fwd<J, WP>& st, i
   return true;
 }
 
-template <int J, int WP, bool VEC, bool A1 = true>
+template <int J, int WP, int VEC, bool A1 = true>
 __device__ __forceinline__ void forward_relax(const FBParams& p, int j0, const float invz[J]) {
   const size_t SZ = (size_t)2 * p.Lpad;
   const int s = blockIdx.x;
@@ -976,8 +1106,12 @@ __global__ void __launch_bounds__(64) k_forward_relax(FBParams p_arg) {
   if constexpr (J % 4 == 0) {
     if ((p.L & 3) == 0) {
       // the EM passes store no d = 1 rows of alpha (a1_bytes = 0): no a1 row formed either
-      if (p.a1_bytes == 0) forward_relax<J, WP, true, false>(p, j0, invz);
-      else forward_relax<J, WP, true>(p, j0, invz);
+      if (p.a1_bytes == 0) {
+        if (p.L == p.Lpad) forward_relax<J, WP, 2, false>(p, j0, invz);
+        else forward_relax<J, WP, 1, false>(p, j0, invz);
+      } else {
+        forward_relax<J, WP, 1>(p, j0, invz);
+      }
       return;
     }
   }
@@ -990,11 +1124,15 @@ __global__ void __launch_bounds__(64) k_forward_relax(FBParams p_arg) {
 // on the warm-up and on the output path, so two chunks that have converged to
 // the same beta produce bit-identical continuations (as the forward does).
 // ---------------------------------------------------------------------------
-template <int J, int WP>
+template <int J, int WP, int NW = 1>
 struct Bwd {
+  static constexpr int NL = (WP + J - 1) / J;
   float b0[J], b1[J];  // beta at the current time
+  ChainX<NW, J> x;
+  float hl[NW > 1 ? NL * J : 1], hr[NW > 1 ? NL * J : 1];  // this step's halo of e * beta0 (NW > 1)
 
   __device__ void init_ones(const FBParams& p, int j0) {
+    x.init();
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       b0[j] = (j0 + j < p.L) ? 1.f : 0.f;
@@ -1015,10 +1153,35 @@ struct Bwd {
       dst[p.Lpad + j0 + j] = b1[j];
     }
   }
+  // the step's chain-wide sums (V0, V1 and, G != null, the output pass's G) and, NW > 1,
+  // the halo of eb0 for step_back's band convolution: one LDS exchange per step
+  __device__ __forceinline__ void sums(const float eb0[J], float& V0, float& V1, float* G) {
+    if (G) {
+      wave_sum2(V0, V1);
+      *G = wave_sum(*G);
+    } else {
+      wave_sum2(V0, V1);
+    }
+    if constexpr (NW > 1) {
+      if (G) {
+        float t[3] = {V0, V1, *G};
+        x.template exchange<NL, 3>(eb0, hl, hr, t);
+        V0 = t[0];
+        V1 = t[1];
+        *G = t[2];
+      } else {
+        float t[2] = {V0, V1};
+        x.template exchange<NL, 2>(eb0, hl, hr, t);
+        V0 = t[0];
+        V1 = t[1];
+      }
+    }
+  }
   // beta <- Trans(v), v = e*beta / (V0+V1), given eb0 = e*b0 and eb1 = e*b1 (V0, V1
-  // their sums): the scale 1/(V0+V1) rides on the scalar coefficients.  KEEP_V: also
-  // return v (the joint partner rho of the decode / relaxation passes).  Lanes past L
-  // get beta != 0 but every consumer weights beta by e or alpha, which are 0 there.
+  // their chain sums, from sums()): the scale 1/(V0+V1) rides on the scalar coefficients.
+  // KEEP_V: also return v (the joint partner rho of the decode / relaxation passes).
+  // Lanes past L get beta != 0 but every consumer weights beta by e or alpha, which are
+  // 0 there.
   template <bool KEEP_V>
   __device__ void step_back(const FBParams& p, const float invz[J], const float eb0[J], const float eb1[J],
                             float V0, float V1, float v0[J], float v1[J]) {
@@ -1031,7 +1194,8 @@ struct Bwd {
       }
     }
     float w0[J];
-    band_conv<J, WP>(p, eb0, w0);
+    if constexpr (NW > 1) band_conv<J, WP, NW>(p, eb0, w0, hl, hr);
+    else band_conv<J, WP>(p, eb0, w0);
     const float w1 = V1 * sc * p.invL;
     const float a00 = p.A00 * sc, a10 = p.A10 * sc, c01 = p.A01 * w1, c11 = p.A11 * w1;
 #pragma unroll
@@ -1043,9 +1207,9 @@ struct Bwd {
   }
 };
 
-// eb = e * beta per dynamics state and their wave sums
-template <int J, int WP>
-__device__ __forceinline__ void e_beta(const Bwd<J, WP>& st, const float e[J], float eb0[J], float eb1[J], float& V0,
+// eb = e * beta per dynamics state and their (lane-local) sums
+template <int J, int WP, int NW>
+__device__ __forceinline__ void e_beta(const Bwd<J, WP, NW>& st, const float e[J], float eb0[J], float eb1[J], float& V0,
                                        float& V1) {
   V0 = 0.f;
   V1 = 0.f;
@@ -1059,21 +1223,21 @@ __device__ __forceinline__ void e_beta(const Bwd<J, WP>& st, const float e[J], f
 }
 
 // one plain backward step at time t (beta_t -> beta_{t-1}); v kept in (v0, v1)
-template <int J, int WP>
-__device__ __forceinline__ void bwd_plain(const FBParams& p, Bwd<J, WP>& st, int j0, const float invz[J],
+template <int J, int WP, int NW>
+__device__ __forceinline__ void bwd_plain(const FBParams& p, Bwd<J, WP, NW>& st, int j0, const float invz[J],
                                           int64_t t, float v0[J], float v1[J]) {
   EmRaw<J> r;
   em_load<J>(p, t, j0, r);
   float e[J], eb0[J], eb1[J], V0, V1;
   em_exp<J>(p, j0, r, e);
-  e_beta<J, WP>(st, e, eb0, eb1, V0, V1);
-  chain_sum2(V0, V1);
+  e_beta(st, e, eb0, eb1, V0, V1);
+  st.sums(eb0, V0, V1, nullptr);
   st.template step_back<true>(p, invz, eb0, eb1, V0, V1, v0, v1);
 }
 
 // plain steps t = t_hi .. t_lo (descending), emission rows PF steps ahead
-template <int J, int WP, int PF, bool VEC>
-__device__ __forceinline__ void bwd_stream_warm(const FBParams& p, Bwd<J, WP>& st, int j0, const float invz[J],
+template <int J, int WP, int PF, int VEC, int NW>
+__device__ __forceinline__ void bwd_stream_warm(const FBParams& p, Bwd<J, WP, NW>& st, int j0, const float invz[J],
                                                 int64_t t_hi, int64_t t_lo) {
   if (t_hi < t_lo) return;
   EmRaw<J> ring[PF];
@@ -1081,11 +1245,12 @@ __device__ __forceinline__ void bwd_stream_warm(const FBParams& p, Bwd<J, WP>& s
   for (int q = 0; q < PF; ++q) bem_load<J, VEC>(p, t_hi - q > t_lo ? t_hi - q : t_lo, j0, ring[q]);
   auto body = [&](int q, int64_t t, bool refill) {
     float e[J];
-    em_exp<J>(p, j0, ring[q], e);
+    order_after(ring[q].ph, st.b0[0]);
+    em_exp<J, VEC == 2>(p, j0, ring[q], e);
     if (refill) bem_load<J, VEC>(p, t - PF > t_lo ? t - PF : t_lo, j0, ring[q]);
     float eb0[J], eb1[J], V0, V1;
-    e_beta<J, WP>(st, e, eb0, eb1, V0, V1);
-    chain_sum2(V0, V1);
+    e_beta(st, e, eb0, eb1, V0, V1);
+    st.sums(eb0, V0, V1, nullptr);
     st.template step_back<false>(p, invz, eb0, eb1, V0, V1, nullptr, nullptr);
   };
   int64_t tb = t_hi;
@@ -1105,7 +1270,7 @@ struct BRow {
   float js, ji;  // the forward's (jump, 1/S) of this step
 };
 
-template <int J, bool VEC>
+template <int J, int VEC>
 __device__ __forceinline__ void brow_load(const FBParams& p, int64_t t, int j0, BRow<J>& r) {
   bem_load<J, VEC>(p, t, j0, r.em);
   bload_row<J, VEC>(p.alpha_in + t * 2 * (int64_t)p.L, p.L, j0, r.a0);
@@ -1125,12 +1290,12 @@ __device__ __forceinline__ void alpha1_row(float js, float ji, const float e[J],
 }
 
 // the boundary weights of chunk c: alpha at its first step t_c, (2, Lpad) layout
-template <int J, bool VEC>
+template <int J, int VEC>
 __device__ __forceinline__ void store_weights(const FBParams& p, int64_t t_c, int j0, float* dst) {
   BRow<J> r;
   brow_load<J, VEC>(p, t_c, j0, r);
   float e[J], a1[J];
-  em_exp<J>(p, j0, r.em, e);
+  em_exp<J, VEC == 2>(p, j0, r.em, e);
   alpha1_row<J>(r.js, r.ji, e, a1);
 #pragma unroll
   for (int j = 0; j < J; ++j) {
@@ -1142,8 +1307,8 @@ __device__ __forceinline__ void store_weights(const FBParams& p, int64_t t_c, in
 // output steps t = t_e-1 .. t_c; on entry st = beta_{t_e-1} and (vp0, vp1) the v that
 // produced it (has_prev false at the sequence end), on exit beta_{t_c}.
 // MODE 0 (EM): P only.  MODE 1: P / gamma / rho as given (decode, relaxation).
-template <int J, int WP, int PF, bool VEC, int MODE>
-__device__ __forceinline__ void bwd_stream_out(const FBParams& p, Bwd<J, WP>& st, int j0, const float invz[J],
+template <int J, int WP, int PF, int VEC, int MODE, int NW>
+__device__ __forceinline__ void bwd_stream_out(const FBParams& p, Bwd<J, WP, NW>& st, int j0, const float invz[J],
                                                int64_t t_c, int64_t t_e, float vp0[J], float vp1[J],
                                                bool has_prev) {
   if (t_e - 1 < t_c) return;
@@ -1153,12 +1318,13 @@ __device__ __forceinline__ void bwd_stream_out(const FBParams& p, Bwd<J, WP>& st
   for (int q = 0; q < PF; ++q) brow_load<J, VEC>(p, t_e - 1 - q > t_c ? t_e - 1 - q : t_c, j0, ring[q]);
   auto body = [&](int q, int64_t t, bool refill) {
     float a0[J], a1[J], e[J], eb0[J], eb1[J], pp[J], V0, V1;
-    em_exp<J>(p, j0, ring[q].em, e);
+    order_after(ring[q].em.ph, st.b0[0]);
+    em_exp<J, VEC == 2>(p, j0, ring[q].em, e);
 #pragma unroll
     for (int j = 0; j < J; ++j) a0[j] = ring[q].a0[j];
     const float js = ring[q].js, ji = ring[q].ji;
     if (refill) brow_load<J, VEC>(p, t - PF > t_c ? t - PF : t_c, j0, ring[q]);
-    e_beta<J, WP>(st, e, eb0, eb1, V0, V1);
+    e_beta(st, e, eb0, eb1, V0, V1);
     float G = 0.f;
     if constexpr (MODE == 0) {
       // gamma_t summed over d, unnormalised: alpha0 beta0 + (js ji) e beta1
@@ -1177,8 +1343,7 @@ __device__ __forceinline__ void bwd_stream_out(const FBParams& p, Bwd<J, WP>& st
         G += a0[j] + a1[j];
       }
     }
-    chain_sum2(V0, V1);
-    G = chain_sum(G);
+    st.sums(eb0, V0, V1, &G);
     const float iG = rcp_nr(G);
     if constexpr (MODE == 0) {
 #pragma unroll
@@ -1225,12 +1390,12 @@ __device__ __forceinline__ void bwd_stream_out(const FBParams& p, Bwd<J, WP>& st
 }
 
 // speculative pass: beta guess (ones) `B` steps after the chunk, warmed up backwards
-template <int J, int WP, bool VEC, int MODE>
+template <int J, int WP, int VEC, int MODE, int NW = 1>
 __device__ __forceinline__ void backward_chunk(const FBParams& p, int c, int j0, const float invz[J]) {
   const size_t SZ = (size_t)2 * p.Lpad;
   const int64_t t_c = (int64_t)c * p.C;
   const int64_t t_e = t_c + p.C < p.T ? t_c + p.C : p.T;
-  Bwd<J, WP> st;
+  Bwd<J, WP, NW> st;
   float vp0[J], vp1[J];
 #pragma unroll
   for (int j = 0; j < J; ++j) vp0[j] = vp1[j] = 0.f;
@@ -1252,15 +1417,18 @@ __device__ __forceinline__ void backward_chunk(const FBParams& p, int c, int j0,
 #define PMG_BWD_DISPATCH(MODE)                                          \
   if constexpr (J % 4 == 0) {                                           \
     if ((p.L & 3) == 0) {                                               \
-      backward_chunk<J, WP, true, MODE>(p, c, j0, invz);                \
+      if (MODE == 0 && p.L == p.Lpad)                                   \
+        backward_chunk<J, WP, 2, MODE, NW>(p, c, j0, invz);             \
+      else                                                              \
+        backward_chunk<J, WP, 1, MODE, NW>(p, c, j0, invz);             \
       return;                                                           \
     }                                                                   \
   }                                                                     \
-  backward_chunk<J, WP, false, MODE>(p, c, j0, invz);
+  backward_chunk<J, WP, false, MODE, NW>(p, c, j0, invz);
 
-// speculative pass, EM outputs (P only)
-template <int J, int WP>
-__global__ void __launch_bounds__(64) k_backward(FBParams p_arg) {
+// speculative pass, EM outputs (P only); NW waves per chain as k_forward
+template <int J, int WP, int NW = 1>
+__global__ void __launch_bounds__(64 * NW) k_backward(FBParams p_arg) {
   const FBParams p = batch_view(p_arg);
   const int c = blockIdx.x;
   if (c >= p.M) return;
@@ -1271,8 +1439,8 @@ __global__ void __launch_bounds__(64) k_backward(FBParams p_arg) {
 }
 
 // speculative pass, decode outputs (P / gamma / rho as given)
-template <int J, int WP>
-__global__ void __launch_bounds__(64) k_backward_full(FBParams p_arg) {
+template <int J, int WP, int NW = 1>
+__global__ void __launch_bounds__(64 * NW) k_backward_full(FBParams p_arg) {
   const FBParams p = batch_view(p_arg);
   const int c = blockIdx.x;
   if (c >= p.M) return;
@@ -1291,7 +1459,7 @@ __global__ void __launch_bounds__(64) k_backward_full(FBParams p_arg) {
 // boundary metric of k_verify) and boundary c-1 is not flagged, stop.  Returns true
 // iff the segment's end state (b_first[a]) moved; otherwise *stop = the chunk it
 // settled at.
-template <int J, int WP, bool VEC, int MODE = 1>
+template <int J, int WP, int VEC, int MODE = 1>
 __device__ __forceinline__ bool bwd_segment(const FBParams& p, Bwd<J, WP>& st, int c0, int a, int j0, const float invz[J],
                             const int* flg, int& nrep, int* stop = nullptr) {
   const size_t SZ = (size_t)2 * p.Lpad;
@@ -1314,7 +1482,7 @@ __device__ __forceinline__ bool bwd_segment(const FBParams& p, Bwd<J, WP>& st, i
   return true;
 }
 
-template <int J, int WP, bool VEC, int MODE = 1>
+template <int J, int WP, int VEC, int MODE = 1>
 __device__ __forceinline__ void backward_relax(const FBParams& p, int j0, const float invz[J]) {
   const size_t SZ = (size_t)2 * p.Lpad;
   const int s = blockIdx.x;
@@ -1373,8 +1541,12 @@ __global__ void __launch_bounds__(64) k_backward_relax(FBParams p_arg) {
     if ((p.L & 3) == 0) {
       // EM passes (P only): the main pass's P arithmetic (MODE 0: P bit-identical to a
       // main pass from the same beta), no gamma / rho rows, no v kept
-      if (!p.gamma && !p.rho) backward_relax<J, WP, true, 0>(p, j0, invz);
-      else backward_relax<J, WP, true>(p, j0, invz);
+      if (!p.gamma && !p.rho) {
+        if (p.L == p.Lpad) backward_relax<J, WP, 2, 0>(p, j0, invz);
+        else backward_relax<J, WP, 1, 0>(p, j0, invz);
+      } else {
+        backward_relax<J, WP, 1>(p, j0, invz);
+      }
       return;
     }
   }
@@ -1383,10 +1555,13 @@ __global__ void __launch_bounds__(64) k_backward_relax(FBParams p_arg) {
 
 typedef void (*fb_kernel_t)(FBParams);
 
-// the kernels of one (J, WP) instance (fb_inst_j*.hip)
+// the kernels of one (J, WP) instance (fb_inst_j*.hip); forward2 / backward2: the main
+// passes with each chain on two waves of J / 2 latents per lane (same state layout,
+// Lpad = 64 J), compiled for J = 8 and 16 (null elsewhere)
 struct FBKernelSet {
   fb_kernel_t forward, forward_relax;
   fb_kernel_t backward, backward_full, backward_relax;
+  fb_kernel_t forward2, backward2;
 };
 
 template <int J, int WP>
@@ -1396,6 +1571,12 @@ inline void fb_fill(FBKernelSet* k) {
   k->backward = k_backward<J, WP>;
   k->backward_full = k_backward_full<J, WP>;
   k->backward_relax = k_backward_relax<J, WP>;
+  k->forward2 = nullptr;
+  k->backward2 = nullptr;
+  if constexpr (J == 8 || J == 16) {
+    k->forward2 = k_forward<J / 2, WP, 2>;
+    k->backward2 = k_backward<J / 2, WP, 2>;
+  }
 }
 
 // one (J, WP) instance fb_set_j<J>_w<WP>, defined in the fb_inst_j*_w*.hip unit that lists it

@@ -294,7 +294,8 @@ static int forward_impl(const float* delta, const float* phi, const double* m, i
   const bool have = fb_set(J, WP, &ks);
   PMG_REQUIRE(have && ks.forward && ks.forward_relax, "pmg_forward_filter: no kernel for J=%d WP=%d", J, WP);
   if (phase & 1) {
-    hipLaunchKernelGGL(ks.forward, dim3(p.M, R), dim3(64), 0, st, p);
+    const bool two = (phase & PMG_PHASE_TWO_WAVES) && ks.forward2;
+    hipLaunchKernelGGL(two ? ks.forward2 : ks.forward, dim3(p.M, R), dim3(two ? 128 : 64), 0, st, p);
     PMG_LAUNCH_CHECK();
   }
   if (phase & 2) {
@@ -374,7 +375,8 @@ static int backward_impl(const float* delta, const float* phi, const float* alph
   fb_kernel_t kb = !have ? nullptr : (rho || gamma || !P) ? ks.backward_full : ks.backward;
   PMG_REQUIRE(kb && ks.backward_relax, "pmg_backward_smoother: no kernel for J=%d WP=%d", J, WP);
   if (phase & 1) {
-    hipLaunchKernelGGL(kb, dim3(p.M, R), dim3(64), 0, st, p);
+    const bool two = (phase & PMG_PHASE_TWO_WAVES) && kb == ks.backward && ks.backward2;   // EM (P-only) passes
+    hipLaunchKernelGGL(two ? ks.backward2 : kb, dim3(p.M, R), dim3(two ? 128 : 64), 0, st, p);
     PMG_LAUNCH_CHECK();
   }
   if ((phase & 2) && p.M > 1) {

@@ -77,6 +77,8 @@ class ScanConfig:
                                   # batched restarts; PMG_PHASE_SEGMENTS).  The repaired states depend
                                   # on the segment grid, so a single fit with #CUs / R segments
                                   # reproduces restart r of an R-restart batch bit for bit
+    two_waves: bool = False       # PMG_PHASE_TWO_WAVES: the main passes run each chain on two waves
+                                  # (L in (256, 1024]; half the latents per lane, LDS halo exchange)
     decode_exact: bool = True     # decode_latent / _decode_latent (the calls that return the pairwise
                                   # joint) run the dense log-domain scans with the full kernel: every
                                   # row of p_transition_* is then the reference's conditional, also for
@@ -341,6 +343,9 @@ class DeviceEM:
     def _seg_bits(self):
         """PMG_PHASE_SEGMENTS of ScanConfig.relax_segments (0: the library default)."""
         return nat.phase_segments(self.scan.relax_segments)
+
+    def _tw_bits(self):
+        return nat.PHASE_TWO_WAVES if self.scan.two_waves else 0
 
     # ------------------------------------------------------------------ setup
     def set_transition(self, tr):
@@ -719,7 +724,7 @@ class DeviceEM:
         self.alpha_bits = 0 if keep_alpha else nat.PHASE_NO_JUMP_ROWS
         ad = nat.PHASE_ADAPTIVE_WARMUP if (sc.device_adaptive and self.adaptive) else 0
         with self._t('forward_filter'):          # main chunk-parallel pass (k_forward)
-            nat.check(self.lib.pmg_forward_filter_phase(*args, 1 | ad | self.alpha_bits), "pmg_forward_filter")
+            nat.check(self.lib.pmg_forward_filter_phase(*args, 1 | ad | self.alpha_bits | self._tw_bits()), "pmg_forward_filter")
         with self._t('forward_repair'):          # verify / relaxation / logZ
             nat.check(self.lib.pmg_forward_filter_phase(*args, 2 | ad | self.alpha_bits | self._seg_bits()),
                       "pmg_forward_filter")
@@ -752,7 +757,7 @@ class DeviceEM:
         if P:
             self._p_fresh = 'planes' if planes else 'f32'
         with self._t('backward_smoother'):       # main chunk-parallel pass (k_backward)
-            nat.check(self.lib.pmg_backward_smoother_phase(*args, 1 | ad), "pmg_backward_smoother")
+            nat.check(self.lib.pmg_backward_smoother_phase(*args, 1 | ad | self._tw_bits()), "pmg_backward_smoother")
         with self._t('backward_repair'):         # verify / relaxation
             nat.check(self.lib.pmg_backward_smoother_phase(*args, 2 | ad | self._seg_bits()), "pmg_backward_smoother")
 
@@ -996,6 +1001,7 @@ class RestartBatchEM:
 
     _t = DeviceEM._t
     _seg_bits = DeviceEM._seg_bits
+    _tw_bits = DeviceEM._tw_bits
     PLANES = False
     P = DeviceEM.P
 
@@ -1110,7 +1116,7 @@ class RestartBatchEM:
                 nat.ptr(self.alpha), nat.ptr(self.logc), nat.ptr(logz_out), nat.ptr(self.ws_fb),
                 self.ws_fb.numel(), nat.stream_handle())
         with self._t('forward_filter'):
-            nat.check(self.lib.pmg_forward_filter_batched(*args, 1 | bits), "pmg_forward_filter_batched")
+            nat.check(self.lib.pmg_forward_filter_batched(*args, 1 | bits | self._tw_bits()), "pmg_forward_filter_batched")
         with self._t('forward_repair'):
             nat.check(self.lib.pmg_forward_filter_batched(*args, 2 | bits | self._seg_bits()),
                       "pmg_forward_filter_batched")
@@ -1125,7 +1131,7 @@ class RestartBatchEM:
         ad = (nat.PHASE_ADAPTIVE_WARMUP if self.scan.device_adaptive else 0) | (nat.PHASE_P_BF16X3 if planes else 0)
         self._p_fresh = 'planes' if planes else 'f32'
         with self._t('backward_smoother'):
-            nat.check(self.lib.pmg_backward_smoother_batched(*args, 1 | ad), "pmg_backward_smoother_batched")
+            nat.check(self.lib.pmg_backward_smoother_batched(*args, 1 | ad | self._tw_bits()), "pmg_backward_smoother_batched")
         with self._t('backward_repair'):
             nat.check(self.lib.pmg_backward_smoother_batched(*args, 2 | ad | self._seg_bits()),
                       "pmg_backward_smoother_batched")

@@ -156,6 +156,33 @@ def test_forward_backward_vs_oracle(case):
         np.testing.assert_allclose(J, np.exp(lj), rtol=1e-5, atol=1e-5 * max(1.0, np.exp(lj).max()))
 
 
+@pytest.mark.parametrize("L,chunk,warm", [(512, None, 48), (300, 16, 0), (1024, 32, 8), (512, 40, 24)])
+def test_two_wave_chains_match_one_wave(L, chunk, warm):
+    """PMG_PHASE_TWO_WAVES (each main-pass chain on two waves of J/2 latents, band halo
+    and per-step sums through LDS): the EM E-step (P only) against the one-wave kernels
+    and the f64 oracle -- logZ rel 1e-7 and P within the scan bars (the two forms differ
+    only in f32 summation order); (300, 16, 0) has partial lanes and every boundary
+    repaired, (1024, .) runs the J = 16 layout as two waves of 8."""
+    from poor_man_gplvm_amd.engine import ScanConfig
+    N, T = 40, 2000
+    d = make(N, L, T)
+    out = {}
+    for tw in (False, True):
+        sp, eng = _engine(d, L, chunk=chunk, warmup=warm)
+        eng.scan = ScanConfig(chunk=chunk, warmup=warm, two_waves=tw)
+        eng.set_tuning(d['tuning'])
+        logz = torch.zeros(1, dtype=torch.float64, device='cuda')
+        eng.e_step(1.0, logz)
+        eng.scan_status()
+        out[tw] = (logz.item(), eng.P.cpu().numpy().copy())
+    K, logK, A, logA = O.create_transition_prob_1d(L, 1.0, 0.01, 0.01)
+    lpa, lz, _, _, _, _ = O.smooth_all_step_combined_ma_chunk(d['y'], d['tuning'], logK, logA, with_joint=False)
+    for tw in (False, True):
+        assert abs(out[tw][0] - lz) <= 1e-7 * abs(lz)
+        close_prob(out[tw][1], np.exp(lpa).sum(1))
+    assert abs(out[True][0] - out[False][0]) <= 1e-9 * abs(lz)
+
+
 @pytest.mark.parametrize("L,chunk,warm", [(64, None, 64), (128, 16, 0), (256, None, 48), (512, 16, 0),
                                           (1024, 32, 8), (200, None, 48)])
 def test_backward_planes_bit_identical(L, chunk, warm, monkeypatch):
