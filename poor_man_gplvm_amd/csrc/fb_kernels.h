@@ -200,24 +200,33 @@ __device__ __forceinline__ void relax_warm_decision(const FBParams& p, int pendi
 // ---------------------------------------------------------------------------
 // per-lane helpers (lane owns latents j0 .. j0+J-1, j0 = lane*J)
 // ---------------------------------------------------------------------------
+// One lane's J values of a streamed row, held as 4-wide vectors: a row-ring slot is then
+// a few 128-bit values that its buffer loads fill in place (as J separate floats hipcc
+// re-pairs them for the packed math and copies every refill into the slot's registers,
+// each copy waiting for its load).
+typedef float f4v __attribute__((ext_vector_type(4)));
 template <int J>
-__device__ __forceinline__ void load_row(const float* __restrict__ row, int L, int j0, float v[J]) {
+struct RowV {
+  f4v q[(J + 3) / 4];
+  __device__ __forceinline__ float operator[](int j) const { return q[j >> 2][j & 3]; }
+  __device__ __forceinline__ void set(int j, float x) { q[j >> 2][j & 3] = x; }
+};
+
+template <int J>
+__device__ __forceinline__ void load_row(const float* __restrict__ row, int L, int j0, RowV<J>& v) {
   if ((L & 3) == 0 && (J & 3) == 0 && j0 + J <= L) {
 #pragma unroll
-    for (int j = 0; j < J; j += 4) {
-      float4 q = *reinterpret_cast<const float4*>(row + j0 + j);
-      v[j] = q.x; v[j + 1] = q.y; v[j + 2] = q.z; v[j + 3] = q.w;
-    }
+    for (int j = 0; j < J; j += 4) v.q[j >> 2] = *reinterpret_cast<const f4v*>(row + j0 + j);
   } else {
 #pragma unroll
-    for (int j = 0; j < J; ++j) v[j] = (j0 + j < L) ? row[j0 + j] : 0.f;
+    for (int j = 0; j < J; ++j) v.set(j, (j0 + j < L) ? row[j0 + j] : 0.f);
   }
 }
 
 // raw emission operands for one time step
 template <int J>
 struct EmRaw {
-  float d[J];
+  RowV<J> d;
   float ph;
 };
 
@@ -228,11 +237,35 @@ __device__ __forceinline__ void em_load(const FBParams& p, int64_t t, int j0, Em
   r.ph = (b < p.nblk) ? p.phi[t * p.ldphi + b] : 0.f;
 }
 
+// exp_acc on an aligned element pair (j, j + 1) as packed math: the pairing is the one the
+// row slot's 128-bit loads deliver, so hipcc does not re-pair (copy) the loaded values
+typedef float f2x __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2x exp_acc2(f2x x) {
+  constexpr float kL2E = 1.44269502162933349609375f;
+  constexpr float kL2E_lo = 1.925963033500011e-08f;
+  const f2x y = x * (f2x){kL2E, kL2E};
+  f2x err = __builtin_elementwise_fma(x, (f2x){kL2E, kL2E}, -y);
+  err = __builtin_elementwise_fma(x, (f2x){kL2E_lo, kL2E_lo}, err);
+  const f2x r = {__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)};
+  return __builtin_elementwise_fma(r, err * (f2x){0.693147180559945309f, 0.693147180559945309f}, r);
+}
+
 // FULL: every lane's latents are < L (L == Lpad), so no lane-validity select
 template <int J, bool FULL = false>
 __device__ __forceinline__ void em_exp(const FBParams& p, int j0, const EmRaw<J>& r, float e[J]) {
+  if constexpr (FULL && (J % 2) == 0) {
 #pragma unroll
-  for (int j = 0; j < J; ++j) e[j] = (FULL || j0 + j < p.L) ? exp_acc(fmaf(p.s, r.d[j], r.ph)) : 0.f;
+    for (int j = 0; j < J; j += 2) {
+      const f2x d = {r.d[j], r.d[j + 1]};
+      const f2x x = __builtin_elementwise_fma((f2x){p.s, p.s}, d, (f2x){r.ph, r.ph});
+      const f2x v = exp_acc2(x);
+      e[j] = v.x;
+      e[j + 1] = v.y;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < J; ++j) e[j] = (FULL || j0 + j < p.L) ? exp_acc(fmaf(p.s, r.d[j], r.ph)) : 0.f;
+  }
 }
 
 // One wave holds the whole line (lane l owns latents lJ .. lJ+J-1): the halo comes
@@ -660,20 +693,15 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 template <int J, int VEC>
-__device__ __forceinline__ void bload_row(const float* row, int L, int j0, float v[J]) {
+__device__ __forceinline__ void bload_row(const float* row, int L, int j0, RowV<J>& v) {
   const __amdgpu_buffer_rsrc_t rs = rsrc_of(row, (uint32_t)L * 4u);
   if constexpr (VEC) {
 #pragma unroll
-    for (int j = 0; j < J; j += 4) {
-      const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, (j0 + j) * 4, 0, 0);
-      v[j] = __uint_as_float(q.x);
-      v[j + 1] = __uint_as_float(q.y);
-      v[j + 2] = __uint_as_float(q.z);
-      v[j + 3] = __uint_as_float(q.w);
-    }
+    for (int j = 0; j < J; j += 4)
+      v.q[j >> 2] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, (j0 + j) * 4, 0, 0));
   } else {
 #pragma unroll
-    for (int j = 0; j < J; ++j) v[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (j0 + j) * 4, 0, 0));
+    for (int j = 0; j < J; ++j) v.set(j, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (j0 + j) * 4, 0, 0)));
   }
 }
 
@@ -763,6 +791,18 @@ __device__ __forceinline__ void bstore_f64_lane0(double* base, int64_t t, double
 // since (s_waitcnt vmcnt(0) once per ring cycle).
 __device__ __forceinline__ void order_after(float& v, float dep) { asm volatile("" : "+v"(v) : "v"(dep)); }
 
+// The values derived from a ring slot exist before the slot's refill is issued: the old
+// and the new contents of the slot are then never live together, so the refill loads
+// straight into the slot's registers.  Otherwise hipcc hoists the refill, loads into
+// other registers and copies them into the slot before the loop's back edge -- and a copy
+// of a loaded register waits for the load (s_waitcnt vmcnt(0) inside the ring cycle).
+template <int J>
+__device__ __forceinline__ void slot_consumed(const float v[J]) {
+#pragma unroll
+  for (int j = 0; j < J; ++j) asm volatile("" ::"v"(v[j]));
+  asm volatile("" ::: "memory");
+}
+
 template <int J, int VEC>
 __device__ __forceinline__ void bem_load(const FBParams& p, int64_t t, int j0, EmRaw<J>& r) {
   bload_row<J, VEC>(p.delta + t * p.ldd, p.L, j0, r.d);
@@ -794,6 +834,7 @@ __device__ __forceinline__ double fwd_stream_piece(const FBParams& p, Fwd<J, WP,
     double mt = 0.0;
     if constexpr (OUT && MLDS) mt = sm[t - t_a];
     if constexpr (OUT && !MLDS) mt = mr[q];
+    slot_consumed<J>(e);
     if (refill) {
       const int64_t tl = t + PF < last ? t + PF : last;
       bem_load<J, VEC>(p, tl, j0, ring[q]);
@@ -1247,6 +1288,7 @@ __device__ __forceinline__ void bwd_stream_warm(const FBParams& p, Bwd<J, WP, NW
     float e[J];
     order_after(ring[q].ph, st.b0[0]);
     em_exp<J, VEC == 2>(p, j0, ring[q], e);
+    slot_consumed<J>(e);
     if (refill) bem_load<J, VEC>(p, t - PF > t_lo ? t - PF : t_lo, j0, ring[q]);
     float eb0[J], eb1[J], V0, V1;
     e_beta(st, e, eb0, eb1, V0, V1);
@@ -1263,11 +1305,12 @@ __device__ __forceinline__ void bwd_stream_warm(const FBParams& p, Bwd<J, WP, NW
     if (tb - q >= t_lo) body(q, tb - q, false);
 }
 
+typedef float f2v_t __attribute__((ext_vector_type(2)));
 template <int J>
 struct BRow {
   EmRaw<J> em;
-  float a0[J];
-  float js, ji;  // the forward's (jump, 1/S) of this step
+  RowV<J> a0;
+  f2v_t jj;  // the forward's (jump, 1/S) of this step
 };
 
 template <int J, int VEC>
@@ -1275,8 +1318,7 @@ __device__ __forceinline__ void brow_load(const FBParams& p, int64_t t, int j0, 
   bem_load<J, VEC>(p, t, j0, r.em);
   bload_row<J, VEC>(p.alpha_in + t * 2 * (int64_t)p.L, p.L, j0, r.a0);
   const __amdgpu_buffer_rsrc_t rs = rsrc_of(p.jsc + 2 * t, 8u);
-  r.js = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, 0, 0, 0));
-  r.ji = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, 4, 0, 0));
+  r.jj = __builtin_bit_cast(f2v_t, __builtin_amdgcn_raw_buffer_load_b64(rs, 0, 0, 0));
 }
 
 // alpha_t's d = 1 row as the forward formed it: (jump * e) * (1/S)
@@ -1296,7 +1338,7 @@ __device__ __forceinline__ void store_weights(const FBParams& p, int64_t t_c, in
   brow_load<J, VEC>(p, t_c, j0, r);
   float e[J], a1[J];
   em_exp<J, VEC == 2>(p, j0, r.em, e);
-  alpha1_row<J>(r.js, r.ji, e, a1);
+  alpha1_row<J>(r.jj.x, r.jj.y, e, a1);
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     dst[j0 + j] = r.a0[j];
@@ -1322,8 +1364,7 @@ __device__ __forceinline__ void bwd_stream_out(const FBParams& p, Bwd<J, WP, NW>
     em_exp<J, VEC == 2>(p, j0, ring[q].em, e);
 #pragma unroll
     for (int j = 0; j < J; ++j) a0[j] = ring[q].a0[j];
-    const float js = ring[q].js, ji = ring[q].ji;
-    if (refill) brow_load<J, VEC>(p, t - PF > t_c ? t - PF : t_c, j0, ring[q]);
+    const float js = ring[q].jj.x, ji = ring[q].jj.y;
     e_beta(st, e, eb0, eb1, V0, V1);
     float G = 0.f;
     if constexpr (MODE == 0) {
@@ -1334,6 +1375,8 @@ __device__ __forceinline__ void bwd_stream_out(const FBParams& p, Bwd<J, WP, NW>
         pp[j] = fmaf(a0[j], st.b0[j], jj * eb1[j]);
         G += pp[j];
       }
+      slot_consumed<J>(pp);
+      slot_consumed<J>(eb0);
     } else {
       alpha1_row<J>(js, ji, e, a1);
 #pragma unroll
@@ -1342,14 +1385,22 @@ __device__ __forceinline__ void bwd_stream_out(const FBParams& p, Bwd<J, WP, NW>
         a1[j] *= st.b1[j];
         G += a0[j] + a1[j];
       }
+      slot_consumed<J>(a0);
+      slot_consumed<J>(a1);
+      slot_consumed<J>(eb0);
     }
+    if (refill) brow_load<J, VEC>(p, t - PF > t_c ? t - PF : t_c, j0, ring[q]);
     st.sums(eb0, V0, V1, &G);
     const float iG = rcp_nr(G);
     if constexpr (MODE == 0) {
 #pragma unroll
       for (int j = 0; j < J; ++j) pp[j] *= iG;
-      if (p.Pq) bstore_planes<J, VEC>(p, t, j0, pp);
-      else bstore_row<J, VEC>(p.P + t * p.ldd, p.L, j0, pp);
+      if constexpr (VEC == 2) {   // dispatched only without planes: no branch in the step loop
+        bstore_row<J, VEC>(p.P + t * p.ldd, p.L, j0, pp);
+      } else {
+        if (p.Pq) bstore_planes<J, VEC>(p, t, j0, pp);
+        else bstore_row<J, VEC>(p.P + t * p.ldd, p.L, j0, pp);
+      }
     } else {
 #pragma unroll
       for (int j = 0; j < J; ++j) {
@@ -1417,7 +1468,7 @@ __device__ __forceinline__ void backward_chunk(const FBParams& p, int c, int j0,
 #define PMG_BWD_DISPATCH(MODE)                                          \
   if constexpr (J % 4 == 0) {                                           \
     if ((p.L & 3) == 0) {                                               \
-      if (MODE == 0 && p.L == p.Lpad)                                   \
+      if (MODE == 0 && p.L == p.Lpad && !p.Pq)                          \
         backward_chunk<J, WP, 2, MODE, NW>(p, c, j0, invz);             \
       else                                                              \
         backward_chunk<J, WP, 1, MODE, NW>(p, c, j0, invz);             \
@@ -1542,7 +1593,7 @@ __global__ void __launch_bounds__(64) k_backward_relax(FBParams p_arg) {
       // EM passes (P only): the main pass's P arithmetic (MODE 0: P bit-identical to a
       // main pass from the same beta), no gamma / rho rows, no v kept
       if (!p.gamma && !p.rho) {
-        if (p.L == p.Lpad) backward_relax<J, WP, 2, 0>(p, j0, invz);
+        if (p.L == p.Lpad && !p.Pq) backward_relax<J, WP, 2, 0>(p, j0, invz);
         else backward_relax<J, WP, 1, 0>(p, j0, invz);
       } else {
         backward_relax<J, WP, 1>(p, j0, invz);
