@@ -258,10 +258,11 @@ def bench_timeshard(args):
     nus = [torch.zeros_like(Ws[0]) for _ in range(n)]
     cnts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(n)]
     n_all = args.warmup + args.steps
-    stats = torch.zeros((n_all, 4), dtype=torch.float64, device=dev)
-    lh = torch.zeros((n_all, adam.maxiter), dtype=torch.float64, device=dev)
+    n_inst = min(args.steps, 5)      # instrumented iterations after the timed window
+    stats = torch.zeros((n_all + n_inst, 4), dtype=torch.float64, device=dev)
+    lh = torch.zeros((n_all + n_inst, adam.maxiter), dtype=torch.float64, device=dev)
     eh = torch.zeros_like(lh)
-    logz = torch.zeros(n_all, dtype=torch.float64, device=dev)
+    logz = torch.zeros(n_all + n_inst, dtype=torch.float64, device=dev)
     rounds = []
 
     def em_iter(i):
@@ -288,8 +289,7 @@ def bench_timeshard(args):
                    "kernels_ms_total": {k: round(v[1] * v[0], 3) for k, v in s0.items()},
                    "repairs": [list(s.repairs()) for s in eng.shards]}
     torch.cuda.synchronize()
-    timer = KernelTimer()
-    eng.set_timer(timer)
+    eng.set_timer(None)          # the timed window runs uninstrumented (as the default engine's)
     if rccl:
         dist.barrier()
     torch.cuda.synchronize()
@@ -304,9 +304,16 @@ def bench_timeshard(args):
         te = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
         elapsed = float(te.item())
+    # per-section HIP events over a few more iterations of the same fit
+    timer = KernelTimer()
+    eng.set_timer(timer)
+    for i in range(n_all, n_all + n_inst):
+        em_iter(i)
+    torch.cuda.synchronize()
+    eng.set_timer(None)
     summ = timer.summary()      # mean per call; every local shard makes its own calls
     st = stats.cpu().numpy()
-    adam_iters = float(np.mean(st[args.warmup:, 0])) if args.steps else 0.0
+    adam_iters = float(np.mean(st[args.warmup:n_all, 0])) if args.steps else 0.0
     T_ext = max(s.T for s in eng.shards)
     pmc, pmc_src = load_pmc(args.config)
     rooflines = compute_rooflines(summ, T_ext, L, N, B.shape[1], adam_iters, pmc)
@@ -335,10 +342,12 @@ def bench_timeshard(args):
         "roofline": roof_dom,
         "rooflines": rooflines,
         "kernels_ms": {k: round(v[1], 4) for k, v in summ.items()},
+        "kernels_ms_note": (f"per-section HIP events of {n_inst} more iterations of the same fit right after "
+                            "the timed window (the timed iterations run without them)"),
         "fwd_bwd_GBps_per_shard": 28.0 * T_ext * L / 1e9 / (t_fb / 1e3),
         "adam_iters_mean": adam_iters,
         "chunk": lays[0].chunk,
-        "carry_rounds_timed": rounds[args.warmup:],
+        "carry_rounds_timed": rounds[args.warmup:n_all],
         "repairs_last": [list(s.repairs()) for s in eng.shards],
         "first_iteration": it0,
         "warmup_iteration_s": [round(v, 4) for v in warm_s],

@@ -282,7 +282,10 @@ def adam_stop_body(losses, j0, maxiter, tol, state):
     return None
 
 
-def speculative_adam(run, snapshot, restore, allreduce, maxiter, tol, batch=16):
+SPEC_BATCH = 16     # bodies per speculative launch of the neuron-sharded Adam (the exact-F refresh period)
+
+
+def speculative_adam(run, snapshot, restore, allreduce, maxiter, tol, batch=SPEC_BATCH):
     """Neuron-sharded Adam loop with the reference's global stop rule.
 
     Every rank runs its own neuron slice (the loss and the gradient norm are sums over
@@ -496,15 +499,18 @@ class TimeShardedEM:
 
     def e_step(self, likelihood_scale, logz_out, gamma=None):
         """logz_out: (1,) f64 device tensor <- the global log marginal (decoder.py:169)."""
-        scratch = torch.empty(1, dtype=torch.float64, device=self.dev)
+        if getattr(self, '_estep_bufs', None) is None:     # scratch and per-shard logZ parts, once
+            self._estep_bufs = (torch.empty(1, dtype=torch.float64, device=self.dev),
+                                [torch.empty(1, dtype=torch.float64, device=self.dev) for _ in self.shards])
+        scratch, lzp = self._estep_bufs
         for s in self.shards:
             s.emission(likelihood_scale)
             s.forward(likelihood_scale, scratch, keep_alpha=gamma is not None)
         self.carry_rounds[0] = self._carry(0, likelihood_scale, scratch)
         parts = []
-        for s in self.shards:
-            parts.append([torch.empty(1, dtype=torch.float64, device=self.dev)])
-            s.own_logz(parts[-1][0])
+        for s, buf in zip(self.shards, lzp):
+            parts.append([buf])
+            s.own_logz(buf)
         for s, g in zip(self.shards, gamma or [None] * len(self.shards)):
             s.backward(likelihood_scale, True, g)
         self.carry_rounds[1] = self._carry(1, likelihood_scale, scratch, gamma)
@@ -544,9 +550,13 @@ class TimeShardedEM:
             d['count'] = c
             sl.append(d)
         mi = max(int(cfg.maxiter), 1)
-        st_dev = torch.zeros(4, dtype=torch.float64, device=self.dev)
-        lh_dev = torch.zeros(mi + 1, dtype=torch.float64, device=self.dev)
-        eh_dev = torch.zeros_like(lh_dev)
+        ns = len(self.shards)
+        # per local slice: stats (4) | loss history | error history (hl entries each: a
+        # speculative launch writes SPEC_BATCH + 1 of them whatever maxiter is), so that one
+        # launch per slice and ONE device-to-host copy serve a batch (no host sync between
+        # the slices)
+        hl = max(mi, SPEC_BATCH + 1) + 1
+        hist = torch.zeros((ns, 4 + 2 * hl), dtype=torch.float64, device=self.dev)
 
         def run(kmax):
             # tol < 0: the local stop rule (rel > tol) never fires, so every rank runs exactly
@@ -554,11 +564,17 @@ class TimeShardedEM:
             # early on one rank only and desynchronise the loss all-reduce)
             c = AdamConfig(lr=cfg.lr, maxiter=kmax, tol=-1.0, prior_std=cfg.prior_std, b1=cfg.b1, b2=cfg.b2,
                            eps=cfg.eps, eps_root=cfg.eps_root)
+            k = int(kmax)
+            if k > hl:
+                raise ValueError(f"speculative Adam launch of {k} bodies > history slots {hl}")
+            for i, (s, d) in enumerate(zip(self.shards, sl)):
+                h = hist[i]
+                s.adam(d['W'], d['mu'], d['nu'], d['count'], c, h[:4], h[4:4 + hl], h[4 + hl:], yw=d['yw'])
+            sel = torch.cat([hist[:, :1], hist[:, 4:4 + k], hist[:, 4 + hl:4 + hl + k]], dim=1).cpu().numpy()
             outs = []
-            for s, d in zip(self.shards, sl):
-                s.adam(d['W'], d['mu'], d['nu'], d['count'], c, st_dev, lh_dev, eh_dev, yw=d['yw'])
-                n = int(st_dev[0].item())
-                outs.append((n, lh_dev[:n].cpu().numpy(), eh_dev[:n].cpu().numpy()))
+            for row in sel:
+                n = int(row[0])
+                outs.append((n, row[1:1 + n], row[1 + k:1 + k + n]))
             return outs
 
         def snapshot():
@@ -572,7 +588,7 @@ class TimeShardedEM:
                 d['count'].copy_(c)
 
         res = speculative_adam(run, snapshot, restore, self.comm.allreduce_process_sum, int(cfg.maxiter),
-                               float(cfg.tol))
+                               float(cfg.tol), batch=SPEC_BATCH)
         self.comm.allgather_cols([d['W'] for d in sl], Ws, bounds)
         n = res['n_iter']
         stats.copy_(torch.tensor([n, res['final_loss'], res['final_error'], res['loss0']], dtype=torch.float64))
