@@ -59,9 +59,18 @@ constexpr int kMaxBand = 32;
 #ifndef PMG_ALPHA_AUX
 #define PMG_ALPHA_AUX 2
 #endif
-constexpr int kPfFwd = 4;
-constexpr int kPfBwdWarm = 4;
-constexpr int kPfBwdOut = 2;
+#ifndef PMG_PF_FWD
+#define PMG_PF_FWD 4
+#endif
+#ifndef PMG_PF_BWD_WARM
+#define PMG_PF_BWD_WARM 4
+#endif
+#ifndef PMG_PF_BWD_OUT
+#define PMG_PF_BWD_OUT 2
+#endif
+constexpr int kPfFwd = PMG_PF_FWD;
+constexpr int kPfBwdWarm = PMG_PF_BWD_WARM;
+constexpr int kPfBwdOut = PMG_PF_BWD_OUT;
 // the relaxation kernel runs <= 1 wave per CU: a deeper ring covers the latency alone,
 // as deep as the registers allow (a backward row is 3J floats).  J = 8 forward: 4, not 8
 // (with the EM relaxation's A1-free loop, the 4-deep ring was 7 % faster on the first
