@@ -160,7 +160,7 @@ def cpu_baseline(N, T, L, adam_iters, t_sample=1024, adam_sample=20):
 
 def load_pmc(config):
     """Per-kernel HBM bytes from this round's PMC summary (tools/gpu_pmc.sh), if any."""
-    for rnd in ("r05", "r04", "r03", "r02", "r01"):
+    for rnd in ("r06", "r05", "r04", "r03", "r02", "r01"):
         path = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{config}.json")
         if os.path.exists(path):
             with open(path) as fh:

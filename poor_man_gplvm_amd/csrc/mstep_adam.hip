@@ -344,8 +344,8 @@ __global__ void __launch_bounds__(kThreads) k_adam(AdamParams p_arg) {
   __shared__ double sYw[SP][kThreads];
   __shared__ double sTw[kThreads];
   __shared__ double sF[SP][kThreads];
-  __shared__ __attribute__((aligned(16))) double sLog[2 * kLogTab];   // log_tab's table
-  for (int q = tid; q < kLogTab; q += blockDim.x) log_tab_entry(q, sLog[2 * q], sLog[2 * q + 1]);
+  __shared__ __attribute__((aligned(16))) double sLog[kMathTab];      // softplus_tab's log + exp tables
+  for (int q = tid; q < kLogTab + kExpTab; q += blockDim.x) math_tab_entry(q, sLog);
 #pragma unroll
   for (int s = 0; s < SP; ++s) {
     sYw[s][tid] = (is_row && s < S) ? p.yw[(size_t)lrow * p.N + n0 + s] : 0.0;

@@ -149,23 +149,84 @@ PMG_HD double log_tab(double x, const double* tab) {
   return hi + fma(kd, 1.90821492927058770002e-10, lp);
 }
 
-// softplus, its log and the sigmoid with the table log: log1p(e) = log(u) + (e - (u - 1)) / u,
-// u = 1 + e rounded (u - 1 and e - (u - 1) are exact; the correction is below ulp(u), so an
-// approximate reciprocal suffices).  The sigmoid is returned to f32 accuracy: it only scales
-// the f32 gradient factor G.
+// log u for u in [1, 2) with the table of log_tab: no exponent split (k = 0)
+PMG_HD double log_tab_unit(double u, const double* tab) {
+#ifdef __HIP_DEVICE_COMPILE__
+  const int j = (int)((__double2hiint(u) >> 13) & (kLogTab - 1));
+#else
+  long long bits;
+  memcpy(&bits, &u, 8);
+  const int j = (int)((bits >> 45) & (kLogTab - 1));
+#endif
+  const double invc = tab[2 * j], nlc = tab[2 * j + 1];
+  const double r = fma(u, invc, -1.0);
+  double p = -1.0 / 8.0;
+  p = fma(p, r, 1.0 / 7.0);
+  p = fma(p, r, -1.0 / 6.0);
+  p = fma(p, r, 1.0 / 5.0);
+  p = fma(p, r, -1.0 / 4.0);
+  p = fma(p, r, 1.0 / 3.0);
+  p = fma(p, r, -1.0 / 2.0);
+  return nlc + fma(r * r, p, r);
+}
+
+// ---------------------------------------------------------------------------------
+// Table-driven e^x (x <= 0) for the hot loop: x = (64 n + j) ln2 / 64 + r, |r| <= ln2 / 128,
+// e^x = 2^n 2^(j/64) e^r with e^r to degree 6 (r^7 / 7! < 2^-64); entry j = 2^(j/64) is
+// built from exp_neg64 (2 e^((j - 64) ln2 / 64)).  It sits after the log table: the k_adam
+// LDS table and softplus_tab's `tab` hold both (kMathTab doubles).
+// ---------------------------------------------------------------------------------
+constexpr int kExpTab = 64;
+constexpr int kMathTab = 2 * kLogTab + kExpTab;
+
+PMG_HD double exp_tab_entry(int j) {
+  return 2.0 * exp_neg64((double)(j - kExpTab) * (6.93147180559945309417e-01 / kExpTab));
+}
+
+// the whole table: log part (log_tab_entry) then exp part
+PMG_HD void math_tab_entry(int q, double* tab) {
+  if (q < kLogTab) log_tab_entry(q, tab[2 * q], tab[2 * q + 1]);
+  else if (q < kLogTab + kExpTab) tab[2 * kLogTab + (q - kLogTab)] = exp_tab_entry(q - kLogTab);
+}
+
+PMG_HD double exp_neg_tab(double x, const double* et) {
+  const double kL2E64 = 92.332482616893656;                 // 64 / ln 2
+  const double kLn2Hi64 = 6.93147180369123816490e-01 / 64;  // 32 significant bits: k * it is exact
+  const double kLn2Lo64 = 1.90821492927058770002e-10 / 64;
+  x = x < -745.0 ? -745.0 : x;
+  const double k = rint(x * kL2E64);
+  double r = fma(-k, kLn2Hi64, x);
+  r = fma(-k, kLn2Lo64, r);
+  double p = 1.0 / 720.0;
+  p = fma(p, r, 1.0 / 120.0);
+  p = fma(p, r, 1.0 / 24.0);
+  p = fma(p, r, 1.0 / 6.0);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  const int ki = (int)k;
+  return ldexp(et[ki & (kExpTab - 1)] * p, ki >> 6);
+}
+
+// softplus, its log and the sigmoid with the table log and exp: log1p(e) = log(u) +
+// (e - (u - 1)) / u, u = 1 + e rounded (u - 1 and e - (u - 1) are exact; the correction is
+// below ulp(u), so an approximate reciprocal suffices); u in (1, 2], log 2 exactly at u = 2.
+// The sigmoid is returned to f32 accuracy: it only scales the f32 gradient factor G.
+// tab: kMathTab doubles (math_tab_entry).
 struct SoftplusT {
   double f, logf;
   float sg;
 };
 PMG_HD SoftplusT softplus_tab(double F, const double* tab) {
-  const double e = exp_neg64(-fabs(F));
+  const double e = exp_neg_tab(-fabs(F), tab + 2 * kLogTab);
   const double u = 1.0 + e;
 #ifdef __HIP_DEVICE_COMPILE__
   const double ru = __builtin_amdgcn_rcp(u);
 #else
   const double ru = 1.0 / u;
 #endif
-  const double l1p = log_tab(u, tab) + (e - (u - 1.0)) * ru;
+  const double lu = u < 2.0 ? log_tab_unit(u, tab) : 6.93147180559945309417e-01;
+  const double l1p = lu + (e - (u - 1.0)) * ru;
   SoftplusT o;
   o.f = fmax(F, 0.0) + l1p;
   o.logf = log_tab(o.f + 1e-20, tab);

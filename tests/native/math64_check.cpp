@@ -18,11 +18,11 @@ static double logerr(double got, long double ref) {
 }
 
 int main() {
-  double tab[2 * pmg::kLogTab];
-  for (int j = 0; j < pmg::kLogTab; ++j) pmg::log_tab_entry(j, tab[2 * j], tab[2 * j + 1]);
+  double tab[pmg::kMathTab];
+  for (int q = 0; q < pmg::kLogTab + pmg::kExpTab; ++q) pmg::math_tab_entry(q, tab);
   std::mt19937_64 g(1);
   std::uniform_real_distribution<double> wide(-40, 40), narrow(-3, 3), lx(-350, 350);
-  double ef = 0, el = 0, es = 0, ee = 0, eg = 0, tf = 0, tl = 0, ts = 0, tg = 0;
+  double ef = 0, el = 0, es = 0, ee = 0, eg = 0, tf = 0, tl = 0, ts = 0, tg = 0, te = 0;
   for (int i = 0; i < 1000000; ++i) {
     const double F = (i & 1) ? wide(g) : narrow(g);
     const pmg::Softplus64 o = pmg::softplus64(F);
@@ -38,10 +38,11 @@ int main() {
     tl = std::fmax(tl, logerr(t.logf, lf));
     ts = std::fmax(ts, std::fabs((double)t.sg - (double)sg) / (double)sg);
     ee = std::fmax(ee, ulps(pmg::exp_neg64(-std::fabs(F)), e));
+    te = std::fmax(te, ulps(pmg::exp_neg_tab(-std::fabs(F), tab + 2 * pmg::kLogTab), e));
     const double x = std::exp(lx(g) * 2);
     eg = std::fmax(eg, ulps(pmg::log64(x), logl((long double)x)));
     tg = std::fmax(tg, logerr(pmg::log_tab(x, tab), logl((long double)x)));
   }
-  std::printf("%.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3e %.3f\n", ef, el, es, ee, eg, tf, tl, ts, tg);
+  std::printf("%.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3e %.3f %.3f\n", ef, el, es, ee, eg, tf, tl, ts, tg, te);
   return 0;
 }

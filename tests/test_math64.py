@@ -18,7 +18,7 @@ def test_math64_accuracy(tmp_path):
     subprocess.run(['g++', '-O2', '-std=c++17', '-I', os.path.join(ROOT, 'poor_man_gplvm_amd', 'csrc'),
                     os.path.join(HERE, 'native', 'math64_check.cpp'), '-o', str(exe)], check=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
-    softplus, logf, sigmoid, exp_, log_, t_softplus, t_logf, t_sigmoid_rel, t_log = map(float, out)
+    softplus, logf, sigmoid, exp_, log_, t_softplus, t_logf, t_sigmoid_rel, t_log, t_exp = map(float, out)
     # series forms (f64 ulps; log(f) in eps relative to max(1, |log f|))
     assert softplus <= 4.0
     assert logf <= 6.0
@@ -30,3 +30,4 @@ def test_math64_accuracy(tmp_path):
     assert t_logf <= 7.0
     assert t_log <= 3.0
     assert t_sigmoid_rel <= 3e-7
+    assert t_exp <= 3.0
