@@ -1059,7 +1059,9 @@ struct DenseWork {
 };
 
 // latents per thread: JD = 8 carries L in (1024, 2048], which the banded scans do not hold
-static int dense_jd(int L) { return L <= 256 ? 1 : L <= 512 ? 2 : L <= 1024 ? 4 : L <= 2048 ? 8 : -1; }
+static int dense_jd(int L) {
+  return L <= 256 ? 1 : L <= 512 ? 2 : L <= 1024 ? 4 : L <= 2048 ? 8 : L <= 4096 ? 16 : -1;
+}
 
 static DenseWork carve_dense(void* ws, int64_t T, int Lp, int C, size_t* total = nullptr) {
   const int64_t M = (T + C - 1) / C;
@@ -1091,7 +1093,7 @@ static int dense_params(DenseParams& p, const pmg_dense_transition* tr, int64_t 
               "pmg dense scan: bad transition");
   PMG_REQUIRE(T > 0 && C > 0 && B >= 0, "pmg dense scan: T=%lld chunk=%d warmup=%d", (long long)T, C, B);
   const int JD = dense_jd(tr->L);
-  PMG_REQUIRE(JD > 0, "pmg dense scan: L=%d > 2048 unsupported", tr->L);
+  PMG_REQUIRE(JD > 0, "pmg dense scan: L=%d > 4096 unsupported", tr->L);
   memset(&p, 0, sizeof(p));
   p.T = T;
   p.L = tr->L;
@@ -1128,7 +1130,8 @@ static void dense_kernels(int JD, dense_kernel_t* f, dense_kernel_t* fr, dense_k
     case 1: *f = k_dense_forward<1>; *fr = k_dense_forward_relax<1>; *b = k_dense_backward<1>; *br = k_dense_backward_relax<1>; break;
     case 2: *f = k_dense_forward<2>; *fr = k_dense_forward_relax<2>; *b = k_dense_backward<2>; *br = k_dense_backward_relax<2>; break;
     case 4: *f = k_dense_forward<4>; *fr = k_dense_forward_relax<4>; *b = k_dense_backward<4>; *br = k_dense_backward_relax<4>; break;
-    default: *f = k_dense_forward<8>; *fr = k_dense_forward_relax<8>; *b = k_dense_backward<8>; *br = k_dense_backward_relax<8>; break;
+    case 8: *f = k_dense_forward<8>; *fr = k_dense_forward_relax<8>; *b = k_dense_backward<8>; *br = k_dense_backward_relax<8>; break;
+    default: *f = k_dense_forward<16>; *fr = k_dense_forward_relax<16>; *b = k_dense_backward<16>; *br = k_dense_backward_relax<16>; break;
   }
 }
 

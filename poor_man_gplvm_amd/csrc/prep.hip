@@ -195,6 +195,38 @@ __global__ void __launch_bounds__(256) k_rowref(const double* __restrict__ rblk,
   }
 }
 
+// rows of more than 64 blocks (L > 2048, the dense scans): one wave per (t, group) row,
+// KB blocks per lane (lane, lane + 64, ...)
+template <int KB>
+__global__ void __launch_bounds__(256) k_rowref_wide(const double* __restrict__ rblk, int64_t T, int nblk, int R,
+                                                     double s, float* __restrict__ phi, double* __restrict__ m) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int nb = nblk / R;
+  const bool rlive = row < T * R;
+  const int64_t t = !rlive ? 0 : R == 1 ? row : row / R;
+  const int g = rlive && R != 1 ? (int)(row - t * R) : 0;
+  const int64_t o0 = t * nblk + (int64_t)g * nb;
+  double v[KB], mx = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < KB; ++k) {
+    const int b = lane + 64 * k;
+    v[k] = rlive && b < nb ? rblk[o0 + b] : -INFINITY;
+    mx = fmax(mx, v[k]);
+  }
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) mx = fmax(mx, __shfl_xor(mx, d, 64));
+  if (mx == -INFINITY) mx = 0.0;
+  if (rlive) {
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      const int b = lane + 64 * k;
+      if (b < nb) phi[o0 + b] = (float)(s * (v[k] - mx));
+    }
+    if (lane == 0) m[row] = mx;
+  }
+}
+
 static void launch_rowref(const double* rblk, int64_t T, int nblk, int R, double s, float* phi, double* m,
                           hipStream_t st) {
   const int nb = nblk / R;
@@ -208,6 +240,7 @@ static void launch_rowref(const double* rblk, int64_t T, int nblk, int R, double
   }
   PMG_RR(1) PMG_RR(2) PMG_RR(4) PMG_RR(8) PMG_RR(16) PMG_RR(32) PMG_RR(64)
 #undef PMG_RR
+  hipLaunchKernelGGL(k_rowref_wide<2>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, rblk, T, nblk, R, s, phi, m);
 }
 
 __global__ void k_loglik(const float* __restrict__ delta, const double* __restrict__ rblk,
@@ -332,7 +365,7 @@ int pmg_tuning_softplus_batched(const float* basis, const double* W, int32_t L, 
 int pmg_emission_rowref(const double* rblk, int64_t T, int32_t nblk, double likelihood_scale,
                         float* phi, double* m, void* stream) {
   PMG_REQUIRE(T > 0 && nblk > 0 && rblk && phi && m, "pmg_emission_rowref: bad args");
-  PMG_REQUIRE(nblk <= 64, "pmg_emission_rowref: nblk=%d > 64", nblk);
+  PMG_REQUIRE(nblk <= 128, "pmg_emission_rowref: nblk=%d > 128 (L > 4096)", nblk);
   launch_rowref(rblk, T, nblk, 1, likelihood_scale, phi, m, as_stream(stream));
   PMG_LAUNCH_CHECK();
   return PMG_OK;
@@ -342,7 +375,7 @@ int pmg_emission_rowref_batched(const double* rblk, int64_t T, int32_t nblk, int
                                 float* phi, double* m, void* stream) {
   PMG_REQUIRE(T > 0 && nblk > 0 && R > 0 && nblk % R == 0 && rblk && phi && m,
               "pmg_emission_rowref_batched: bad args (nblk=%d, R=%d)", nblk, R);
-  PMG_REQUIRE(nblk / R <= 64, "pmg_emission_rowref_batched: %d blocks per restart > 64", nblk / R);
+  PMG_REQUIRE(nblk / R <= 128, "pmg_emission_rowref_batched: %d blocks per restart > 128", nblk / R);
   launch_rowref(rblk, T, nblk, R, likelihood_scale, phi, m, as_stream(stream));
   PMG_LAUNCH_CHECK();
   return PMG_OK;

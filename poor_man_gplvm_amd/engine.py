@@ -395,7 +395,7 @@ class DeviceEM:
         self.Cd = self.scan.chunk_dense_for(self.T)
         need = int(self.lib.pmg_dense_workspace_size(self.T, self.L, self.Cd))
         if need == 0:
-            raise nat.NativeError(f"n_latent_bin={self.L} unsupported by the dense scans (max 2048)")
+            raise nat.NativeError(f"n_latent_bin={self.L} unsupported by the dense scans (max 4096)")
         if self.ws_dense is None or self.ws_dense.numel() < need:
             # zero-filled: it holds the sticky relaxation timeout words (include/pmg.h)
             self.ws_dense = torch.zeros(need, dtype=torch.uint8, device=self.dev)

@@ -167,13 +167,14 @@ def test_decode_latent_outputs_finite_with_unvisited_bins():
         np.testing.assert_allclose(r[k], ref[k], rtol=1e-5, atol=1e-12, err_msg=k)
 
 
-def test_large_latent_count_vs_oracle():
+@pytest.mark.parametrize("L,T", [(1280, 200), (2600, 120)])
+def test_large_latent_count_vs_oracle(L, T):
     """n_latent_bin > 1024 (the reference scans any L, decoder.py:151-172): the banded
-    scans hold L <= 1024, so the model takes the dense log-domain scans with 8 latents per
-    thread (L <= 2048).  Decode (posterior, log marginal, one-step predictive) and one EM
-    iteration (tuning, posterior) against the f64 oracle."""
+    scans hold L <= 1024, so the model takes the dense log-domain scans with 8 (L <= 2048)
+    or 16 (L <= 4096) latents per thread.  Decode (posterior, log marginal, one-step
+    predictive) and one EM iteration (tuning, posterior) against the f64 oracle."""
     import poor_man_gplvm_amd as P
-    N, L, T = 24, 1280, 200
+    N = 24
     d = make(N, L, T)
     m = P.PoissonGPLVMJump1D(N, n_latent_bin=L, tuning_lengthscale=10.)
     from poor_man_gplvm_amd.gp_kernel import DenseTransition, dense_transition
