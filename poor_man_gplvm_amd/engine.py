@@ -490,18 +490,101 @@ class DeviceEM:
             raise ValueError(f"adam: W {tuple(W.shape)} / yw {tuple(yw.shape)} mismatch")
         tiled = (self.L > self.PERSISTENT_MAX_L or self.NB > self.PERSISTENT_MAX_NB
                  or not self.lib.pmg_mstep_adam_supported(self.L, self.NB, n))
+        if tiled:
+            blocks = self._adam_blocks(n)
+            if blocks is not None:
+                with self._t('mstep_adam'):     # one section per M-step, whatever the launches
+                    self._adam_blocked(W, mu, nu, count, cfg, stats_out, lh_out, eh_out, yw, blocks)
+                return
+        with self._t('mstep_adam'):
+            self._adam_launch(W, mu, nu, count, cfg, stats_out, lh_out, eh_out, yw, tiled)
+
+    # neuron blocks of the persistent kernel on one GPU (see _adam_blocked); False: the tiled
+    # kernels for every shape one launch cannot hold
+    ADAM_BLOCKED = True
+
+    def _adam_blocks(self, n):
+        """The fewest contiguous neuron blocks that the persistent kernel holds one launch
+        each, when all n neurons in one launch need more workgroups than there are CUs (e.g.
+        C4's N = L = 1024 on one GPU: 4 row blocks x 256 neuron groups); None if no split
+        up to 16 blocks fits or the shape is beyond the persistent kernel anyway."""
+        if (not self.ADAM_BLOCKED or self.L > self.PERSISTENT_MAX_L or self.NB > self.PERSISTENT_MAX_NB
+                or n < 2):
+            return None
+        from .timeshard import neuron_bounds
+        for k in range(2, min(16, n) + 1):
+            bounds = neuron_bounds(n, k)
+            if all(self.lib.pmg_mstep_adam_supported(self.L, self.NB, b - a) for a, b in bounds):
+                return bounds
+        return None
+
+    def _adam_blocked(self, W, mu, nu, count, cfg: AdamConfig, stats_out, lh_out, eh_out, yw, blocks):
+        """One Adam M-step as neuron blocks of the persistent kernel on this GPU: the
+        speculative loop of the neuron-sharded time shards (timeshard.speculative_adam:
+        16-body launches per block with the local stop rule off, the reference's stop rule
+        on the blocks' summed loss partials, replay up to the stopping body), with the blocks
+        in place of ranks.  The per-element arithmetic does not depend on the neuron
+        partition, so W, mu, nu equal one launch's (test_neuron_sharded_adam_bit_identical);
+        in place of the tiled f64 kernels (~97 us per body at C4) each body costs the blocks'
+        persistent bodies."""
+        from .timeshard import SPEC_BATCH, speculative_adam
+        mi = max(int(cfg.maxiter), 1)
+        sl = [dict(W=W[:, a:b].contiguous(), mu=mu[:, a:b].contiguous(), nu=nu[:, a:b].contiguous(),
+                   yw=yw[:, a:b].contiguous(), count=count.clone()) for a, b in blocks]
+        hl = max(mi, SPEC_BATCH + 1) + 1
+        hist = torch.zeros((len(sl), 4 + 2 * hl), dtype=torch.float64, device=self.dev)
+
+        def run(kmax):
+            c = AdamConfig(lr=cfg.lr, maxiter=kmax, tol=-1.0, prior_std=cfg.prior_std, b1=cfg.b1, b2=cfg.b2,
+                           eps=cfg.eps, eps_root=cfg.eps_root)
+            k = int(kmax)
+            if k > hl:
+                raise ValueError(f"blocked Adam launch of {k} bodies > history slots {hl}")
+            for i, d in enumerate(sl):
+                h = hist[i]
+                self._adam_launch(d['W'], d['mu'], d['nu'], d['count'], c, h[:4], h[4:4 + hl], h[4 + hl:],
+                                  d['yw'], False)
+            sel = torch.cat([hist[:, :1], hist[:, 4:4 + k], hist[:, 4 + hl:4 + hl + k]], dim=1).cpu().numpy()
+            return [(int(r[0]), r[1:1 + int(r[0])], r[1 + k:1 + k + int(r[0])]) for r in sel]
+
+        def snapshot():
+            return [(d['W'].clone(), d['mu'].clone(), d['nu'].clone(), d['count'].clone()) for d in sl]
+
+        def restore(snap):
+            for d, (w_, m_, v_, c_) in zip(sl, snap):
+                d['W'].copy_(w_)
+                d['mu'].copy_(m_)
+                d['nu'].copy_(v_)
+                d['count'].copy_(c_)
+
+        res = speculative_adam(run, snapshot, restore, lambda x: np.asarray(x, np.float64), int(cfg.maxiter),
+                               float(cfg.tol), batch=SPEC_BATCH)
+        for (a, b), d in zip(blocks, sl):
+            W[:, a:b].copy_(d['W'])
+            mu[:, a:b].copy_(d['mu'])
+            nu[:, a:b].copy_(d['nu'])
+        count.copy_(sl[0]['count'])
+        n = int(res['n_iter'])
+        stats_out.copy_(torch.tensor([n, res['final_loss'], res['final_error'], res['loss0']], dtype=torch.float64))
+        k = min(n, lh_out.shape[-1])
+        lh_out.zero_()
+        eh_out.zero_()
+        lh_out[:k].copy_(torch.as_tensor(res['loss_history'][:k]))
+        eh_out[:k].copy_(torch.as_tensor(res['error_history'][:k]))
+
+    def _adam_launch(self, W, mu, nu, count, cfg: AdamConfig, stats_out, lh_out, eh_out, yw, tiled):
+        n = int(W.shape[1])
         need = int(self.lib.pmg_mstep_tiled_workspace_size(self.L, self.NB, n) if tiled
                    else self.lib.pmg_mstep_workspace_size(n, int(cfg.maxiter)))
         ws = self.ws_ad.get(need, tiled)
         c = cfg.to_c()
         fn = self.lib.pmg_mstep_adam_tiled if tiled else self.lib.pmg_mstep_adam
-        with self._t('mstep_adam'):
-          nat.check(fn(nat.ptr(W), nat.ptr(mu), nat.ptr(nu), nat.ptr(count),
-                       nat.ptr(self.basis), nat.ptr(yw), nat.ptr(self.tw),
-                       self.L, self.NB, n, ctypes.byref(c), nat.ptr(stats_out),
-                       nat.ptr(lh_out), nat.ptr(eh_out), nat.ptr(ws),
-                       ws.numel(), nat.stream_handle()),
-                    "pmg_mstep_adam_tiled" if tiled else "pmg_mstep_adam")
+        nat.check(fn(nat.ptr(W), nat.ptr(mu), nat.ptr(nu), nat.ptr(count),
+                     nat.ptr(self.basis), nat.ptr(yw), nat.ptr(self.tw),
+                     self.L, self.NB, n, ctypes.byref(c), nat.ptr(stats_out),
+                     nat.ptr(lh_out), nat.ptr(eh_out), nat.ptr(ws),
+                     ws.numel(), nat.stream_handle()),
+                  "pmg_mstep_adam_tiled" if tiled else "pmg_mstep_adam")
 
     def compute_tuning(self, W):
         if self.noise_std is not None:

@@ -261,6 +261,8 @@ def test_c4_time_sharded_vs_single():
     # time-sharded: 8 shards of one recording
     lays = shard_layout(T, R, halo=512, scan=sc)
     eng = TimeShardedEM(y, B, tr, LocalComm(R), lays, sc)
+    for s_ in eng.shards:     # the replicated all-f64 tiled Adam on both sides (see e1 below)
+        s_.ADAM_BLOCKED = False
     for s in eng.shards:
         s.set_log_posterior(np.asarray(lp0[s.lay.ext_start:s.lay.ext_stop]))
     W, mu, nu, cnt, st, lh, eh, lz = fresh_state()
@@ -276,6 +278,12 @@ def test_c4_time_sharded_vs_single():
     torch.cuda.empty_cache()
     # unsharded
     e1 = DeviceEM(SpikeData(np.asarray(y[0:T])), L, basis=B, scan=sc)
+    # both sides run the replicated all-f64 tiled Adam kernels (N = 1024 does not fit one
+    # persistent launch; the default neuron-blocked persistent path is checked against the
+    # oracle in test_gpu_parity.py::test_adam_neuron_blocked_vs_oracle), so that the test
+    # compares the time sharding alone, as in rounds 3-5: after 150 bodies the f32-
+    # incremental persistent Adam sits ~1e-5 from the f64 one on this data
+    e1.ADAM_BLOCKED = False
     e1.adaptive = True
     e1.set_transition(tr)
     e1.set_log_posterior(np.asarray(lp0[0:T]))
@@ -284,9 +292,11 @@ def test_c4_time_sharded_vs_single():
     e1.compute_tuning(W)
     e1.e_step(1.0, lz)
     e1.check_status()
+    tun_rel = torch.max(torch.abs(tun_sh / e1.tuning64 - 1)).item()
+    print(f"C4 T=1e6, 8 shards vs one: tuning rel {tun_rel:.3e}")
     assert n_sh == int(st[0].item())
     assert abs(lz_sh - lz.item()) <= 1e-7 * abs(lz.item())
-    assert torch.max(torch.abs(tun_sh / e1.tuning64 - 1)).item() < 1e-5
+    assert tun_rel < 1e-5
     P1 = e1.P
     assert Psh.shape == P1.shape
     big = torch.maximum(Psh, P1)

@@ -434,6 +434,44 @@ def test_adam_vs_oracle(N, L, maxiter, tol, tiled):
     np.testing.assert_allclose(s[2], ref['final_error'], rtol=1e-5)
 
 
+@pytest.mark.parametrize("N,L,maxiter,tol", [(1100, 300, 200, 1e-6), (1024, 1024, 60, 0.0)])
+def test_adam_neuron_blocked_vs_oracle(N, L, maxiter, tol):
+    """Shapes whose one persistent launch would need more workgroups than CUs (C4's
+    N = L = 1024 on one GPU) run as neuron blocks of the persistent kernel with the
+    speculative stop rule (engine.DeviceEM._adam_blocked) instead of the tiled kernels:
+    identical n_iter, loss history rel 1e-7, tuning at RT against the f64 oracle, and the
+    Adam step count advanced as by one launch."""
+    from poor_man_gplvm_amd.engine import AdamConfig
+    d = make(N, L, 400)
+    sp, eng = _engine(d, L)
+    assert eng.lib.pmg_mstep_adam_supported(eng.L, eng.NB, N) == 0
+    blocks = eng._adam_blocks(N)
+    assert blocks is not None and len(blocks) >= 2 and blocks[-1][1] == N
+    yw, tw = O.get_statistics(d['lp0'].astype(np.float64), d['y'])
+    eng.yw.copy_(torch.as_tensor(yw, device='cuda'))
+    eng.tw.copy_(torch.as_tensor(tw, device='cuda'))
+    W = torch.as_tensor(d['W0'].astype(np.float64), device='cuda').contiguous()
+    mu, nu = torch.zeros_like(W), torch.zeros_like(W)
+    cnt = torch.zeros(1, dtype=torch.int64, device='cuda')
+    stats = torch.zeros(4, dtype=torch.float64, device='cuda')
+    lh = torch.zeros(max(maxiter, 1), dtype=torch.float64, device='cuda')
+    eh = torch.zeros_like(lh)
+    eng.adam(W, mu, nu, cnt, AdamConfig(maxiter=maxiter, tol=tol), stats, lh, eh)
+    eng.adam_status()
+    ref = O.adam_run(d['W0'].astype(np.float64), O.adam_init(d['W0']), 1.0, d['B'].astype(np.float64), yw, tw,
+                     maxiter=maxiter, tol=tol)
+    s = stats.cpu().numpy()
+    n = int(s[0])
+    assert n == ref['n_iter']
+    assert int(cnt.item()) == n - 1
+    B = d['B'].astype(np.float64)
+    np.testing.assert_allclose(np.logaddexp(B @ W.cpu().numpy(), 0), np.logaddexp(B @ ref['params'], 0), rtol=RT)
+    np.testing.assert_allclose(lh.cpu().numpy()[:n], ref['loss_history'][:n], rtol=1e-7)
+    np.testing.assert_allclose(eh.cpu().numpy()[:n], ref['error_history'][:n], rtol=1e-5)
+    np.testing.assert_allclose(s[1], ref['final_loss'], rtol=1e-7)
+    np.testing.assert_allclose(s[2], ref['final_error'], rtol=1e-5)
+
+
 def test_adam_c3_full_loop_vs_f64_ensemble():
     """The headline Adam instance (N = L = 512, NB = 79: k_adam<16,5,2>) over the whole
     reference loop (maxiter 1000, tol 1e-6; on these statistics it never stops early).
