@@ -10,12 +10,15 @@
 // Precision: the posterior depends on differences ll[t,l]-ll[t,l'] of sums of ~N
 // terms of size O(1-10); fp32 accumulation would cost ~1e-5 absolute.  The fast
 // path is therefore EXACT integer arithmetic: y (0..127) as int8 and log(lam) as a
-// 2^-32 fixed-point number split into 5 balanced base-256 int8 digits; the digit
-// GEMMs run on v_mfma_i32_32x32x32_i8 with exact int32 accumulation and are
-// recombined in int64 (quantisation error <= 2^-33 per log(lam), i.e. ll exact to
-// ~1e-9 for any realistic spike count).  Anything the integer path cannot represent
-// (non-integer / >127 counts, weighted or 2-D masks) goes through the f64 kernel at
-// the bottom.
+// 2^-32 fixed-point number split into kDig = 5 balanced base-256 int8 digits; the digit
+// GEMMs run on v_mfma_i32_32x32x32_i8 with exact int32 accumulation and are recombined
+// exactly in f64 (quantisation error <= 2^-33 per log(lam), i.e. ll exact to ~1e-9 for
+// any realistic spike count).  PMG_EMISSION_DIGITS=4 (A/B builds only) keeps 4 digits of
+// a 2^-24 fixed point: 2^-25 per log(lam) is a FIXED error per (l, n), so it adds up
+// coherently over a slowly mixing chain's memory (nearly flat tuning: 1.7e-5 relative on
+// the posterior, test_flat_tuning_cascade) -- not kept.  Anything the integer path
+// cannot represent (non-integer / >127 counts, weighted or 2-D masks) goes through the
+// f64 kernel at the bottom.
 //
 // Output format (both paths): delta[t,l] = f32(ll[t,l] - r[t,b]) with
 // r[t,b] = max over the 32-latent block b (f64), so an fp32 consumer recovers
@@ -33,11 +36,16 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
 
-constexpr int kDig = 5;
-constexpr double kQScale = 4294967296.0;  // 2^32
-constexpr double kQInv = 1.0 / 4294967296.0;
+#ifndef PMG_EMISSION_DIGITS
+#define PMG_EMISSION_DIGITS 5
+#endif
+constexpr int kDig = PMG_EMISSION_DIGITS;
+static_assert(kDig == 4 || kDig == 5, "4 or 5 digits");
+// 2^(8 (kDig - 1)): the top digit stays within int8 (|q| <= 61) for |log lam| < 60
+constexpr double kQScale = kDig == 5 ? 4294967296.0 : 16777216.0;
+constexpr double kQInv = 1.0 / kQScale;
 
-// One 4-wave workgroup per latent row: log(lam) -> 5 int8 digits, lamsum = sum_n m_n lam,
+// One 4-wave workgroup per latent row: log(lam) -> kDig int8 digits, lamsum = sum_n m_n lam,
 // and the pipelined kernel's per-latent constant lconst = -lamsum (+inf: latent masked by
 // ma_latent, -inf: padding row l >= L).  Wave w takes the neuron groups j = w, w + 4, ...
 // (neurons n = 64 j + lane); the products m_n lam pass through LDS so wave 0 adds each
@@ -58,7 +66,7 @@ __global__ void __launch_bounds__(256) k_rates_prepare(
   for (int jb = 0; jb < nj; jb += kRpBlk) {
     for (int j = jb + w; j < nj && j < jb + kRpBlk; j += 4) {
       const int n = 64 * j + lane;
-      int8_t dg[kDig] = {0, 0, 0, 0, 0};
+      int8_t dg[kDig] = {};
       double mlam = 0.0;
       if (l < L && n < N) {
         const double lam = tuning[(size_t)l * N + n] * dt + 1e-20;
@@ -99,7 +107,7 @@ __global__ void __launch_bounds__(256) k_rates_prepare(
 }
 
 // Workgroup tile 128 time bins x 64 latents, 8 waves as 4 (time) x 2 (latent); each
-// wave owns 32 t x 32 l for all 5 digits (5 v16i accumulators).  MFMA operand A = y
+// wave owns 32 t x 32 l for all kDig digits (kDig v16i accumulators).  MFMA operand A = y
 // (rows = time), B = digits (cols = latent), so C[t][l] rows leave as 128-byte
 // coalesced stores.  K (neurons) advances in 128-byte chunks staged through
 // double-buffered LDS (rows of 144 B: the 16-byte fragment reads of 16 consecutive
@@ -123,10 +131,10 @@ __device__ __forceinline__ int xcd_group(int bid, int nwg) {
 }
 
 // MT time fragments per wave: the workgroup tile is ET = 128 MT time bins x 64 latents and
-// each wave 32 MT t x 32 l (5 MT accumulators).  MT = 2 halves the digit planes' L2 -> LDS
+// each wave 32 MT t x 32 l (kDig MT accumulators).  MT = 2 halves the digit planes' L2 -> LDS
 // traffic per output (each plane chunk feeds twice the MFMAs) and the LDS reads per MFMA
 // (one B fragment per digit serves both A fragments): the digit planes are re-read once
-// per time tile, so their traffic is T / ET x 5 Lp Kp bytes.
+// per time tile, so their traffic is T / ET x kDig Lp Kp bytes.
 // MT = 1: 80 accumulator registers, <= 128 per lane so two workgroups share a CU (one's
 // epilogue beside the other's MFMAs); MT = 2: 160, one workgroup per CU.
 // LL: the f64 ll rows are written (exact decodes); the EM passes skip those stores.
@@ -283,7 +291,7 @@ __global__ void __launch_bounds__(512, MT == 1 ? 4 : 2) k_emission_i8(
 // K-chunk waited for its own L2 round trip behind a barrier, and the 128 x 64 tile
 // moved 350 B from L2 per MFMA).
 // - Tiles of 256 time bins x 64 latents (16 waves as 8 (time) x 2 (latent), each wave
-//   32 t x 32 l x 5 digits): 225 B of staged operands per MFMA.
+//   32 t x 32 l x kDig digits; 5 digits): 225 B of staged operands per MFMA.
 // - One 1024-thread workgroup per CU walks its own list of tiles (the 8 latent tiles of a
 //   time tile on one XCD, so y rows are re-read from that XCD's L2).  The operands of
 //   each 64-neuron chunk (y: 256 rows x 64 B, digits: 5 x 64 rows x 64 B = 36 KiB) stream
@@ -504,7 +512,7 @@ __global__ void __launch_bounds__(1024) k_emission_pipe(
 #pragma unroll
       for (int d = kDig - 2; d >= 0; --d) q = fma(q, 256.0, (double)acc[d][i]);
       const double gc = *reinterpret_cast<const double*>(cs + gco + ri * 8);
-      double v = q * kQInv + lc - gc;   // lc = -lamsum: (q/2^32 - lamsum) - gc as k_emission_i8
+      double v = q * kQInv + lc - gc;   // lc = -lamsum: (q / kQScale - lamsum) - gc as k_emission_i8
       v = v == INFINITY ? -1e20 : v;      // masked latent (lc = +inf); padding latents: -inf
       const double mx = (double)half_max32((float)v);
       const float dv = (float)(v - mx);
@@ -731,8 +739,10 @@ __global__ void __launch_bounds__(512) k_emission_yreg(
           // digit pairs combine exactly in int32 first (|a0 + 256 a1| < 2^31 for Kp <= 512)
           const int lo = acc[0][i] + (acc[1][i] << 8);
           const int mid = acc[2][i] + (acc[3][i] << 8);
-          const double q = fma(fma((double)acc[4][i], 65536.0, (double)mid), 65536.0, (double)lo);
-          double v = q * kQInv + lcg[e] - gcv;   // lc = -lamsum: (q/2^32 - lamsum) - gc
+          double q;
+          if constexpr (kDig == 5) q = fma(fma((double)acc[4][i], 65536.0, (double)mid), 65536.0, (double)lo);
+          else q = fma((double)mid, 65536.0, (double)lo);
+          double v = q * kQInv + lcg[e] - gcv;   // lc = -lamsum: (q / kQScale - lamsum) - gc
           if constexpr (MASK) v = v == INFINITY ? -1e20 : v;   // masked latent (lc = +inf)
           vv[i] = v;                                            // padding latents: lc = -inf
           fm = fmaxf(fm, (float)v);
