@@ -41,6 +41,9 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 #endif
 constexpr int kDig = PMG_EMISSION_DIGITS;
 static_assert(kDig == 4 || kDig == 5, "4 or 5 digits");
+#ifndef PMG_EMISSION_DIAG
+#define PMG_EMISSION_DIAG 0   // timing diagnostics of k_emission_yreg (A/B builds only)
+#endif
 // 2^(8 (kDig - 1)): the top digit stays within int8 (|q| <= 61) for |log lam| < 60
 constexpr double kQScale = kDig == 5 ? 4294967296.0 : 16777216.0;
 constexpr double kQInv = 1.0 / kQScale;
@@ -699,8 +702,14 @@ __global__ void __launch_bounds__(512) k_emission_yreg(
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int d = 0; d < kDig; ++d)
+        for (int d = 0; d < kDig; ++d) {
+#if PMG_EMISSION_DIAG == 2
+          // timing diagnostic (A/B builds only): the B reads without the MFMAs
+          acc[d][0] += bq[ks & 1][d][0] ^ ya[(CK / 32) * c + ks][1];
+#else
           acc[d] = __builtin_amdgcn_mfma_i32_32x32x32_i8(bq[ks & 1][d], ya[(CK / 32) * c + ks], acc[d], 0, 0, 0);
+#endif
+        }
         __builtin_amdgcn_sched_barrier(0);
         if (ks == 0) {
           // the next DMA behind the first k-step's MFMAs (their issue hides its SALU work)
@@ -711,6 +720,33 @@ __global__ void __launch_bounds__(512) k_emission_yreg(
       }
     }
 
+#if PMG_EMISSION_DIAG == 1
+    // timing diagnostic (A/B builds only, wrong results): the epilogue's stores without its
+    // arithmetic (same store count, so the counted vmcnt waits stay as in the real kernel)
+    {
+      const int nrow = (int)(T - t0 < RT ? T - t0 : RT);
+      const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(delta + t0 * (int64_t)L, (short)0,
+                                                                           nrow * L * 4, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(rblk + t0 * (int64_t)(Lp >> 5), (short)0,
+                                                                           nrow * (Lp >> 5) * 8, 0x00020000);
+      const int tr = 32 * wid + r;
+      int sacc = 0;
+#pragma unroll
+      for (int d = 0; d < kDig; ++d)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc += acc[d][i];
+      const uint32_t sv = (uint32_t)sacc;
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int lg = l0 + 8 * gq + 4 * h;
+        const uint32_t od = (tr < nrow && lg < L) ? (uint32_t)(tr * L + lg) * 4u : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128((v4u){sv, sv, sv, sv}, rd, od, 0, 0);
+      }
+      const uint32_t ob = (h == 0 && tr < nrow) ? (uint32_t)(tr * (Lp >> 5) + (l0 >> 5)) * 8u : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b64((u32x2){sv, sv}, rr, ob, 0, 0);
+    }
+    continue;
+#endif
     // epilogue (k_emission_i8's arithmetic) on the transposed tile: the MFMAs ran with the
     // operands swapped, so lane (r, h) holds time row t0 + 32 wid + r and, in register
     // i = 4 g + e, latent l0 + 8 g + 4 h + e.  The block max over the item's 32 latents is
