@@ -706,6 +706,9 @@ __global__ void __launch_bounds__(512) k_emission_yreg(
 #if PMG_EMISSION_DIAG == 2
           // timing diagnostic (A/B builds only): the B reads without the MFMAs
           acc[d][0] += bq[ks & 1][d][0] ^ ya[(CK / 32) * c + ks][1];
+#elif PMG_EMISSION_DIAG == 3
+          // timing diagnostic (A/B builds only): neither the B reads nor the MFMAs
+          acc[d][0] += ya[(CK / 32) * c + ks][1] + d;
 #else
           acc[d] = __builtin_amdgcn_mfma_i32_32x32x32_i8(bq[ks & 1][d], ya[(CK / 32) * c + ks], acc[d], 0, 0, 0);
 #endif
