@@ -574,6 +574,86 @@ template <int CK> struct YRing {
   static constexpr int NSEG = CK / 16;                   // 16-B segments per row
 };
 
+// The epilogue of one 256 x 32 work item of k_emission_yreg (k_emission_i8's
+// arithmetic) on the transposed tile: the MFMAs ran with the digit planes as the A operand, so
+// lane (r, h) holds time row t0 + tr (tr = 32 wid + r) and, in register i = 4 g + e, latent
+// l0 + 8 g + 4 h + e.  The block max over the item's 32 latents is a register max plus one
+// half-wave swap, each group of 4 latents one 16-B delta store (and two of ll64).  Returns
+// the block max (the caller writes rblk).
+template <bool LL, bool MASK>
+__device__ __forceinline__ double item_rows(const v16i (&acc)[kDig], const double* __restrict__ slc, int l0,
+                                            int64_t t0, int64_t T, int L, int tr, int h, double gcv,
+                                            float* __restrict__ delta, double* __restrict__ ll64) {
+  const int nrow = (int)(T - t0 < RT ? T - t0 : RT);
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(delta + t0 * (int64_t)L, (short)0,
+                                                                       nrow * L * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+      LL ? (void*)(ll64 + t0 * (int64_t)L) : (void*)delta, (short)0, LL ? nrow * L * 8 : 0, 0x00020000);
+  const bool tvalid = tr < nrow;
+  double vv[16];
+  float fm = -INFINITY;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const double* lcg = slc + l0 + 8 * g + 4 * h;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int i = 4 * g + e;
+      // digit pairs combine exactly in int32 first (|a0 + 256 a1| < 2^31 for Kp <= 512)
+      const int lo = acc[0][i] + (acc[1][i] << 8);
+      const int mid = acc[2][i] + (acc[3][i] << 8);
+      double q;
+      if constexpr (kDig == 5) q = fma(fma((double)acc[4][i], 65536.0, (double)mid), 65536.0, (double)lo);
+      else q = fma((double)mid, 65536.0, (double)lo);
+      double v = q * kQInv + lcg[e] - gcv;   // lc = -lamsum: (q / kQScale - lamsum) - gc
+      if constexpr (MASK) v = v == INFINITY ? -1e20 : v;   // masked latent (lc = +inf)
+      vv[i] = v;                                            // padding latents: lc = -inf
+      fm = fmaxf(fm, (float)v);
+    }
+  }
+  {
+    const auto pr = __builtin_amdgcn_permlane32_swap(__float_as_int(fm), __float_as_int(fm), false, false);
+    fm = fmaxf(__int_as_float((int)pr[0]), __int_as_float((int)pr[1]));
+  }
+  const double mx = (double)fm;
+  const bool vec4 = (L & 3) == 0;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int lg = l0 + 8 * g + 4 * h;
+    float dv[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dv[e] = (float)(vv[4 * g + e] - mx);
+    if (vec4) {
+      const uint32_t od = (tvalid && lg < L) ? (uint32_t)(tr * L + lg) * 4u : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b128(
+          (v4u){__float_as_uint(dv[0]), __float_as_uint(dv[1]), __float_as_uint(dv[2]), __float_as_uint(dv[3])},
+          rd, od, 0, 0);
+      if constexpr (LL) {
+        const uint32_t ol = (tvalid && lg < L) ? (uint32_t)(tr * L + lg) * 8u : 0x80000000u;
+        const unsigned long long a0 = __double_as_longlong(vv[4 * g]), a1 = __double_as_longlong(vv[4 * g + 1]);
+        const unsigned long long a2 = __double_as_longlong(vv[4 * g + 2]), a3 = __double_as_longlong(vv[4 * g + 3]);
+        __builtin_amdgcn_raw_buffer_store_b128(
+            (v4u){(uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32)}, rl, ol, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(
+            (v4u){(uint32_t)a2, (uint32_t)(a2 >> 32), (uint32_t)a3, (uint32_t)(a3 >> 32)}, rl,
+            ol == 0x80000000u ? ol : ol + 16u, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool ok = tvalid && lg + e < L;
+        const uint32_t od = ok ? (uint32_t)(tr * L + lg + e) * 4u : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dv[e]), rd, od, 0, 0);
+        if constexpr (LL) {
+          const uint32_t ol = ok ? (uint32_t)(tr * L + lg + e) * 8u : 0x80000000u;
+          const unsigned long long vu = __double_as_longlong(vv[4 * g + e]);
+          __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)vu, (uint32_t)(vu >> 32)}, rl, ol, 0, 0);
+        }
+      }
+    }
+  }
+  return mx;
+}
+
 template <int CK, int KC, bool LL, bool MASK>
 __global__ void __launch_bounds__(512) k_emission_yreg(
     const int8_t* __restrict__ yq, const int8_t* __restrict__ qd, const double* __restrict__ lconst,
@@ -750,84 +830,17 @@ __global__ void __launch_bounds__(512) k_emission_yreg(
     }
     continue;
 #endif
-    // epilogue (k_emission_i8's arithmetic) on the transposed tile: the MFMAs ran with the
-    // operands swapped, so lane (r, h) holds time row t0 + 32 wid + r and, in register
-    // i = 4 g + e, latent l0 + 8 g + 4 h + e.  The block max over the item's 32 latents is
-    // a register max plus one half-wave swap, and each group of 4 latents one 16-B store.
+    // epilogue (item_rows), then the item's block maxima
     {
       const int nblk = Lp >> 5;
       const int blk = l0 >> 5;
       const int64_t nrow64 = T - t0 < RT ? T - t0 : RT;
       const int nrow = (int)nrow64;
-      const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(delta + t0 * (int64_t)L, (short)0,
-                                                                           nrow * L * 4, 0x00020000);
       const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(rblk + t0 * (int64_t)nblk, (short)0,
                                                                            nrow * nblk * 8, 0x00020000);
-      const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
-          LL ? (void*)(ll64 + t0 * (int64_t)L) : (void*)delta, (short)0, LL ? nrow * L * 8 : 0, 0x00020000);
       const int tr = 32 * wid + r;
       const bool tvalid = tr < nrow;
-      double vv[16];
-      float fm = -INFINITY;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const double* lcg = slc + l0 + 8 * g + 4 * h;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = 4 * g + e;
-          // digit pairs combine exactly in int32 first (|a0 + 256 a1| < 2^31 for Kp <= 512)
-          const int lo = acc[0][i] + (acc[1][i] << 8);
-          const int mid = acc[2][i] + (acc[3][i] << 8);
-          double q;
-          if constexpr (kDig == 5) q = fma(fma((double)acc[4][i], 65536.0, (double)mid), 65536.0, (double)lo);
-          else q = fma((double)mid, 65536.0, (double)lo);
-          double v = q * kQInv + lcg[e] - gcv;   // lc = -lamsum: (q / kQScale - lamsum) - gc
-          if constexpr (MASK) v = v == INFINITY ? -1e20 : v;   // masked latent (lc = +inf)
-          vv[i] = v;                                            // padding latents: lc = -inf
-          fm = fmaxf(fm, (float)v);
-        }
-      }
-      {
-        const auto pr = __builtin_amdgcn_permlane32_swap(__float_as_int(fm), __float_as_int(fm), false, false);
-        fm = fmaxf(__int_as_float((int)pr[0]), __int_as_float((int)pr[1]));
-      }
-      const double mx = (double)fm;
-      const bool vec4 = (L & 3) == 0;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int lg = l0 + 8 * g + 4 * h;
-        float dv[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) dv[e] = (float)(vv[4 * g + e] - mx);
-        if (vec4) {
-          const uint32_t od = (tvalid && lg < L) ? (uint32_t)(tr * L + lg) * 4u : 0x80000000u;
-          __builtin_amdgcn_raw_buffer_store_b128(
-              (v4u){__float_as_uint(dv[0]), __float_as_uint(dv[1]), __float_as_uint(dv[2]), __float_as_uint(dv[3])},
-              rd, od, 0, 0);
-          if constexpr (LL) {
-            const uint32_t ol = (tvalid && lg < L) ? (uint32_t)(tr * L + lg) * 8u : 0x80000000u;
-            const unsigned long long a0 = __double_as_longlong(vv[4 * g]), a1 = __double_as_longlong(vv[4 * g + 1]);
-            const unsigned long long a2 = __double_as_longlong(vv[4 * g + 2]), a3 = __double_as_longlong(vv[4 * g + 3]);
-            __builtin_amdgcn_raw_buffer_store_b128(
-                (v4u){(uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32)}, rl, ol, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b128(
-                (v4u){(uint32_t)a2, (uint32_t)(a2 >> 32), (uint32_t)a3, (uint32_t)(a3 >> 32)}, rl,
-                ol == 0x80000000u ? ol : ol + 16u, 0, 0);
-          }
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const bool ok = tvalid && lg + e < L;
-            const uint32_t od = ok ? (uint32_t)(tr * L + lg + e) * 4u : 0x80000000u;
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dv[e]), rd, od, 0, 0);
-            if constexpr (LL) {
-              const uint32_t ol = ok ? (uint32_t)(tr * L + lg + e) * 8u : 0x80000000u;
-              const unsigned long long vu = __double_as_longlong(vv[4 * g + e]);
-              __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)vu, (uint32_t)(vu >> 32)}, rl, ol, 0, 0);
-            }
-          }
-        }
-      }
+      const double mx = item_rows<LL, MASK>(acc, slc, l0, t0, T, L, tr, h, gcv, delta, ll64);
       const unsigned long long mu = (unsigned long long)__double_as_longlong(mx);
 #if PMG_RBLK_PAIRS
       // rblk in runs of up to kRbRun blocks: a block whose successor is this workgroup's next
