@@ -502,6 +502,9 @@ class DeviceEM:
     # neuron blocks of the persistent kernel on one GPU (see _adam_blocked); False: the tiled
     # kernels for every shape one launch cannot hold
     ADAM_BLOCKED = True
+    # the blocked loop's launches double from 16 up to this many bodies: each launch round
+    # trip (host stop rule, snapshot) costs ~0.8 ms at C4 against ~34 us per body of kernel
+    ADAM_BLOCKED_MAX_BATCH = 64
 
     def _adam_blocks(self, n):
         """The fewest contiguous neuron blocks that the persistent kernel holds one launch
@@ -521,7 +524,8 @@ class DeviceEM:
     def _adam_blocked(self, W, mu, nu, count, cfg: AdamConfig, stats_out, lh_out, eh_out, yw, blocks):
         """One Adam M-step as neuron blocks of the persistent kernel on this GPU: the
         speculative loop of the neuron-sharded time shards (timeshard.speculative_adam:
-        16-body launches per block with the local stop rule off, the reference's stop rule
+        launches of 16, 32, then 64 bodies per block (ADAM_BLOCKED_MAX_BATCH) with the local
+        stop rule off, one snapshot copy per launch round, the reference's stop rule
         on the blocks' summed loss partials, replay up to the stopping body), with the blocks
         in place of ranks.  The per-element arithmetic does not depend on the neuron
         partition, so W, mu, nu equal one launch's (test_neuron_sharded_adam_bit_identical);
@@ -529,9 +533,23 @@ class DeviceEM:
         persistent bodies."""
         from .timeshard import SPEC_BATCH, speculative_adam
         mi = max(int(cfg.maxiter), 1)
-        sl = [dict(W=W[:, a:b].contiguous(), mu=mu[:, a:b].contiguous(), nu=nu[:, a:b].contiguous(),
-                   yw=yw[:, a:b].contiguous(), count=count.clone()) for a, b in blocks]
-        hl = max(mi, SPEC_BATCH + 1) + 1
+        mb = self.ADAM_BLOCKED_MAX_BATCH
+        # every block's (W, mu, nu) as views of ONE flat buffer and the counts of one tensor,
+        # so a snapshot / restore is one copy each (not four per block)
+        NB = W.shape[0]
+        flat = torch.empty(3 * NB * W.shape[1], dtype=W.dtype, device=W.device)
+        cnts = count.repeat(len(blocks)).contiguous()
+        sl, off = [], 0
+        for i, (a, b) in enumerate(blocks):
+            n_b = NB * (b - a)
+            d = dict(yw=yw[:, a:b].contiguous(), count=cnts[i:i + 1])
+            for k, src in (('W', W), ('mu', mu), ('nu', nu)):
+                v = flat[off:off + n_b].view(NB, b - a)
+                v.copy_(src[:, a:b])
+                d[k] = v
+                off += n_b
+            sl.append(d)
+        hl = max(mi, mb + 1) + 1
         hist = torch.zeros((len(sl), 4 + 2 * hl), dtype=torch.float64, device=self.dev)
 
         def run(kmax):
@@ -548,17 +566,14 @@ class DeviceEM:
             return [(int(r[0]), r[1:1 + int(r[0])], r[1 + k:1 + k + int(r[0])]) for r in sel]
 
         def snapshot():
-            return [(d['W'].clone(), d['mu'].clone(), d['nu'].clone(), d['count'].clone()) for d in sl]
+            return flat.clone(), cnts.clone()
 
         def restore(snap):
-            for d, (w_, m_, v_, c_) in zip(sl, snap):
-                d['W'].copy_(w_)
-                d['mu'].copy_(m_)
-                d['nu'].copy_(v_)
-                d['count'].copy_(c_)
+            flat.copy_(snap[0])
+            cnts.copy_(snap[1])
 
         res = speculative_adam(run, snapshot, restore, lambda x: np.asarray(x, np.float64), int(cfg.maxiter),
-                               float(cfg.tol), batch=SPEC_BATCH)
+                               float(cfg.tol), batch=SPEC_BATCH, max_batch=mb)
         for (a, b), d in zip(blocks, sl):
             W[:, a:b].copy_(d['W'])
             mu[:, a:b].copy_(d['mu'])

@@ -285,7 +285,7 @@ def adam_stop_body(losses, j0, maxiter, tol, state):
 SPEC_BATCH = 16     # bodies per speculative launch of the neuron-sharded Adam (the exact-F refresh period)
 
 
-def speculative_adam(run, snapshot, restore, allreduce, maxiter, tol, batch=SPEC_BATCH):
+def speculative_adam(run, snapshot, restore, allreduce, maxiter, tol, batch=SPEC_BATCH, max_batch=None):
     """Neuron-sharded Adam loop with the reference's global stop rule.
 
     Every rank runs its own neuron slice (the loss and the gradient norm are sums over
@@ -300,6 +300,9 @@ def speculative_adam(run, snapshot, restore, allreduce, maxiter, tol, batch=SPEC
                    (the kernel's outputs for maxiter = kmax, tol < 0)
       snapshot() / restore(): all local slices' (W, mu, nu, count)
       allreduce(x) -> sum over ranks of the local sum x (host float64 arrays)
+    max_batch: the launches double from `batch` up to max_batch bodies (multiples of
+    `batch`, so every launch still starts on a refresh body): fewer host round trips for
+    long loops, at the price of up to max_batch - 1 speculative bodies past the stop.
     Returns dict(n_iter, final_loss, final_error, loss_history, error_history, loss0)."""
     if maxiter <= 1:   # eval only: the loss at W_0, no update
         outs = run(1)
@@ -307,12 +310,14 @@ def speculative_adam(run, snapshot, restore, allreduce, maxiter, tol, batch=SPEC
         g = allreduce(loc)
         return dict(n_iter=1, final_loss=float(g[0]), final_error=float(np.sqrt(g[1])),
                     loss_history=np.array([g[0]]), error_history=np.array([np.sqrt(g[1])]), loss0=float(g[0]))
+    mb = batch if max_batch is None else max(batch, (int(max_batch) // batch) * batch)
     j0, st = 0, {}
     lh, eh = [], []
+    cur = batch
     while True:
         snap = snapshot()
-        outs = run(batch + 1)
-        nb = int(outs[0][0]) - 1                        # bodies this launch ran: exactly `batch` (tol < 0)
+        outs = run(cur + 1)
+        nb = int(outs[0][0]) - 1                        # bodies this launch ran: exactly `cur` (tol < 0)
         if any(int(o[0]) - 1 != nb for o in outs):
             raise RuntimeError("speculative_adam: local slices ran different body counts")
         loc = np.zeros((2, nb))
@@ -334,6 +339,7 @@ def speculative_adam(run, snapshot, restore, allreduce, maxiter, tol, batch=SPEC
             return dict(n_iter=j + 2, final_loss=float(lh[-1]), final_error=float(eh[-1]),
                         loss_history=hist_l, error_history=hist_e, loss0=float(lh[0]))
         j0 += nb
+        cur = min(2 * cur, mb)
 
 
 # --------------------------------------------------------------------------- shard

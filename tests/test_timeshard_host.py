@@ -134,9 +134,10 @@ def _kernel_mimic(W, mu, nu, count, kmax, tol, a, c, lr=0.01, b1=0.9, b2=0.999, 
             return j + 2, np.array([lh[0]] + lh), np.array([eh[0]] + eh)
 
 
+@pytest.mark.parametrize("max_batch", [None, 64])
 @pytest.mark.parametrize("maxiter,tol,world", [(1000, 1e-6, 3), (40, 0.0, 2), (23, 0.0, 4), (1, 1e-6, 2),
-                                               (7, 1e-6, 3)])
-def test_speculative_adam_matches_unsharded(maxiter, tol, world):
+                                               (7, 1e-6, 3), (150, 0.0, 2)])
+def test_speculative_adam_matches_unsharded(maxiter, tol, world, max_batch):
     from poor_man_gplvm_amd.timeshard import neuron_bounds, speculative_adam
     rng = np.random.default_rng(0)
     N = 37
@@ -161,7 +162,7 @@ def test_speculative_adam_matches_unsharded(maxiter, tol, world):
         for d, (w, m, v, k) in zip(sl, snap):
             d['W'][:], d['mu'][:], d['nu'][:], d['cnt'][:] = w, m, v, k
 
-    res = speculative_adam(run, snapshot, restore, lambda x: x, maxiter, tol)
+    res = speculative_adam(run, snapshot, restore, lambda x: x, maxiter, tol, max_batch=max_batch)
     assert res['n_iter'] == n_ref
     np.testing.assert_array_equal(np.concatenate([d['W'] for d in sl]), W)
     assert all(d['cnt'][0] == cnt[0] for d in sl)
