@@ -27,4 +27,6 @@ for _ in range(200):
     call()
 b.record()
 b.synchronize()
-print(os.environ.get('PMG_LIB_PATH', 'tree'), 'us per call', round(1e3 * a.elapsed_time(b) / 200, 2), 'sum', float(t64.sum()))
+import hashlib  # noqa: E402
+print(os.environ.get('PMG_LIB_PATH', 'tree'), 'us per call', round(1e3 * a.elapsed_time(b) / 200, 2), 'sum', float(t64.sum()),
+      'sha', hashlib.sha256(t64.cpu().numpy().tobytes() + t32.cpu().numpy().tobytes()).hexdigest()[:16])
